@@ -1,0 +1,233 @@
+/*
+ * vaeunet.h — C-ABI of the MI355X-native VAE-U-Net training hot path.
+ *
+ * The reference (tmuird/VAEUNET) is pure Python on PyTorch: its "plugin API"
+ * is torch.nn.Module + autograd, and the device work it reaches is ATen
+ * (SURVEY.md §2b).  This library replaces those ATen calls on the hot path
+ * (SURVEY.md §8a rows A-Q).  Every entry point takes plain device pointers,
+ * sizes and a hipStream_t (passed as void*), launches asynchronously on that
+ * stream and returns 0 or a hipError_t code.  No torch types cross this
+ * boundary; the Python host side (vaeunet_amd/_lib.py) binds it with ctypes,
+ * which is how a Python reference would bind any C library
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   dtype   : 0 = fp32 (parity mode), 1 = bf16 (autocast / speed mode)
+ *   layout  : activations are NHWC with a pixel stride (elements) so that a
+ *             channel slice of a wider tensor can be addressed in place
+ *             (torch channels_last tensors are exactly this).
+ *   stats   : BatchNorm partial statistics are (sum, centered M2) per
+ *             (row-tile, channel); they are combined in fp64 with Chan's
+ *             formula, in a fixed order (bitwise reproducible).
+ */
+#ifndef VAEUNET_H
+#define VAEUNET_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Implicit-GEMM operand: element [m][k] of a (virtual) im2col matrix.
+ * m = (n*H + h)*W + w over the row grid, k = (r*S + s)*C + c over taps and
+ * channels.  The source pixel is (h*sy + r*dy + oy, w*sx + s*dx + ox) in a
+ * (Hs, Ws) image; out-of-range pixels read as 0 (zero padding).  Channel c
+ * comes from source t where cend[t-1] <= c < cend[t] (channel concat,
+ * unet_parts.py:94 / unet_resnet.py:98 never materialised).
+ *   3x3 conv fwd (unet_parts.py:40,43): R=S=3, sy=sx=dy=dx=1, oy=ox=-1
+ *   1x1 conv     (unet_parts.py:11,15,19,100): R=S=1, oy=ox=0
+ *   ConvT 2x2 s2 input-grad gather (unet_parts.py:76): R=S=2, sy=sx=2 */
+typedef struct VuGather {
+  const void* src[3];
+  int64_t stride[3];   /* pixel stride of each source, elements */
+  int32_t cend[3];     /* cumulative channel end of each source */
+  int32_t nsrc;
+  int32_t C;           /* channels per tap (== cend[nsrc-1]) */
+  int32_t N, H, W;     /* row grid */
+  int32_t Hs, Ws;      /* source image */
+  int32_t R, S;        /* taps */
+  int32_t sy, sx, dy, dx, oy, ox;
+} VuGather;
+
+/* out[m][j] = sum_k A[m][k] * B[j][k] (+ bias), B dense [ncol][ldb].
+ * out_mode 0: out[m*out_stride + out_coff + j]
+ * out_mode 1: ConvTranspose 2x2/s2 pixel shuffle, j = (a*2+b)*cout + co ->
+ *             out pixel (n, 2h+a+opy, 2w+b+opx) of an (oH, oW) image.
+ * stat_sum/stat_m2 (optional): per (row tile, column) sum and centered M2 of
+ * the stored (dtype-rounded) values, for BatchNorm (unet_parts.py:41,44). */
+typedef struct VuGemmFwd {
+  VuGather a;
+  const void* b;
+  int64_t ldb;
+  int32_t ncol;
+  int32_t out_mode;
+  void* out;
+  int64_t out_stride;
+  int32_t out_coff;
+  int32_t oH, oW, opy, opx, cout;
+  const float* bias;
+  float* stat_sum;
+  float* stat_m2;
+  int32_t accumulate;  /* out += result (gradient accumulation) */
+} VuGemmFwd;
+
+/* Weight-gradient GEMM: out[s][i][j] = sum_{m in split s} P[m][i] * Q[m][j]
+ * (fp32 slabs, one per split of the m range; reduced by vu_slab_reduce). */
+typedef struct VuGemmWgrad {
+  VuGather p;
+  VuGather q;
+  int32_t ni, nj;
+  int32_t splits;
+  int64_t m_per_split;
+  float* out;
+} VuGemmWgrad;
+
+/* ---- GEMM family ------------------------------------------------------ */
+int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream);
+int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype);  /* BM used */
+int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream);
+/* out[i*s_i + (j / C)*s_tap + (j % C)*s_c] (=|+=) sum_s slab[s][i][j],
+ * skipping channels (j % C) >= cvalid (zero-padded input channels) */
+int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
+                   int cvalid, int64_t s_i, int64_t s_tap, int64_t s_c,
+                   float* out, int accumulate, void* stream);
+
+/* ---- weights ----------------------------------------------------------- */
+/* out[i0][i1][i2][i3] (contiguous) = in[base + i0*s0 + i1*s1 + i2*s2 + i3*s3]
+ * for i3 < d3v, 0 for d3v <= i3 < d3 (channel padding of the 3-channel input
+ * layer); strides may be negative (flipped taps of the input-gradient
+ * weights). */
+int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1,
+                int64_t s2, int64_t s3, int d0, int d1, int d2, int d3,
+                int d3v, void* out, int dtype, void* stream);
+
+/* ---- BatchNorm (nn.BatchNorm2d train mode, unet_parts.py:41,44) -------- */
+/* combine per-tile (sum, M2) partials; counts: tile t has
+ * min(tile_rows, rows - t*tile_rows) rows.  Writes scale/shift (y*scale+shift
+ * is the affine-normalised value), save_mean/save_invstd and updates running
+ * stats in place (momentum, unbiased variance), like F.batch_norm. */
+int vu_bn_finalize(const float* psum, const float* pm2, int tiles,
+                   int64_t tile_rows, int64_t rows, int C,
+                   const float* gamma, const float* beta,
+                   float* running_mean, float* running_var, float momentum,
+                   float eps, float* scale, float* shift, float* save_mean,
+                   float* save_invstd, int64_t* num_batches_tracked,
+                   float* workspace, void* stream);
+/* eval mode: scale/shift from running statistics */
+int vu_bn_eval_coeffs(const float* gamma, const float* beta,
+                      const float* running_mean, const float* running_var,
+                      float eps, int C, float* scale, float* shift, void* stream);
+/* y = max(0, x*scale[c] + shift[c]) (relu=1) or x*scale+shift (relu=0) */
+int vu_bn_apply(const void* x, int64_t x_stride, void* y, int64_t y_stride,
+                int64_t P, int C, const float* scale, const float* shift,
+                int relu, int dtype, void* stream);
+/* Backward of y = relu(x*scale+shift): per-channel sums of dz and dz*xhat,
+ * dz = dy * (z > 0).  Writes dgamma, dbeta (accumulate flag) and the
+ * coefficients (k1, k2, k3) with dx = k1*dz + k2*(x - mean) + k3. */
+int vu_bn_bwd_reduce(const void* dy, int64_t dy_stride, const void* x,
+                     int64_t x_stride, int64_t P, int C, const float* scale,
+                     const float* shift, const float* mean,
+                     const float* invstd, const float* gamma, int relu,
+                     float* dgamma, float* dbeta, int accumulate,
+                     float* coef, float* workspace, int dtype, void* stream);
+/* dx = k1*dz + k2*(x-mean) + k3 (+ add) */
+int vu_bn_bwd_apply(const void* dy, int64_t dy_stride, const void* x,
+                    int64_t x_stride, int64_t P, int C, const float* scale,
+                    const float* shift, const float* mean, const float* coef,
+                    int relu, void* dx, int64_t dx_stride, int dtype,
+                    void* stream);
+
+/* ---- per-channel reductions / elementwise ------------------------------ */
+/* out[c] (=|+=) sum over the pixels of the (Hr, Wr) window at (y0, x0) of
+ * every (H, W) image of x[pix*stride + c]  (bias gradients) */
+int vu_chan_sum(const void* x, int64_t stride, int N, int H, int W, int y0,
+                int x0, int Hr, int Wr, int C, float* out, int accumulate,
+                float* workspace, int dtype, void* stream);
+int64_t vu_reduce_workspace_bytes(int64_t P, int C);
+int64_t vu_bn_finalize_workspace_bytes(int tiles, int C);
+/* generic NHWC copy/cast: y[p*ys + c] = x[p*xs + c] (+ y if accumulate) */
+int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys,
+            int ydtype, int64_t P, int C, int accumulate, void* stream);
+/* NCHW/NHWC fp32 input -> NHWC storage padded to Cp channels (zeros) */
+int vu_input_pack(const float* x, int64_t sn, int64_t sc, int64_t sh,
+                  int64_t sw, int N, int C, int H, int W, int Cp, void* y,
+                  int dtype, void* stream);
+
+/* ---- pooling / resampling (unet_parts.py:57,73,85-89) ------------------ */
+int vu_maxpool2_fwd(const void* x, int64_t xs, int N, int H, int W, int C,
+                    void* y, int64_t ys, int dtype, void* stream);
+/* dx (over the full HxW input) = routed dy (first max wins) [+ add] */
+int vu_maxpool2_bwd(const void* x, int64_t xs, const void* dy, int64_t dys,
+                    int N, int H, int W, int C, void* dx, int64_t dxs,
+                    const void* add, int64_t adds, int dtype, void* stream);
+/* bilinear, align_corners=True, (Hi,Wi) -> (Ho,Wo) placed at (py,px) inside
+ * a zero (Hp,Wp) canvas (F.pad of unet_parts.py:88-89 folded in). */
+int vu_upsample_fwd(const void* x, int64_t xs, int N, int Hi, int Wi, int C,
+                    void* y, int64_t ys, int Ho, int Wo, int Hp, int Wp,
+                    int py, int px, int dtype, void* stream);
+/* transposed gather (no atomics): dx[n,i,j] = sum over the output pixels
+ * whose stencil touches (i,j). */
+int vu_upsample_bwd(const void* dy, int64_t dys, int N, int Hi, int Wi, int C,
+                    void* dx, int64_t dxs, int Ho, int Wo, int Hp, int Wp,
+                    int py, int px, int accumulate, int dtype, void* stream);
+
+/* ---- attention gate (unet_parts.py:7-30) ------------------------------- */
+/* q[p] = bpsi + sum_c wpsi[c] * relu(ug[p,c]*sg[c]+tg[c] + ux[p,c]*sx[c]+tx[c])
+ * plus per-tile (sum, M2) of q for BatchNorm2d(1). */
+int vu_attn_psi_fwd(const void* ug, const void* ux, int64_t P, int F,
+                    const float* sg, const float* tg, const float* sx,
+                    const float* tx, const float* wpsi, const float* bpsi,
+                    float* q, float* psum, float* pm2, int64_t tile_rows,
+                    int dtype, void* stream);
+/* p = sigmoid(q*s + t); out[p,c] = x[p,c] * p  (also stores p) */
+int vu_attn_gate_fwd(const float* q, const float* st, const void* x,
+                     int64_t xs, int64_t P, int C, float* pmap, void* out,
+                     int64_t os, int dtype, void* stream);
+/* backward of out = x*p: dx_direct = dout*p (written to dx), and
+ * dq_pre[p] = (sum_c dout*x) * p * (1-p)  (grad w.r.t. the BN(1) output) */
+int vu_attn_gate_bwd(const void* dout, int64_t dos, const void* x, int64_t xs,
+                     const float* pmap, int64_t P, int C, void* dx,
+                     int64_t dxs, float* dqpre, int dtype, void* stream);
+/* backward through psi conv + relu: given dq[p] (grad of q), produce
+ * ds[p,c] = dq[p]*wpsi[c]*(s>0) as bf16/fp32 for both BN branches (same
+ * tensor), dwpsi[c] partials and dbpsi. */
+int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F,
+                    const float* sg, const float* tg, const float* sx,
+                    const float* tx, const float* wpsi, const float* dq,
+                    void* ds, float* dwpsi, float* dbpsi, int accumulate,
+                    float* workspace, int dtype, void* stream);
+
+/* ---- 1x1 conv with a tiny output (OutConv, psi) ------------------------- */
+/* y[p*ys + j] = b[j] + sum_c x[p*xs+c] w[j*C+c], j < J <= 4, y fp32 */
+int vu_pointwise_fwd(const void* x, int64_t xs, int64_t P, int C, int J,
+                     const float* w, const float* b, float* y, int64_t ys,
+                     int dtype, void* stream);
+/* dx[p,c] = sum_j dy[p,j] w[j,c];  dw[j,c] += sum_p dy x;  db[j] += sum_p dy */
+int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int64_t dys,
+                     int64_t P, int C, int J, const float* w, void* dx,
+                     int64_t dxs, float* dw, float* db, int accumulate,
+                     float* workspace, int dtype, void* stream);
+
+/* ---- loss (utils/loss.py) ---------------------------------------------- */
+/* sums[0..3] = {sum BCE-with-logits, sum sigmoid*t, sum sigmoid, sum t} over
+ * n elements (fp64 accumulation, deterministic) */
+int vu_bce_dice_fwd(const float* logits, const float* target, int64_t n,
+                    double* sums, double* workspace, void* stream);
+/* grad = g * d/dlogit (w_bce*BCE_mean + w_dice*(1-dice)) */
+int vu_bce_dice_bwd(const float* logits, const float* target, int64_t n,
+                    const double* sums, float smooth, float w_bce,
+                    float w_dice, const float* gscale, float* grad,
+                    void* stream);
+/* kl_with_free_bits (loss.py:148-170), B x L, forward + grads */
+int vu_kl_free_bits(const float* mu, const float* logvar, int B, int L,
+                    float free_bits, float* value, float* gmu, float* glogvar,
+                    void* stream);
+
+/* ---- optimizer (train.py:334,406-411) ---------------------------------- */
+/* sum of squares of n fp32 values into out (fp64, deterministic) */
+int vu_sumsq(const float* x, int64_t n, double* out, double* workspace,
+             void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

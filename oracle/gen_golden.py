@@ -1,0 +1,237 @@
+"""Golden-vector generator — TEST INFRASTRUCTURE, runs only in the build container.
+
+Imports the reference (``/root/reference``, read-only) and records small
+input/output/gradient fixtures under ``tests/golden/*.npz``.  Nothing here
+ships to the GPU box as code: only the ``.npz`` data travels.  The reference
+modules imported are
+
+* ``unet.unet_parts``  (AttentionGate 7-30, DoubleConv 32-49, Down 51-63,
+  Up 65-95, OutConv 97-103)
+* ``unet.unet_model.UNet`` (6-36)
+* ``utils.loss``  (dice_loss 6-28, CombinedLoss 44-63, KLAnnealer 114-145,
+  kl_with_free_bits 148-170)
+* ``utils.metrics.dice_score`` (8-35)
+* ``unet/unet_resnet.py``: ``timm`` (requirements.txt:2, timm~=1.0.13) is
+  absent here, so the module cannot be imported.  ``DecoderBlock`` (31-101)
+  and ``AttentionGate`` (6-29) do not use timm; their class bodies are
+  compiled from the reference file's AST *without* the ``import timm`` line
+  (no timm stand-in is written).  The ResNet34 encoder and the
+  ``UNetResNet`` wiring stay parity-unpinned.
+
+The train-step golden restates ``train.py:381-411`` (the reference's own
+``train.py`` needs wandb/torchvision and cannot be imported) using the
+reference's own model and loss objects and ``torch.optim.AdamW`` exactly as
+``train.py:334`` configures it.
+
+Usage:  python oracle/gen_golden.py   (writes tests/golden/*.npz)
+"""
+import ast
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+
+from vaeunet_amd.init import seeded_init_  # noqa: E402
+from unet.unet_parts import AttentionGate, DoubleConv, Down, Up, OutConv  # noqa: E402
+from unet.unet_model import UNet  # noqa: E402
+from utils.loss import dice_loss, CombinedLoss, KLAnnealer, kl_with_free_bits  # noqa: E402
+from utils.metrics import dice_score  # noqa: E402
+
+torch.set_num_threads(8)
+torch.use_deterministic_algorithms(True)
+
+
+def _rng(seed):
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def _rand(seed, shape, lo=-1.0, hi=1.0):
+    return _rng(seed).uniform(lo, hi, size=shape).astype(np.float32)
+
+
+def _t(a, cl=False):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.to(memory_format=torch.channels_last) if cl and t.dim() == 4 else t
+
+
+def _np(t):
+    return t.detach().contiguous().cpu().numpy().copy()
+
+
+def _load_decoder_block():
+    """Compile DecoderBlock/AttentionGate from unet/unet_resnet.py without `import timm`."""
+    path = os.path.join(REF, "unet", "unet_resnet.py")
+    src = open(path).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.ClassDef)
+            and n.name in ("AttentionGate", "DecoderBlock")]
+    mod = ast.Module(body=keep, type_ignores=[])
+    ns = {"torch": torch, "nn": nn, "F": F}
+    exec(compile(mod, path, "exec"), ns)
+    return ns["DecoderBlock"]
+
+
+def record_module(name, module, inputs, seed, cl=True):
+    """Forward (train mode) + backward with a seeded grad_output."""
+    seeded_init_(module, seed)
+    module.train()
+    state = {k: _np(v) for k, v in module.state_dict().items()
+             if v.dtype.is_floating_point}
+    ins = [_t(a, cl).requires_grad_(True) for a in inputs]
+    if cl:
+        module = module.to(memory_format=torch.channels_last)
+    out = module(*ins)
+    gout = _rand(seed + 1000, tuple(out.shape))
+    out.backward(_t(gout, cl))
+    rec = {"out": _np(out), "gout": gout}
+    for i, (a, t) in enumerate(zip(inputs, ins)):
+        rec[f"in{i}"] = a
+        rec[f"gin{i}"] = _np(t.grad) if t.grad is not None else np.zeros_like(a)
+    for k, v in state.items():
+        rec[f"p0.{k}"] = v
+    for k, p in module.named_parameters():
+        rec[f"grad.{k}"] = _np(p.grad)
+    for k, b in module.named_buffers():
+        rec[f"buf.{k}"] = _np(b)
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **rec)
+    print(f"{name}: out {tuple(out.shape)}  |out|={float(out.detach().abs().mean()):.4f}")
+
+
+def gen_parts():
+    record_module("doubleconv_8_16", DoubleConv(8, 16), [_rand(1, (2, 8, 16, 16))], 11)
+    record_module("doubleconv_3_16_mid8", DoubleConv(3, 16, 8), [_rand(2, (2, 3, 12, 12))], 12)
+    record_module("down_16_32", Down(16, 32), [_rand(3, (2, 16, 16, 16))], 13)
+    record_module("down_odd_16_32", Down(16, 32), [_rand(4, (2, 16, 11, 9))], 14)
+    record_module("up_64_32_convT", Up(64, 32, bilinear=False),
+                  [_rand(5, (2, 64, 4, 4)), _rand(6, (2, 32, 8, 8))], 15)
+    record_module("up_64_32_bilinear", Up(64, 32, bilinear=True),
+                  [_rand(7, (2, 32, 4, 4)), _rand(8, (2, 32, 8, 8))], 16)
+    record_module("up_odd_64_32_convT", Up(64, 32, bilinear=False),
+                  [_rand(9, (2, 64, 4, 4)), _rand(10, (2, 32, 9, 10))], 17)
+    record_module("up_odd_64_32_bilinear", Up(64, 32, bilinear=True),
+                  [_rand(18, (2, 32, 5, 4)), _rand(19, (2, 32, 11, 9))], 20)
+    record_module("attention_32_32_16", AttentionGate(32, 32, 16),
+                  [_rand(21, (2, 32, 8, 8)), _rand(22, (2, 32, 8, 8))], 23)
+    record_module("outconv_16_2", OutConv(16, 2), [_rand(24, (2, 16, 8, 8))], 25)
+    DecoderBlock = _load_decoder_block()
+    record_module("decoder_64_32_48", DecoderBlock(64, 32, 48, 8, True, True, True),
+                  [_rand(26, (2, 64, 4, 4)), _rand(27, (2, 32, 8, 8)),
+                   _rand(28, (2, 8, 1, 1))], 29)
+    record_module("decoder_noattn_64_32_48", DecoderBlock(64, 32, 48, 8, False, True, False),
+                  [_rand(30, (2, 64, 4, 4)), _rand(31, (2, 32, 8, 8)),
+                   _rand(32, (2, 8, 1, 1))], 33)
+
+
+def gen_losses():
+    rec = {}
+    cases = {
+        "a": (_rand(40, (2, 1, 16, 16), -4, 4), (_rand(41, (2, 1, 16, 16), 0, 1) < 0.1)),
+        "b": (_rand(42, (3, 1, 8, 8), -9, 9), (_rand(43, (3, 1, 8, 8), 0, 1) < 0.5)),
+        "empty": (_rand(44, (2, 1, 8, 8), -8, -2), np.zeros((2, 1, 8, 8), bool)),
+        "c2": (_rand(45, (2, 2, 8, 8), -3, 3), (_rand(46, (2, 2, 8, 8), 0, 1) < 0.2)),
+    }
+    crit = CombinedLoss()
+    for k, (lg, tg) in cases.items():
+        tg = tg.astype(np.float32)
+        x = _t(lg).requires_grad_(True)
+        loss = crit(x, _t(tg))
+        loss.backward()
+        rec[f"{k}.logits"], rec[f"{k}.target"] = lg, tg
+        rec[f"{k}.loss"] = np.float32(loss.item())
+        rec[f"{k}.grad"] = _np(x.grad)
+        rec[f"{k}.dice_loss"] = np.float32(dice_loss(_t(lg), _t(tg)).item())
+        rec[f"{k}.bce"] = np.float32(F.binary_cross_entropy_with_logits(_t(lg), _t(tg)).item())
+        rec[f"{k}.dice_score"] = np.float32(dice_score(_t(lg), _t(tg)).item())
+    # KL with free bits: include exact ties with free_bits and clamp saturation.
+    mu = _rand(50, (4, 8), -2, 2)
+    lv = _rand(51, (4, 8), -3, 3)
+    mu[0, 0], lv[0, 0] = 0.0, 0.0           # kl == 0  -> below free bits
+    mu[1, 1], lv[1, 1] = 30.0, 0.0          # kl = 450 -> clamped at 100
+    lv[2, 2] = 6.0                          # large logvar
+    for fb in (1e-3, 1e-4, 0.0, 0.5):
+        m = _t(mu).requires_grad_(True)
+        v = _t(lv).requires_grad_(True)
+        kl = kl_with_free_bits(m, v, free_bits=fb)
+        kl.backward()
+        tag = f"kl_fb{fb:g}"
+        rec[f"{tag}.value"] = np.float32(kl.item())
+        rec[f"{tag}.gmu"] = _np(m.grad)
+        rec[f"{tag}.glogvar"] = _np(v.grad)
+    rec["kl.mu"], rec["kl.logvar"] = mu, lv
+    ann = KLAnnealer(kl_start=0.0, kl_end=1e-3, warmup_epochs=20)
+    rec["annealer"] = np.array([ann.get_weight(e) for e in range(0, 25)], np.float64)
+    np.savez_compressed(os.path.join(OUT, "losses.npz"), **rec)
+    print("losses: ok")
+
+
+def _grad_summary(model, rec, prefix):
+    names, norms, heads = [], [], []
+    for k, p in model.named_parameters():
+        names.append(k)
+        norms.append(float(p.grad.double().norm()))
+        heads.append(_np(p.grad).reshape(-1)[:16])
+    rec[f"{prefix}names"] = np.array(names)
+    rec[f"{prefix}gnorm"] = np.array(norms, np.float64)
+    rec[f"{prefix}ghead"] = np.stack([np.pad(h, (0, 16 - len(h))) for h in heads])
+
+
+def gen_unet(n_classes, bilinear, tag, batch=2, size=64, steps=1):
+    """Tiny-config train step (train.py:381-411) on the reference UNet."""
+    torch.manual_seed(0)
+    model = UNet(3, n_classes, bilinear=bilinear)
+    seeded_init_(model, 0)
+    model = model.to(memory_format=torch.channels_last).train()
+    x = _rand(100, (batch, 3, size, size), 0.0, 1.0)
+    m = (_rand(101, (batch, 1, size, size), 0, 1) < 0.05).astype(np.float32)
+    if n_classes == 2:
+        target = np.concatenate([1.0 - m, m], axis=1).astype(np.float32)
+    else:
+        target = m
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-5)
+    crit = CombinedLoss()
+    rec = {"x": x, "target": target}
+    xs = _t(x, cl=True)
+    logits = model(xs)
+    # dice_loss does .view(-1): channels_last output with C>1 cannot be viewed
+    # (SURVEY appendix); the C=2 golden uses contiguous logits.
+    lg = logits.contiguous() if n_classes > 1 else logits
+    loss = crit(lg, _t(target))
+    loss.backward()
+    rec["logits"] = _np(logits)
+    rec["argmax"] = _np(logits.argmax(1)) if n_classes > 1 else _np(logits > 0)
+    rec["loss"] = np.float32(loss.item())
+    _grad_summary(model, rec, "")
+    total = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    rec["total_norm"] = np.float32(total.item())
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    for k, v in model.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            rec[f"buf.{k}"] = _np(v)
+    heads = [(_np(p).reshape(-1)[:16]) for _, p in model.named_parameters()]
+    rec["p1head"] = np.stack([np.pad(h, (0, 16 - len(h))) for h in heads])
+    # second forward (after the update) in eval mode: running-stat path
+    model.eval()
+    with torch.no_grad():
+        rec["eval_logits"] = _np(model(xs))
+    np.savez_compressed(os.path.join(OUT, f"{tag}.npz"), **rec)
+    print(f"{tag}: loss {rec['loss']:.6f} total_norm {rec['total_norm']:.6f}")
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    gen_parts()
+    gen_losses()
+    gen_unet(1, False, "unet_c1_64")
+    gen_unet(2, False, "unet_c2_64")
+    gen_unet(1, True, "unet_c1_bilinear_64")

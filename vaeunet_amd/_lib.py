@@ -1,0 +1,126 @@
+"""ctypes binding of the C-ABI library ``libvaeunet_hip.so`` (include/vaeunet.h).
+
+This is the only place the product path touches native code.  There is no
+CPU or PyTorch fallback: if the library is missing or a launch fails the call
+raises, loudly (the oracle under ``oracle/`` is test infrastructure only).
+"""
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvaeunet_hip.so")
+
+F32, BF16 = 0, 1
+
+_p = C.c_void_p
+_i = C.c_int
+_l = C.c_int64
+_f = C.c_float
+
+
+class VuGather(C.Structure):
+    _fields_ = [("src", _p * 3), ("stride", _l * 3), ("cend", C.c_int32 * 3),
+                ("nsrc", C.c_int32), ("C", C.c_int32),
+                ("N", C.c_int32), ("H", C.c_int32), ("W", C.c_int32),
+                ("Hs", C.c_int32), ("Ws", C.c_int32), ("R", C.c_int32), ("S", C.c_int32),
+                ("sy", C.c_int32), ("sx", C.c_int32), ("dy", C.c_int32), ("dx", C.c_int32),
+                ("oy", C.c_int32), ("ox", C.c_int32)]
+
+
+class VuGemmFwd(C.Structure):
+    _fields_ = [("a", VuGather), ("b", _p), ("ldb", _l), ("ncol", C.c_int32),
+                ("out_mode", C.c_int32), ("out", _p), ("out_stride", _l),
+                ("out_coff", C.c_int32), ("oH", C.c_int32), ("oW", C.c_int32),
+                ("opy", C.c_int32), ("opx", C.c_int32), ("cout", C.c_int32),
+                ("bias", _p), ("stat_sum", _p), ("stat_m2", _p), ("accumulate", C.c_int32)]
+
+
+class VuGemmWgrad(C.Structure):
+    _fields_ = [("p", VuGather), ("q", VuGather), ("ni", C.c_int32), ("nj", C.c_int32),
+                ("splits", C.c_int32), ("m_per_split", _l), ("out", _p)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "vu_gemm_fwd": (_i, [C.POINTER(VuGemmFwd), _i, _p]),
+    "vu_gemm_fwd_row_tile": (_l, [C.POINTER(VuGemmFwd), _i]),
+    "vu_gemm_wgrad": (_i, [C.POINTER(VuGemmWgrad), _i, _p]),
+    "vu_slab_reduce": (_i, [_p, _i, _i, _i, _i, _i, _l, _l, _l, _p, _i, _p]),
+    "vu_permute4": (_i, [_p, _l, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "vu_bn_finalize": (_i, [_p, _p, _i, _l, _l, _i, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p,
+                            _p, _p, _p]),
+    "vu_bn_finalize_workspace_bytes": (_l, [_i, _i]),
+    "vu_bn_eval_coeffs": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
+    "vu_bn_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _i, _i, _p]),
+    "vu_bn_bwd_reduce": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p,
+                              _p, _i, _p]),
+    "vu_bn_bwd_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _i, _p, _l, _i, _p]),
+    "vu_reduce_workspace_bytes": (_l, [_l, _i]),
+    "vu_chan_sum": (_i, [_p, _l, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
+    "vu_copy": (_i, [_p, _l, _i, _p, _l, _i, _l, _i, _i, _p]),
+    "vu_input_pack": (_i, [_p, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),
+    "vu_maxpool2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _p]),
+    "vu_maxpool2_bwd": (_i, [_p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _p, _l, _i, _p]),
+    "vu_upsample_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "vu_upsample_bwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _i, _i, _i, _i, _i, _i, _i,
+                             _p]),
+    "vu_attn_tile_rows": (_l, []),
+    "vu_attn_psi_fwd": (_i, [_p, _p, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _l, _i, _p]),
+    "vu_attn_gate_fwd": (_i, [_p, _p, _p, _l, _l, _i, _p, _p, _l, _i, _p]),
+    "vu_attn_gate_bwd": (_i, [_p, _l, _p, _l, _p, _l, _i, _p, _l, _p, _i, _p]),
+    "vu_attn_psi_bwd_workspace_bytes": (_l, [_l, _i]),
+    "vu_attn_psi_bwd": (_i, [_p, _p, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _i,
+                             _p]),
+    "vu_pointwise_fwd": (_i, [_p, _l, _l, _i, _i, _p, _p, _p, _l, _i, _p]),
+    "vu_pointwise_bwd_workspace_bytes": (_l, [_l, _i, _i]),
+    "vu_pointwise_bwd": (_i, [_p, _l, _p, _l, _l, _i, _i, _p, _p, _l, _p, _p, _i, _p, _i, _p]),
+    "vu_loss_workspace_bytes": (_l, []),
+    "vu_bce_dice_fwd2": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p]),
+    "vu_bce_dice_bwd": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p]),
+    "vu_kl_free_bits2": (_i, [_p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
+    "vu_sumsq": (_i, [_p, _l, _p, _p, _p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the library once; raise if it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"vaeunet_amd: HIP library {LIB_PATH} is missing; run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or `make`)")
+        h = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return sorted(_SIGS)
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"vaeunet_amd: {name} failed with hipError {rc}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(lib(), name)(*args)
+
+
+def stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())

@@ -1,0 +1,410 @@
+// AttentionGate (unet_parts.py:7-30 / unet_resnet.py:6-29) memory-bound parts
+// and the tiny-output 1x1 convolutions (OutConv unet_parts.py:97-103,
+// final_conv unet_resnet.py:189).
+//
+//   g1 = BN(W_g g + b_g), x1 = BN(W_x x + b_x)      (GEMMs: gemm_fwd.hip)
+//   s  = relu(g1 + x1)                              \
+//   q  = W_psi s + b_psi   (F_int -> 1)              } vu_attn_psi_fwd (one pass)
+//   p  = sigmoid(BN(q));  out = x * p               vu_attn_gate_fwd
+//
+// A pixel's F_int channels are spread over LPP = F_int/8 lanes (8 channels
+// per lane, 16-byte loads), the dot product reduced with cross-lane shuffles;
+// a 256-thread block owns a 256-pixel tile and emits that tile's BatchNorm(1)
+// partial (sum, centered M2).  Weight-gradient sums use per-block partial
+// slabs reduced in a fixed order (deterministic, no float atomics).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+namespace {
+
+constexpr int TILE = 256;  // pixels per block
+
+inline unsigned ew_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+VU_DEV float group_sum(float v, int lpp) {
+  for (int o = lpp >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+VU_DEV void load8(const T* p, float* f) {
+  Vec8<T> v; v.load(p);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = v.get(k);
+}
+
+// block reduction of one float over 256 threads, result broadcast
+VU_DEV float block_sum(float v, float* sh) {
+  v = warp_sum(v);
+  int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  float t = sh[0] + sh[1] + sh[2] + sh[3];
+  return t;
+}
+
+template <typename T>
+__global__ void psi_fwd_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg, const float* tg,
+                               const float* sx, const float* tx, const float* wpsi, const float* bpsi, float* q,
+                               float* psum, float* pm2) {
+  __shared__ float sq[TILE];
+  __shared__ float red[4];
+  const int lpp = F >> 3;              // lanes per pixel (power of two <= 64)
+  const int ppw = 64 / lpp;            // pixels per wave-pass
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int64_t p0 = (int64_t)blockIdx.x * TILE;
+  const int c = sub * 8;
+  float wsg[8], wtg[8], wsx[8], wtx[8], wp[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wsg[k] = sg[c + k]; wtg[k] = tg[c + k]; wsx[k] = sx[c + k]; wtx[k] = tx[c + k]; wp[k] = wpsi[c + k];
+  }
+  const float b = bpsi[0];
+  for (int i = w * ppw + slot; i < TILE; i += 4 * ppw) {
+    int64_t p = p0 + i;
+    float acc = 0.f;
+    if (p < P) {
+      float a[8], bb[8];
+      load8<T>(ug + p * F + c, a);
+      load8<T>(ux + p * F + c, bb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s = fmaxf(a[k] * wsg[k] + wtg[k] + bb[k] * wsx[k] + wtx[k], 0.f);
+        acc += wp[k] * s;
+      }
+    }
+    acc = group_sum(acc, lpp) + b;
+    if (sub == 0) {
+      sq[i] = p < P ? acc : 0.f;
+      if (p < P) q[p] = acc;
+    }
+  }
+  __syncthreads();
+  int64_t nvalid = P - p0 < TILE ? P - p0 : TILE;
+  float v = threadIdx.x < nvalid ? sq[threadIdx.x] : 0.f;
+  float tot = block_sum(v, red);
+  float mean = tot / (float)nvalid;
+  float d = threadIdx.x < nvalid ? sq[threadIdx.x] - mean : 0.f;
+  float m2 = block_sum(d * d, red);
+  if (threadIdx.x == 0) { psum[blockIdx.x] = tot; pm2[blockIdx.x] = m2; }
+}
+
+template <typename T>
+__global__ void gate_fwd_kernel(const float* q, const float* st, const T* x, int64_t xs, int64_t P, int C,
+                                float* pmap, T* out, int64_t os) {
+  int V = C >> 3;
+  int64_t tot = P * V;
+  const float s = st[0], t = st[1];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / V;
+    int c = (int)(e - p * V) * 8;
+    float z = q[p] * s + t;
+    float pv = 1.f / (1.f + __expf(-z));
+    if (c == 0 && pmap) pmap[p] = pv;
+    Vec8<T> v; v.load(x + p * xs + c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v.set(k, v.get(k) * pv);
+    v.store(out + p * os + c);
+  }
+}
+
+// dx = dout * p ; dbnq[p] = (sum_c dout*x) * p*(1-p)
+template <typename T>
+__global__ void gate_bwd_kernel(const T* dout, int64_t dos, const T* x, int64_t xs, const float* pmap, int64_t P,
+                                int C, T* dx, int64_t dxs, float* dbnq) {
+  const int lpp = C >> 3 > 64 ? 64 : C >> 3;   // lanes per pixel
+  const int ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t pb = wave * ppw; pb < P; pb += nwaves * ppw) {
+    int64_t p = pb + slot;
+    float acc = 0.f;
+    if (p < P) {
+      float pv = pmap[p];
+      for (int c = sub * 8; c < C; c += lpp * 8) {
+        Vec8<T> vd, vx, vo;
+        vd.load(dout + p * dos + c);
+        vx.load(x + p * xs + c);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          acc += vd.get(k) * vx.get(k);
+          vo.set(k, vd.get(k) * pv);
+        }
+        vo.store(dx + p * dxs + c);
+      }
+    }
+    acc = group_sum(acc, lpp);
+    if (sub == 0 && p < P) { float pv = pmap[p]; dbnq[p] = acc * pv * (1.f - pv); }
+  }
+}
+
+// ds[p,c] = dq[p]*wpsi[c]*(s>0); partial dwpsi[c] over the tile; partial dbpsi
+template <typename T>
+__global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg, const float* tg,
+                               const float* sx, const float* tx, const float* wpsi, const float* dq, T* ds,
+                               float* part) {
+  __shared__ float sh[256 * 8];
+  __shared__ float sb[256];
+  const int lpp = F >> 3, ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int64_t p0 = (int64_t)blockIdx.x * TILE;
+  const int c = sub * 8;
+  float wsg[8], wtg[8], wsx[8], wtx[8], wp[8], dw[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wsg[k] = sg[c + k]; wtg[k] = tg[c + k]; wsx[k] = sx[c + k]; wtx[k] = tx[c + k]; wp[k] = wpsi[c + k];
+    dw[k] = 0.f;
+  }
+  float db = 0.f;
+  for (int i = w * ppw + slot; i < TILE; i += 4 * ppw) {
+    int64_t p = p0 + i;
+    if (p >= P) continue;
+    float g = dq[p];
+    if (sub == 0) db += g;
+    float a[8], bb[8];
+    load8<T>(ug + p * F + c, a);
+    load8<T>(ux + p * F + c, bb);
+    Vec8<T> o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float s = a[k] * wsg[k] + wtg[k] + bb[k] * wsx[k] + wtx[k];
+      bool on = s > 0.f;
+      dw[k] += on ? g * s : 0.f;
+      o.set(k, on ? g * wp[k] : 0.f);
+    }
+    o.store(ds + p * F + c);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = dw[k];
+  sb[threadIdx.x] = db;
+  __syncthreads();
+  // threads with equal `sub` hold the same channels: sum them in fixed order
+  for (int cc = threadIdx.x; cc < F; cc += 256) {
+    int sb_ = cc >> 3, k = cc & 7;
+    float s = 0.f;
+    for (int t = 0; t < 256; ++t)
+      if (((t & 63) % lpp) == sb_) s += sh[t * 8 + k];
+    part[(int64_t)blockIdx.x * (F + 1) + cc] = s;
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int t = 0; t < 256; ++t) s += sb[t];
+    part[(int64_t)blockIdx.x * (F + 1) + F] = s;
+  }
+}
+
+__global__ void part_final(const float* part, int nblk, int width, float* out, int n_out, float* out2,
+                           int accumulate) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= width) return;
+  double s = 0;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * width + c];
+  float* o = c < n_out ? out + c : out2 + (c - n_out);
+  if (o == nullptr) return;
+  *o = accumulate ? *o + (float)s : (float)s;
+}
+
+// ---- tiny-output pointwise conv ----
+template <typename T>
+__global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, const float* w, const float* b,
+                              float* y, int64_t ys) {
+  const int lpp = C >> 3 > 64 ? 64 : C >> 3;
+  const int ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t pb = wave * ppw; pb < P; pb += nwaves * ppw) {
+    int64_t p = pb + slot;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p < P) {
+      for (int c = sub * 8; c < C; c += lpp * 8) {
+        float f[8];
+        load8<T>(x + p * xs + c, f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < J)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[j] += f[k] * w[j * C + c + k];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = group_sum(acc[j], lpp);
+    if (sub == 0 && p < P)
+      for (int j = 0; j < J; ++j) y[p * ys + j] = acc[j] + (b ? b[j] : 0.f);
+  }
+}
+
+// dx = dy w ; per-block partials of dw[j][c] = sum dy[p,j] x[p,c] and db[j]
+template <typename T>
+__global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t dys, int64_t P, int C, int J,
+                              const float* w, T* dx, int64_t dxs, float* part) {
+  __shared__ float sh[256 * 8];
+  const int lpp = C >> 3;   // <= 32 enforced on host (C <= 256)
+  const int ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int64_t p0 = (int64_t)blockIdx.x * TILE;
+  const int c = sub * 8;
+  const int width = J * C + J;
+  for (int j = 0; j < J; ++j) {
+    // one pass per output column j keeps registers small (J <= 4)
+    float dw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dw[k] = 0.f;
+    float dbj = 0.f;
+    for (int i = wv * ppw + slot; i < TILE; i += 4 * ppw) {
+      int64_t p = p0 + i;
+      if (p >= P) continue;
+      float g = dy[p * dys + j];
+      if (sub == 0) dbj += g;
+      float f[8];
+      load8<T>(x + p * xs + c, f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dw[k] += g * f[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = dw[k];
+    __syncthreads();
+    for (int cc = threadIdx.x; cc < C; cc += 256) {
+      int sb_ = cc >> 3, k = cc & 7;
+      float s = 0.f;
+      for (int t = 0; t < 256; ++t)
+        if (((t & 63) % lpp) == sb_) s += sh[t * 8 + k];
+      part[(int64_t)blockIdx.x * width + j * C + cc] = s;
+    }
+    __syncthreads();
+    sh[threadIdx.x] = dbj;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int t = 0; t < 256; ++t) s += sh[t];
+      part[(int64_t)blockIdx.x * width + J * C + j] = s;
+    }
+    __syncthreads();
+  }
+  // dx
+  for (int i = wv * ppw + slot; i < TILE; i += 4 * ppw) {
+    int64_t p = p0 + i;
+    if (p >= P) continue;
+    Vec8<T> o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float s = 0.f;
+      for (int j = 0; j < J; ++j) s += dy[p * dys + j] * w[j * C + c + k];
+      o.set(k, s);
+    }
+    o.store(dx + p * dxs + c);
+  }
+}
+
+inline bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+}  // namespace
+
+#define DISPATCH_T(dtype, ...) \
+  if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
+
+extern "C" int64_t vu_attn_tile_rows() { return TILE; }
+
+extern "C" int vu_attn_psi_fwd(const void* ug, const void* ux, int64_t P, int F, const float* sg, const float* tg,
+                               const float* sx, const float* tx, const float* wpsi, const float* bpsi, float* q,
+                               float* psum, float* pm2, int64_t tile_rows, int dtype, void* stream) {
+  if (F % 8 != 0 || !pow2(F / 8) || F / 8 > 64 || tile_rows != TILE) return (int)hipErrorInvalidValue;
+  int nblk = (int)((P + TILE - 1) / TILE);
+  if (nblk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((psi_fwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
+                       sx, tx, wpsi, bpsi, q, psum, pm2);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_attn_gate_fwd(const float* q, const float* st_, const void* x, int64_t xs, int64_t P, int C,
+                                float* pmap, void* out, int64_t os, int dtype, void* stream) {
+  if (C % 8 != 0 || xs % 8 != 0 || os % 8 != 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (P == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((gate_fwd_kernel<T>), dim3(ew_grid(P * C / 8)), dim3(256), 0, st, q, st_, (const T*)x, xs, P,
+                       C, pmap, (T*)out, os);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_attn_gate_bwd(const void* dout, int64_t dos, const void* x, int64_t xs, const float* pmap,
+                                int64_t P, int C, void* dx, int64_t dxs, float* dqpre, int dtype, void* stream) {
+  if (C % 8 != 0 || !pow2(C / 8 > 64 ? 64 : C / 8) || dos % 8 || xs % 8 || dxs % 8) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (P == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((gate_bwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)dout, dos,
+                       (const T*)x, xs, pmap, P, C, (T*)dx, dxs, dqpre);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t vu_attn_psi_bwd_workspace_bytes(int64_t P, int F) {
+  return ((P + TILE - 1) / TILE) * (F + 1) * (int64_t)sizeof(float);
+}
+
+extern "C" int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F, const float* sg, const float* tg,
+                               const float* sx, const float* tx, const float* wpsi, const float* dq, void* ds,
+                               float* dwpsi, float* dbpsi, int accumulate, float* workspace, int dtype,
+                               void* stream) {
+  if (F % 8 != 0 || !pow2(F / 8) || F / 8 > 64 || F > 2048) return (int)hipErrorInvalidValue;
+  int nblk = (int)((P + TILE - 1) / TILE);
+  if (nblk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((psi_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
+                       sx, tx, wpsi, dq, (T*)ds, workspace);
+  })
+  hipLaunchKernelGGL(part_final, dim3((F + 1 + 63) / 64), dim3(64), 0, st, workspace, nblk, F + 1, dwpsi, F, dbpsi,
+                     accumulate);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_pointwise_fwd(const void* x, int64_t xs, int64_t P, int C, int J, const float* w, const float* b,
+                                float* y, int64_t ys, int dtype, void* stream) {
+  if (C % 8 != 0 || xs % 8 != 0 || J < 1 || J > 4 || !pow2(C / 8 > 64 ? 64 : C / 8)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (P == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((pw_fwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w, b, y,
+                       ys);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t vu_pointwise_bwd_workspace_bytes(int64_t P, int C, int J) {
+  return ((P + TILE - 1) / TILE) * (int64_t)(J * C + J) * (int64_t)sizeof(float);
+}
+
+extern "C" int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int64_t dys, int64_t P, int C, int J,
+                                const float* w, void* dx, int64_t dxs, float* dw, float* db, int accumulate,
+                                float* workspace, int dtype, void* stream) {
+  if (C % 8 != 0 || xs % 8 || dxs % 8 || J < 1 || J > 4 || !pow2(C / 8) || C / 8 > 32)
+    return (int)hipErrorInvalidValue;
+  int nblk = (int)((P + TILE - 1) / TILE);
+  if (nblk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((pw_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w, (T*)dx,
+                       dxs, workspace);
+  })
+  hipLaunchKernelGGL(part_final, dim3((J * C + J + 63) / 64), dim3(64), 0, st, workspace, nblk, J * C + J, dw, J * C,
+                     db, accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,444 @@
+// BatchNorm2d (train/eval), fused ReLU, and per-channel reductions over NHWC.
+//
+// Reference semantics: nn.BatchNorm2d in train mode (unet_parts.py:41,44 and
+// the attention-gate BNs :12,16,20): batch mean and biased variance over
+// (N,H,W), y = gamma*(x-mean)/sqrt(var+eps) + beta, running stats updated with
+// momentum 0.1 and the UNBIASED variance, then nn.ReLU(inplace=True)
+// (unet_parts.py:42,45) whose backward masks by output > 0.
+//
+// Statistics come from the producing GEMM's epilogue as per-row-tile (sum,
+// centered M2) pairs; vu_bn_finalize combines them with Chan's parallel
+// formula in fp64 in a fixed order, so results are bitwise reproducible.
+// Backward needs two per-channel sums (sum dz, sum dz*xhat): a two-stage
+// deterministic reduction (fp32 per block, fp64 across blocks).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+namespace {
+
+VU_DEV void chan_combine(double& n, double& m, double& M2, double nb, double mb, double M2b) {
+  double nn = n + nb;
+  if (nb <= 0.0) return;
+  double d = mb - m;
+  m += d * nb / nn;
+  M2 += M2b + d * d * n * nb / nn;
+  n = nn;
+}
+
+// stage 1: grid (ceil(C/64), S), 256 threads = 64 channels x 4 tile lanes
+__global__ void bn_stats_stage1(const float* psum, const float* pm2, int tiles, int64_t tile_rows,
+                                int64_t rows, int C, int S, double* ws) {
+  __shared__ double sh[3][4][64];
+  int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  int c = blockIdx.x * 64 + cl;
+  int per = (tiles + S - 1) / S;
+  int tb = blockIdx.y * per, te = min(tiles, tb + per);
+  double n = 0, m = 0, M2 = 0;
+  if (c < C) {
+    for (int t = tb + tl; t < te; t += 4) {
+      int64_t nb = rows - (int64_t)t * tile_rows;
+      if (nb > tile_rows) nb = tile_rows;
+      double s = psum[(int64_t)t * C + c];
+      chan_combine(n, m, M2, (double)nb, s / (double)nb, (double)pm2[(int64_t)t * C + c]);
+    }
+  }
+  sh[0][tl][cl] = n; sh[1][tl][cl] = m; sh[2][tl][cl] = M2;
+  __syncthreads();
+  if (tl == 0 && c < C) {
+    for (int q = 1; q < 4; ++q) chan_combine(n, m, M2, sh[0][q][cl], sh[1][q][cl], sh[2][q][cl]);
+    double* o = ws + ((int64_t)blockIdx.y * C + c) * 3;
+    o[0] = n; o[1] = m; o[2] = M2;
+  }
+}
+
+__global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gamma, const float* beta,
+                                float* rmean, float* rvar, float momentum, float eps, float* scale,
+                                float* shift, float* smean, float* sinvstd, int64_t* nbt) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double n = 0, m = 0, M2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const double* o = ws + ((int64_t)s * C + c) * 3;
+    chan_combine(n, m, M2, o[0], o[1], o[2]);
+  }
+  double var = n > 0 ? M2 / n : 0.0;
+  float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  float mean = (float)m;
+  scale[c] = g * invstd;
+  shift[c] = b - mean * g * invstd;
+  if (smean) smean[c] = mean;
+  if (sinvstd) sinvstd[c] = invstd;
+  if (nbt && c == 0) nbt[0] += 1;
+  if (rmean && momentum != 0.f) {
+    double unb = n > 1 ? M2 / (n - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+  }
+}
+
+__global__ void bn_eval_kernel(const float* gamma, const float* beta, const float* rm, const float* rv,
+                               float eps, int C, float* scale, float* shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float invstd = 1.f / sqrtf(rv[c] + eps);
+  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * invstd;
+  shift[c] = b - rm[c] * g * invstd;
+}
+
+// ---- elementwise apply: y = relu?(x*scale+shift), 8 channels per thread ----
+template <typename T>
+__global__ void bn_apply_kernel(const T* x, int64_t xs, T* y, int64_t ys, int64_t P, int C,
+                                const float* scale, const float* shift, int relu) {
+  int V = C >> 3;
+  int64_t tot = P * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / V;
+    int c = (int)(e - p * V) * 8;
+    Vec8<T> v;
+    v.load(x + p * xs + c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float z = v.get(i) * scale[c + i] + shift[c + i];
+      v.set(i, relu ? fmaxf(z, 0.f) : z);
+    }
+    v.store(y + p * ys + c);
+  }
+}
+
+// ---- per-channel partial reductions ----
+// MODE 0: s0 = sum x
+// MODE 1: s0 = sum dz, s1 = sum dz*xhat; dz = dy*(z>0 if relu), xhat=(x-mean)*invstd
+constexpr int RED_PB = 2048;  // pixels per block
+
+struct RedArgs {
+  const void* a; int64_t as;   // x (mode 0) or dy (mode 1)
+  const void* b; int64_t bs;   // x (mode 1)
+  int64_t P; int C;
+  const float* scale; const float* shift; const float* mean; const float* invstd;
+  int relu;
+  float* part;                 // [nblk][2][C]
+  int H, W, y0, x0, Hr, Wr;    // pixel window (mode 0); Hr == 0: dense
+};
+
+VU_DEV int64_t win_pix(const RedArgs& r, int64_t p) {
+  if (r.Hr == 0) return p;
+  int64_t j = p % r.Wr, t = p / r.Wr;
+  int64_t i = t % r.Hr, n = t / r.Hr;
+  return (n * r.H + r.y0 + i) * r.W + r.x0 + j;
+}
+
+template <typename T, int MODE>
+__global__ void chan_partial_kernel(RedArgs r) {
+  __shared__ float sh[2][256 * 8];
+  const int V = r.C >> 3;            // vectors per pixel (<= 256)
+  const int R = 256 / V;             // pixels per pass
+  const int t = threadIdx.x;
+  const int cv = t % V, row = t / V;
+  const bool act = row < R;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { s0[i] = 0.f; s1[i] = 0.f; }
+  const int c = cv * 8;
+  int64_t pb = (int64_t)blockIdx.x * RED_PB, pe = pb + RED_PB;
+  if (pe > r.P) pe = r.P;
+  if (act) {
+    for (int64_t p = pb + row; p < pe; p += R) {
+      Vec8<T> va;
+      va.load(reinterpret_cast<const T*>(r.a) + win_pix(r, p) * r.as + c);
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s0[i] += va.get(i);
+      } else {
+        Vec8<T> vb;
+        vb.load(reinterpret_cast<const T*>(r.b) + p * r.bs + c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float xv = vb.get(i);
+          float dz = va.get(i);
+          if (r.relu && !(xv * r.scale[c + i] + r.shift[c + i] > 0.f)) dz = 0.f;
+          float xh = (xv - r.mean[c + i]) * r.invstd[c + i];
+          s0[i] += dz;
+          s1[i] += dz * xh;
+        }
+      }
+    }
+  }
+  // reduce over the R rows in fixed order
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sh[0][row * r.C + c + i] = s0[i]; sh[1][row * r.C + c + i] = s1[i]; }
+  }
+  __syncthreads();
+  for (int cc = t; cc < r.C; cc += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int q = 0; q < R; ++q) { a0 += sh[0][q * r.C + cc]; a1 += sh[1][q * r.C + cc]; }
+    r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + cc] = a0;
+    r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + cc] = a1;
+  }
+}
+
+// scalar fallback for C % 8 != 0 (C <= 256)
+template <typename T, int MODE>
+__global__ void chan_partial_scalar(RedArgs r) {
+  __shared__ float sh[2][256];
+  const int R = 256 / r.C;
+  const int t = threadIdx.x, c = t % r.C, row = t / r.C;
+  const bool act = row < R;
+  float s0 = 0.f, s1 = 0.f;
+  int64_t pb = (int64_t)blockIdx.x * RED_PB, pe = pb + RED_PB;
+  if (pe > r.P) pe = r.P;
+  if (act) {
+    for (int64_t p = pb + row; p < pe; p += R) {
+      float av = ld1<T>(reinterpret_cast<const T*>(r.a) + win_pix(r, p) * r.as + c);
+      if (MODE == 0) s0 += av;
+      else {
+        float xv = ld1<T>(reinterpret_cast<const T*>(r.b) + p * r.bs + c);
+        float dz = av;
+        if (r.relu && !(xv * r.scale[c] + r.shift[c] > 0.f)) dz = 0.f;
+        s0 += dz;
+        s1 += dz * (xv - r.mean[c]) * r.invstd[c];
+      }
+    }
+    sh[0][row * r.C + c] = s0;
+    sh[1][row * r.C + c] = s1;
+  }
+  __syncthreads();
+  if (t < r.C) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int q = 0; q < R; ++q) { a0 += sh[0][q * r.C + t]; a1 += sh[1][q * r.C + t]; }
+    r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + t] = a0;
+    r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + t] = a1;
+  }
+}
+
+// stage 2: per channel, sum partials in fp64 in block order
+__global__ void chan_final_sum(const float* part, int nblk, int C, float* out, int accumulate) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0;
+  for (int b = 0; b < nblk; ++b) s += part[((int64_t)b * 2) * C + c];
+  out[c] = accumulate ? out[c] + (float)s : (float)s;
+}
+
+__global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, const float* gamma,
+                             const float* invstd, float* dgamma, float* dbeta, int accumulate,
+                             float* coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0, s1 = 0;
+  for (int b = 0; b < nblk; ++b) {
+    s0 += part[((int64_t)b * 2 + 0) * C + c];
+    s1 += part[((int64_t)b * 2 + 1) * C + c];
+  }
+  float g = gamma ? gamma[c] : 1.f;
+  float is = invstd[c];
+  float k1 = g * is;
+  coef[c] = k1;
+  coef[C + c] = (float)(-(double)k1 * is * s1 / (double)P);
+  coef[2 * C + c] = (float)(-(double)k1 * s0 / (double)P);
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* dy, int64_t dys, const T* x, int64_t xs, int64_t P, int C,
+                                    const float* scale, const float* shift, const float* mean,
+                                    const float* coef, int relu, T* dx, int64_t dxs) {
+  int V = C >> 3;
+  int64_t tot = P * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / V;
+    int c = (int)(e - p * V) * 8;
+    Vec8<T> vd, vx, vo;
+    vd.load(dy + p * dys + c);
+    vx.load(x + p * xs + c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int cc = c + i;
+      float xv = vx.get(i), dz = vd.get(i);
+      if (relu && !(xv * scale[cc] + shift[cc] > 0.f)) dz = 0.f;
+      vo.set(i, coef[cc] * dz + coef[C + cc] * (xv - mean[cc]) + coef[2 * C + cc]);
+    }
+    vo.store(dx + p * dxs + c);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_scalar(const T* dy, int64_t dys, const T* x, int64_t xs, int64_t P, int C,
+                                    const float* scale, const float* shift, const float* mean,
+                                    const float* coef, int relu, T* dx, int64_t dxs) {
+  int64_t tot = P * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / C;
+    int c = (int)(e - p * C);
+    float xv = ld1<T>(x + p * xs + c), dz = ld1<T>(dy + p * dys + c);
+    if (relu && !(xv * scale[c] + shift[c] > 0.f)) dz = 0.f;
+    st1<T>(dx + p * dxs + c, coef[c] * dz + coef[C + c] * (xv - mean[c]) + coef[2 * C + c]);
+  }
+}
+
+template <typename T>
+__global__ void bn_apply_scalar(const T* x, int64_t xs, T* y, int64_t ys, int64_t P, int C,
+                                const float* scale, const float* shift, int relu) {
+  int64_t tot = P * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / C;
+    int c = (int)(e - p * C);
+    float z = ld1<T>(x + p * xs + c) * scale[c] + shift[c];
+    st1<T>(y + p * ys + c, relu ? fmaxf(z, 0.f) : z);
+  }
+}
+
+inline unsigned ew_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+inline bool vec8_ok(int C, int64_t s0, int64_t s1, int64_t s2 = 0) {
+  return C % 8 == 0 && s0 % 8 == 0 && s1 % 8 == 0 && s2 % 8 == 0;
+}
+
+template <typename T, int MODE>
+int launch_partial(const RedArgs& r, hipStream_t st, int& nblk) {
+  nblk = (int)((r.P + RED_PB - 1) / RED_PB);
+  if (nblk < 1) nblk = 1;
+  bool vec = r.C % 8 == 0 && r.as % 8 == 0 && (MODE == 0 || r.bs % 8 == 0) && r.C / 8 <= 256;
+  if (vec)
+    hipLaunchKernelGGL((chan_partial_kernel<T, MODE>), dim3(nblk), dim3(256), 0, st, r);
+  else if (r.C <= 256)
+    hipLaunchKernelGGL((chan_partial_scalar<T, MODE>), dim3(nblk), dim3(256), 0, st, r);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int64_t vu_reduce_workspace_bytes(int64_t P, int C) {
+  int64_t nblk = (P + RED_PB - 1) / RED_PB;
+  if (nblk < 1) nblk = 1;
+  return nblk * 2 * C * (int64_t)sizeof(float);
+}
+
+extern "C" int64_t vu_bn_finalize_workspace_bytes(int tiles, int C) {
+  int S = (tiles + 63) / 64;
+  if (S > 64) S = 64;
+  if (S < 1) S = 1;
+  return (int64_t)S * C * 3 * sizeof(double);
+}
+
+extern "C" int vu_bn_finalize(const float* psum, const float* pm2, int tiles, int64_t tile_rows,
+                              int64_t rows, int C, const float* gamma, const float* beta,
+                              float* running_mean, float* running_var, float momentum, float eps,
+                              float* scale, float* shift, float* save_mean, float* save_invstd,
+                              int64_t* num_batches_tracked, float* workspace, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int S = (tiles + 63) / 64;
+  if (S > 64) S = 64;
+  if (S < 1) S = 1;
+  double* ws = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(bn_stats_stage1, dim3((C + 63) / 64, S), dim3(256), 0, st, psum, pm2, tiles,
+                     tile_rows, rows, C, S, ws);
+  hipLaunchKernelGGL(bn_stats_stage2, dim3((C + 63) / 64), dim3(64), 0, st, ws, S, C, gamma, beta,
+                     running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd,
+                     num_batches_tracked);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_bn_eval_coeffs(const float* gamma, const float* beta, const float* running_mean,
+                                 const float* running_var, float eps, int C, float* scale,
+                                 float* shift, void* stream) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, gamma,
+                     beta, running_mean, running_var, eps, C, scale, shift);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_bn_apply(const void* x, int64_t xs, void* y, int64_t ys, int64_t P, int C,
+                           const float* scale, const float* shift, int relu, int dtype,
+                           void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (P * C == 0) return 0;
+  bool vec = vec8_ok(C, xs, ys);
+  if (dtype == VU_BF16) {
+    if (vec)
+      hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+                         (const bf16_t*)x, xs, (bf16_t*)y, ys, P, C, scale, shift, relu);
+    else
+      hipLaunchKernelGGL(bn_apply_scalar<bf16_t>, dim3(ew_grid(P * C)), dim3(256), 0, st,
+                         (const bf16_t*)x, xs, (bf16_t*)y, ys, P, C, scale, shift, relu);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+                         (const float*)x, xs, (float*)y, ys, P, C, scale, shift, relu);
+    else
+      hipLaunchKernelGGL(bn_apply_scalar<float>, dim3(ew_grid(P * C)), dim3(256), 0, st,
+                         (const float*)x, xs, (float*)y, ys, P, C, scale, shift, relu);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_bn_bwd_reduce(const void* dy, int64_t dys, const void* x, int64_t xs, int64_t P,
+                                int C, const float* scale, const float* shift, const float* mean,
+                                const float* invstd, const float* gamma, int relu, float* dgamma,
+                                float* dbeta, int accumulate, float* coef, float* workspace,
+                                int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RedArgs r{dy, dys, x, xs, P, C, scale, shift, mean, invstd, relu, workspace, 0, 0, 0, 0, 0, 0};
+  int nblk = 0, rc;
+  rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk) : launch_partial<float, 1>(r, st, nblk);
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64), dim3(64), 0, st, workspace, nblk, C, P,
+                     gamma, invstd, dgamma, dbeta, accumulate, coef);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_bn_bwd_apply(const void* dy, int64_t dys, const void* x, int64_t xs, int64_t P,
+                               int C, const float* scale, const float* shift, const float* mean,
+                               const float* coef, int relu, void* dx, int64_t dxs, int dtype,
+                               void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (P * C == 0) return 0;
+  bool vec = vec8_ok(C, dys, xs, dxs);
+  if (dtype == VU_BF16) {
+    if (vec)
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+                         (const bf16_t*)dy, dys, (const bf16_t*)x, xs, P, C, scale, shift, mean, coef,
+                         relu, (bf16_t*)dx, dxs);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_scalar<bf16_t>, dim3(ew_grid(P * C)), dim3(256), 0, st,
+                         (const bf16_t*)dy, dys, (const bf16_t*)x, xs, P, C, scale, shift, mean, coef,
+                         relu, (bf16_t*)dx, dxs);
+  } else {
+    if (vec)
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+                         (const float*)dy, dys, (const float*)x, xs, P, C, scale, shift, mean, coef,
+                         relu, (float*)dx, dxs);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_scalar<float>, dim3(ew_grid(P * C)), dim3(256), 0, st,
+                         (const float*)dy, dys, (const float*)x, xs, P, C, scale, shift, mean, coef,
+                         relu, (float*)dx, dxs);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_chan_sum(const void* x, int64_t stride, int N, int H, int W, int y0, int x0, int Hr,
+                           int Wr, int C, float* out, int accumulate, float* workspace, int dtype,
+                           void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t P = (int64_t)N * Hr * Wr;
+  RedArgs r{x, stride, nullptr, 0, P, C, nullptr, nullptr, nullptr, nullptr, 0, workspace, H, W, y0, x0, Hr, Wr};
+  int nblk = 0, rc;
+  rc = dtype == VU_BF16 ? launch_partial<bf16_t, 0>(r, st, nblk) : launch_partial<float, 0>(r, st, nblk);
+  if (rc) return rc;
+  hipLaunchKernelGGL(chan_final_sum, dim3((C + 63) / 64), dim3(64), 0, st, workspace, nblk, C, out,
+                     accumulate);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,92 @@
+// Shared device helpers for the VAE-U-Net HIP kernels (gfx950 / CDNA4 only).
+//
+// Storage types: activations are NHWC ("channels_last"), either bf16 (speed
+// mode, the autocast path of train.py:385) or fp32 (parity mode).  Every
+// kernel is templated on the storage type T in {float, bf16_t}; arithmetic
+// and all reductions are fp32 (partials combined in fp64 where counts reach
+// millions of pixels).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+enum VuDType { VU_F32 = 0, VU_BF16 = 1 };
+
+#define VU_DEV __device__ __forceinline__
+
+VU_DEV float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+VU_DEV uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+// Scalar load/store of one element as fp32.
+template <typename T> VU_DEV float ld1(const T* p);
+template <> VU_DEV float ld1<float>(const float* p) { return *p; }
+template <> VU_DEV float ld1<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> VU_DEV void st1(T* p, float v);
+template <> VU_DEV void st1<float>(float* p, float v) { *p = v; }
+template <> VU_DEV void st1<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// Round a float to the storage precision (identity for fp32).
+template <typename T> VU_DEV float rnd(float v);
+template <> VU_DEV float rnd<float>(float v) { return v; }
+template <> VU_DEV float rnd<bf16_t>(float v) { return bf2f(f2bf(v)); }
+
+// 8-element vector helpers (16 B for bf16, 32 B for fp32).
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16_t> {
+  u32x4 v;
+  VU_DEV void load(const bf16_t* p) { v = *reinterpret_cast<const u32x4*>(p); }
+  VU_DEV void store(bf16_t* p) const { *reinterpret_cast<u32x4*>(p) = v; }
+  VU_DEV float get(int i) const {
+    uint32_t w = v[i >> 1];
+    return __uint_as_float((i & 1) ? (w & 0xffff0000u) : (w << 16));
+  }
+  VU_DEV void set(int i, float f) {
+    uint32_t h = f2bf(f);
+    uint32_t w = v[i >> 1];
+    v[i >> 1] = (i & 1) ? ((w & 0xffffu) | (h << 16)) : ((w & 0xffff0000u) | h);
+  }
+  VU_DEV void zero() { v = u32x4{0, 0, 0, 0}; }
+};
+template <> struct Vec8<float> {
+  f32x4 a, b;
+  VU_DEV void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  VU_DEV void store(float* p) const {
+    *reinterpret_cast<f32x4*>(p) = a;
+    *reinterpret_cast<f32x4*>(p + 4) = b;
+  }
+  VU_DEV float get(int i) const { return i < 4 ? a[i & 3] : b[i & 3]; }
+  VU_DEV void set(int i, float f) {
+    if (i < 4) a[i & 3] = f; else b[i & 3] = f;
+  }
+  VU_DEV void zero() { a = f32x4{0, 0, 0, 0}; b = a; }
+};
+
+VU_DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+VU_DEV double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap of a linear block id (cdna_hip_programming T1):
+// consecutive logical ids land on the same XCD (blocks b, b+8 share one).
+VU_DEV int xcd_remap(int bid, int nblk) {
+  if (nblk < 16) return bid;
+  int q = nblk >> 3, r = nblk & 7, xcd = bid & 7, pos = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+}
+
+#define VU_CHECK_LAUNCH() return (int)hipGetLastError()

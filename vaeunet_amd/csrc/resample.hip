@@ -1,0 +1,427 @@
+// Max-pool 2x2 (Down, unet_parts.py:57), bilinear align_corners=True
+// upsampling (Up bilinear :73, DecoderBlock :79/93, UNetResNet :238) with the
+// F.pad of unet_parts.py:85-89 folded into the output placement, and the
+// layout / cast helpers (input packing, weight permutes, strided copies).
+//
+// All NHWC, 8 channels (16 B bf16 / 32 B fp32) per thread where the channel
+// count allows, grid-stride loops.  Backward passes are gathers (each output
+// element written exactly once, no atomics) so results are deterministic.
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+namespace {
+
+inline unsigned ew_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// ------------------------------ max pool --------------------------------
+// PyTorch CPU/GPU max_pool2d scan: window row-major, update when
+// (v > best || isnan(v)): ties keep the FIRST max.
+template <typename T, int VW>
+__global__ void maxpool_fwd_kernel(const T* x, int64_t xs, int N, int H, int W, int C, T* y, int64_t ys) {
+  int Ho = H >> 1, Wo = W >> 1, V = C / VW;
+  int64_t tot = (int64_t)N * Ho * Wo * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t q = e / V;
+    int c = (int)(e - q * V) * VW;
+    int j = (int)(q % Wo);
+    int64_t t = q / Wo;
+    int i = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float best[VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) best[k] = -INFINITY;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const T* src = x + (((int64_t)n * H + 2 * i + a) * W + 2 * j + b) * xs + c;
+        if (VW == 8) {
+          Vec8<T> v; v.load(src);
+#pragma unroll
+          for (int k = 0; k < VW; ++k) { float f = v.get(k); if (f > best[k] || isnan(f)) best[k] = f; }
+        } else {
+          float f = ld1<T>(src); if (f > best[0] || isnan(f)) best[0] = f;
+        }
+      }
+    T* dst = y + q * ys + c;
+    if (VW == 8) { Vec8<T> v; for (int k = 0; k < 8; ++k) v.set(k, best[k]); v.store(dst); }
+    else st1<T>(dst, best[0]);
+  }
+}
+
+template <typename T, int VW>
+__global__ void maxpool_bwd_kernel(const T* x, int64_t xs, const T* dy, int64_t dys, int N, int H, int W, int C,
+                                   T* dx, int64_t dxs, const T* add, int64_t adds) {
+  int Ho = H >> 1, Wo = W >> 1, V = C / VW;
+  int64_t tot = (int64_t)N * Ho * Wo * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t q = e / V;
+    int c = (int)(e - q * V) * VW;
+    int j = (int)(q % Wo);
+    int64_t t = q / Wo;
+    int i = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    float best[VW];
+    int arg[VW];
+    float vals[4][VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) { best[k] = -INFINITY; arg[k] = 0; }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const T* src = x + (((int64_t)n * H + 2 * i + a) * W + 2 * j + b) * xs + c;
+        if (VW == 8) {
+          Vec8<T> v; v.load(src);
+#pragma unroll
+          for (int k = 0; k < VW; ++k) vals[a * 2 + b][k] = v.get(k);
+        } else vals[a * 2 + b][0] = ld1<T>(src);
+#pragma unroll
+        for (int k = 0; k < VW; ++k) {
+          float f = vals[a * 2 + b][k];
+          if (f > best[k] || isnan(f)) { best[k] = f; arg[k] = a * 2 + b; }
+        }
+      }
+    float g[VW];
+    if (VW == 8) { Vec8<T> v; v.load(dy + q * dys + c); for (int k = 0; k < 8; ++k) g[k] = v.get(k); }
+    else g[0] = ld1<T>(dy + q * dys + c);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        int64_t pix = ((int64_t)n * H + 2 * i + a) * W + 2 * j + b;
+        float o[VW];
+        if (add) {
+          if (VW == 8) { Vec8<T> v; v.load(add + pix * adds + c); for (int k = 0; k < 8; ++k) o[k] = v.get(k); }
+          else o[0] = ld1<T>(add + pix * adds + c);
+        } else {
+#pragma unroll
+          for (int k = 0; k < VW; ++k) o[k] = 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < VW; ++k) if (arg[k] == a * 2 + b) o[k] += g[k];
+        if (VW == 8) { Vec8<T> v; for (int k = 0; k < 8; ++k) v.set(k, o[k]); v.store(dx + pix * dxs + c); }
+        else st1<T>(dx + pix * dxs + c, o[0]);
+      }
+  }
+}
+
+// rows/cols of an odd-sized input that no window covers: dx = add (or 0)
+template <typename T>
+__global__ void maxpool_bwd_border(int N, int H, int W, int C, T* dx, int64_t dxs, const T* add, int64_t adds) {
+  int Ho = H >> 1, Wo = W >> 1;
+  int64_t tot = (int64_t)N * H * W * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(e % C);
+    int64_t pix = e / C;
+    int w = (int)(pix % W), h = (int)((pix / W) % H);
+    if (h < 2 * Ho && w < 2 * Wo) continue;
+    st1<T>(dx + pix * dxs + c, add ? ld1<T>(add + pix * adds + c) : 0.f);
+  }
+}
+
+// ---------------------------- bilinear (align_corners) ------------------
+VU_DEV float ac_scale(int in, int out) { return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f; }
+
+VU_DEV void ac_src(int o, float scale, int in, int& i0, int& i1, float& l1) {
+  float src = scale * (float)o;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+}
+
+template <typename T, int VW>
+__global__ void upsample_fwd_kernel(const T* x, int64_t xs, int N, int Hi, int Wi, int C, T* y, int64_t ys,
+                                    int Ho, int Wo, int Hp, int Wp, int py, int px) {
+  float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
+  int V = C / VW;
+  int64_t tot = (int64_t)N * Hp * Wp * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t q = e / V;
+    int c = (int)(e - q * V) * VW;
+    int X = (int)(q % Wp);
+    int64_t t = q / Wp;
+    int Y = (int)(t % Hp);
+    int n = (int)(t / Hp);
+    int oy = Y - py, ox = X - px;
+    float o[VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) o[k] = 0.f;
+    if (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) {
+      int y0, y1, x0, x1; float ly, lx;
+      ac_src(oy, sh, Hi, y0, y1, ly);
+      ac_src(ox, sw, Wi, x0, x1, lx);
+      float hy = 1.f - ly, hx = 1.f - lx;
+      const T* b = x + (int64_t)n * Hi * Wi * xs + c;
+      const T* p00 = b + ((int64_t)y0 * Wi + x0) * xs;
+      const T* p01 = b + ((int64_t)y0 * Wi + x1) * xs;
+      const T* p10 = b + ((int64_t)y1 * Wi + x0) * xs;
+      const T* p11 = b + ((int64_t)y1 * Wi + x1) * xs;
+      if (VW == 8) {
+        Vec8<T> a, bb, cc, d;
+        a.load(p00); bb.load(p01); cc.load(p10); d.load(p11);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          o[k] = hy * (hx * a.get(k) + lx * bb.get(k)) + ly * (hx * cc.get(k) + lx * d.get(k));
+      } else {
+        o[0] = hy * (hx * ld1<T>(p00) + lx * ld1<T>(p01)) + ly * (hx * ld1<T>(p10) + lx * ld1<T>(p11));
+      }
+    }
+    T* dst = y + q * ys + c;
+    if (VW == 8) { Vec8<T> v; for (int k = 0; k < 8; ++k) v.set(k, o[k]); v.store(dst); }
+    else st1<T>(dst, o[0]);
+  }
+}
+
+// weight of input index i in output index o (both terms of the stencil)
+VU_DEV float ac_w(int o, int i, float scale, int in) {
+  int i0, i1; float l1;
+  ac_src(o, scale, in, i0, i1, l1);
+  float w = 0.f;
+  if (i0 == i) w += 1.f - l1;
+  if (i1 == i) w += l1;
+  return w;
+}
+
+VU_DEV void ac_range(int i, float scale, int in, int out, int& lo, int& hi) {
+  if (scale == 0.f) { lo = 0; hi = (i == 0) ? out - 1 : -1; return; }
+  float a = (float)(i - 1) / scale, b = (float)(i + 1) / scale;
+  lo = (int)floorf(a) - 1; hi = (int)ceilf(b) + 1;
+  if (lo < 0) lo = 0;
+  if (hi > out - 1) hi = out - 1;
+}
+
+template <typename T, int VW>
+__global__ void upsample_bwd_kernel(const T* dy, int64_t dys, int N, int Hi, int Wi, int C, T* dx, int64_t dxs,
+                                    int Ho, int Wo, int Hp, int Wp, int py, int px, int accumulate) {
+  float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
+  int V = C / VW;
+  int64_t tot = (int64_t)N * Hi * Wi * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t q = e / V;
+    int c = (int)(e - q * V) * VW;
+    int j = (int)(q % Wi);
+    int64_t t = q / Wi;
+    int i = (int)(t % Hi);
+    int n = (int)(t / Hi);
+    int ylo, yhi, xlo, xhi;
+    ac_range(i, sh, Hi, Ho, ylo, yhi);
+    ac_range(j, sw, Wi, Wo, xlo, xhi);
+    float o[VW];
+#pragma unroll
+    for (int k = 0; k < VW; ++k) o[k] = 0.f;
+    for (int yy = ylo; yy <= yhi; ++yy) {
+      float wy = ac_w(yy, i, sh, Hi);
+      if (wy == 0.f) continue;
+      for (int xx = xlo; xx <= xhi; ++xx) {
+        float wx = ac_w(xx, j, sw, Wi);
+        if (wx == 0.f) continue;
+        const T* src = dy + (((int64_t)n * Hp + yy + py) * Wp + xx + px) * dys + c;
+        float wgt = wy * wx;
+        if (VW == 8) {
+          Vec8<T> v; v.load(src);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += wgt * v.get(k);
+        } else o[0] += wgt * ld1<T>(src);
+      }
+    }
+    T* dst = dx + q * dxs + c;
+    if (VW == 8) {
+      Vec8<T> v;
+      if (accumulate) { v.load(dst); for (int k = 0; k < 8; ++k) o[k] += v.get(k); }
+      for (int k = 0; k < 8; ++k) v.set(k, o[k]);
+      v.store(dst);
+    } else {
+      if (accumulate) o[0] += ld1<T>(dst);
+      st1<T>(dst, o[0]);
+    }
+  }
+}
+
+// ------------------------------ layout helpers ---------------------------
+template <typename TO>
+__global__ void permute4_kernel(const float* in, int64_t base, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                                int d0, int d1, int d2, int d3, int d3v, TO* out) {
+  int64_t tot = (int64_t)d0 * d1 * d2 * d3;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = e;
+    int i3 = (int)(r % d3); r /= d3;
+    int i2 = (int)(r % d2); r /= d2;
+    int i1 = (int)(r % d1);
+    int i0 = (int)(r / d1);
+    st1<TO>(out + e, i3 < d3v ? in[base + i0 * s0 + i1 * s1 + i2 * s2 + i3 * s3] : 0.f);
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void copy_kernel(const TI* x, int64_t xs, TO* y, int64_t ys, int64_t P, int C, int accumulate) {
+  int64_t tot = P * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / C;
+    int c = (int)(e - p * C);
+    float v = ld1<TI>(x + p * xs + c);
+    TO* d = y + p * ys + c;
+    st1<TO>(d, accumulate ? v + ld1<TO>(d) : v);
+  }
+}
+
+template <typename T>
+__global__ void copy8_kernel(const T* x, int64_t xs, T* y, int64_t ys, int64_t P, int C, int accumulate) {
+  int V = C >> 3;
+  int64_t tot = P * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = e / V;
+    int c = (int)(e - p * V) * 8;
+    Vec8<T> v;
+    v.load(x + p * xs + c);
+    if (accumulate) {
+      Vec8<T> w; w.load(y + p * ys + c);
+      for (int k = 0; k < 8; ++k) v.set(k, v.get(k) + w.get(k));
+    }
+    v.store(y + p * ys + c);
+  }
+}
+
+template <typename TO>
+__global__ void input_pack_kernel(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int N, int C,
+                                  int H, int W, int Cp, TO* y) {
+  int64_t tot = (int64_t)N * H * W * Cp;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    int c = (int)(e % Cp);
+    int64_t pix = e / Cp;
+    int w = (int)(pix % W);
+    int64_t t = pix / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float v = c < C ? x[n * sn + c * sc + h * sh + w * sw] : 0.f;
+    st1<TO>(y + e, v);
+  }
+}
+
+}  // namespace
+
+#define DISPATCH_T(dtype, ...) \
+  if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
+
+extern "C" int vu_maxpool2_fwd(const void* x, int64_t xs, int N, int H, int W, int C, void* y, int64_t ys,
+                               int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t work = (int64_t)N * (H / 2) * (W / 2) * C;
+  if (work == 0) return 0;
+  bool vec = C % 8 == 0 && xs % 8 == 0 && ys % 8 == 0;
+  DISPATCH_T(dtype, {
+    if (vec) hipLaunchKernelGGL((maxpool_fwd_kernel<T, 8>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
+                                (const T*)x, xs, N, H, W, C, (T*)y, ys);
+    else hipLaunchKernelGGL((maxpool_fwd_kernel<T, 1>), dim3(ew_grid(work)), dim3(256), 0, st,
+                            (const T*)x, xs, N, H, W, C, (T*)y, ys);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_maxpool2_bwd(const void* x, int64_t xs, const void* dy, int64_t dys, int N, int H, int W, int C,
+                               void* dx, int64_t dxs, const void* add, int64_t adds, int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t work = (int64_t)N * (H / 2) * (W / 2) * C;
+  bool vec = C % 8 == 0 && xs % 8 == 0 && dys % 8 == 0 && dxs % 8 == 0 && (!add || adds % 8 == 0);
+  DISPATCH_T(dtype, {
+    if (work > 0) {
+      if (vec) hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
+                                  (const T*)x, xs, (const T*)dy, dys, N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
+      else hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1>), dim3(ew_grid(work)), dim3(256), 0, st,
+                              (const T*)x, xs, (const T*)dy, dys, N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
+    }
+    if ((H & 1) || (W & 1))
+      hipLaunchKernelGGL((maxpool_bwd_border<T>), dim3(ew_grid((int64_t)N * H * W * C)), dim3(256), 0, st,
+                         N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_upsample_fwd(const void* x, int64_t xs, int N, int Hi, int Wi, int C, void* y, int64_t ys,
+                               int Ho, int Wo, int Hp, int Wp, int py, int px, int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t work = (int64_t)N * Hp * Wp * C;
+  if (work == 0) return 0;
+  bool vec = C % 8 == 0 && xs % 8 == 0 && ys % 8 == 0;
+  DISPATCH_T(dtype, {
+    if (vec) hipLaunchKernelGGL((upsample_fwd_kernel<T, 8>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
+                                (const T*)x, xs, N, Hi, Wi, C, (T*)y, ys, Ho, Wo, Hp, Wp, py, px);
+    else hipLaunchKernelGGL((upsample_fwd_kernel<T, 1>), dim3(ew_grid(work)), dim3(256), 0, st,
+                            (const T*)x, xs, N, Hi, Wi, C, (T*)y, ys, Ho, Wo, Hp, Wp, py, px);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_upsample_bwd(const void* dy, int64_t dys, int N, int Hi, int Wi, int C, void* dx, int64_t dxs,
+                               int Ho, int Wo, int Hp, int Wp, int py, int px, int accumulate, int dtype,
+                               void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t work = (int64_t)N * Hi * Wi * C;
+  if (work == 0) return 0;
+  bool vec = C % 8 == 0 && dys % 8 == 0 && dxs % 8 == 0;
+  DISPATCH_T(dtype, {
+    if (vec) hipLaunchKernelGGL((upsample_bwd_kernel<T, 8>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
+                                (const T*)dy, dys, N, Hi, Wi, C, (T*)dx, dxs, Ho, Wo, Hp, Wp, py, px, accumulate);
+    else hipLaunchKernelGGL((upsample_bwd_kernel<T, 1>), dim3(ew_grid(work)), dim3(256), 0, st,
+                            (const T*)dy, dys, N, Hi, Wi, C, (T*)dx, dxs, Ho, Wo, Hp, Wp, py, px, accumulate);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1, int64_t s2, int64_t s3, int d0,
+                           int d1, int d2, int d3, int d3v, void* out, int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t tot = (int64_t)d0 * d1 * d2 * d3;
+  if (tot == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((permute4_kernel<T>), dim3(ew_grid(tot)), dim3(256), 0, st, in, base, s0, s1, s2, s3, d0, d1,
+                       d2, d3, d3v, (T*)out);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys, int ydtype, int64_t P, int C,
+                       int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t tot = P * C;
+  if (tot == 0) return 0;
+  if (xdtype == ydtype && C % 8 == 0 && xs % 8 == 0 && ys % 8 == 0) {
+    DISPATCH_T(xdtype, {
+      hipLaunchKernelGGL((copy8_kernel<T>), dim3(ew_grid(tot / 8)), dim3(256), 0, st, (const T*)x, xs, (T*)y, ys, P,
+                         C, accumulate);
+    })
+  } else if (xdtype == VU_BF16) {
+    if (ydtype == VU_BF16)
+      hipLaunchKernelGGL((copy_kernel<bf16_t, bf16_t>), dim3(ew_grid(tot)), dim3(256), 0, st, (const bf16_t*)x, xs,
+                         (bf16_t*)y, ys, P, C, accumulate);
+    else
+      hipLaunchKernelGGL((copy_kernel<bf16_t, float>), dim3(ew_grid(tot)), dim3(256), 0, st, (const bf16_t*)x, xs,
+                         (float*)y, ys, P, C, accumulate);
+  } else {
+    if (ydtype == VU_BF16)
+      hipLaunchKernelGGL((copy_kernel<float, bf16_t>), dim3(ew_grid(tot)), dim3(256), 0, st, (const float*)x, xs,
+                         (bf16_t*)y, ys, P, C, accumulate);
+    else
+      hipLaunchKernelGGL((copy_kernel<float, float>), dim3(ew_grid(tot)), dim3(256), 0, st, (const float*)x, xs,
+                         (float*)y, ys, P, C, accumulate);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_input_pack(const float* x, int64_t sn, int64_t sc, int64_t sh, int64_t sw, int N, int C, int H,
+                             int W, int Cp, void* y, int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int64_t tot = (int64_t)N * H * W * Cp;
+  if (tot == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((input_pack_kernel<T>), dim3(ew_grid(tot)), dim3(256), 0, st, x, sn, sc, sh, sw, N, C, H, W,
+                       Cp, (T*)y);
+  })
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,455 @@
+"""Fused forward / backward sequences of the reference's building blocks.
+
+Each function here restates, as a sequence of HIP kernel launches, one block
+of the reference (file:line cited per function).  The nn.Module classes in
+unet_parts.py / unet_model.py / unet_resnet.py own the parameters (same
+attribute tree and state_dict keys as the reference) and call these through
+torch.autograd.Function wrappers, so ``model(x)``, ``loss.backward()`` and
+``optimizer.step()`` stay drop-in.
+
+Parameter gradients are written straight into ``param.grad`` by the weight-
+gradient kernels (allocated on first use, accumulated afterwards — the
+gradient-accumulation semantics of train.py:401-411); the autograd Functions
+return None for parameters.  A ``grad_ready`` hook on the run mode lets the
+data-parallel reducer start all-reducing a block's gradients while the
+backward of the blocks below it is still running.
+"""
+import torch
+
+from . import kernels as K
+from ._lib import BF16, F32
+
+
+class Mode:
+    """Per-call execution mode: storage dtype and training flag."""
+
+    def __init__(self, dtype_code, device, grad_ready=None):
+        self.d = dtype_code
+        self.tdtype = torch.bfloat16 if dtype_code == BF16 else torch.float32
+        self.device = device
+        self.grad_ready = grad_ready
+
+    def act(self, N, Cc, H, W):
+        return K.empty_act(N, Cc, H, W, self.tdtype, self.device)
+
+    def zeros(self, N, Cc, H, W):
+        return K.zeros_act(N, Cc, H, W, self.tdtype, self.device)
+
+    def notify(self, params):
+        if self.grad_ready is not None:
+            self.grad_ready([p for p in params if p is not None and p.grad is not None])
+
+
+def current_mode(device, grad_ready=None):
+    """bf16 under torch.autocast (train.py:385), fp32 otherwise (parity)."""
+    if device.type != "cuda":
+        raise RuntimeError("vaeunet_amd runs on MI355X (HIP) devices only; got "
+                           f"a tensor on {device}")
+    ac = torch.is_autocast_enabled("cuda")
+    return Mode(BF16 if ac else F32, device, grad_ready)
+
+
+# ----------------------------------------------------------------------------
+# weight preparation (derived, version-keyed caches; the fp32 parameter stays
+# the single source of truth so state_dict / optimizer semantics are intact)
+# ----------------------------------------------------------------------------
+def _cached(p, key, build):
+    cache = p.__dict__.setdefault("_vu_cache", {})
+    ent = cache.get(key)
+    ver = (p._version, p.data_ptr())
+    if ent is None or ent[0] != ver:
+        ent = (ver, build())
+        cache[key] = ent
+    return ent[1]
+
+
+def w3x3_fwd(w, d, cin_pad=None):
+    """[Cout, Cin, R, S] -> B[Cout][(r*S+s)*Cp + c] (Cp >= Cin zero padded)."""
+    co, ci, R, S = w.shape
+    cp = cin_pad or ci
+
+    def build():
+        s = w.stride()
+        return K.permute4(w.detach(), 0, (s[0], s[2], s[3], s[1]), (co, R, S, cp), ci, d).view(co, -1)
+    return _cached(w, ("w3f", d, cp), build)
+
+
+def w3x3_dgrad(w, d):
+    """Input-gradient weights: B[ci][(r'*S+s')*Cout + co] = W[co][ci][R-1-r'][S-1-s']."""
+    co, ci, R, S = w.shape
+
+    def build():
+        s = w.stride()
+        base = (R - 1) * s[2] + (S - 1) * s[3]
+        return K.permute4(w.detach(), base, (s[1], -s[2], -s[3], s[0]), (ci, R, S, co), co, d).view(ci, -1)
+    return _cached(w, ("w3d", d), build)
+
+
+def w1x1_fwd(w, d):
+    co, ci = w.shape[0], w.shape[1]
+
+    def build():
+        s = w.stride()
+        return K.permute4(w.detach(), 0, (s[0], s[1], 0, 0), (co, ci, 1, 1), 1, d).view(co, ci)
+    return _cached(w, ("w1f", d), build)
+
+
+def w1x1_dgrad(w, d):
+    co, ci = w.shape[0], w.shape[1]
+
+    def build():
+        s = w.stride()
+        return K.permute4(w.detach(), 0, (s[1], s[0], 0, 0), (ci, co, 1, 1), 1, d).view(ci, co)
+    return _cached(w, ("w1d", d), build)
+
+
+def wT_fwd(w, d):
+    """ConvTranspose2d weight [Cin, Cout, 2, 2] -> B[(a*2+b)*Cout + co][ci]."""
+    ci, co = w.shape[0], w.shape[1]
+
+    def build():
+        s = w.stride()
+        return K.permute4(w.detach(), 0, (s[2], s[3], s[1], s[0]), (2, 2, co, ci), ci, d).view(4 * co, ci)
+    return _cached(w, ("wTf", d), build)
+
+
+def wT_dgrad(w, d):
+    """-> B[ci][(a*2+b)*Cout + co] (gather of the 2x2 output sub-pixels)."""
+    ci, co = w.shape[0], w.shape[1]
+
+    def build():
+        s = w.stride()
+        return K.permute4(w.detach(), 0, (s[0], s[2], s[3], s[1]), (ci, 2, 2, co), co, d).view(ci, 4 * co)
+    return _cached(w, ("wTd", d), build)
+
+
+# ----------------------------------------------------------------------------
+# gradient sinks
+# ----------------------------------------------------------------------------
+def grad_sink(p):
+    """(tensor, accumulate) for writing d(loss)/dp, or (None, False) if frozen."""
+    if p is None or not p.requires_grad:
+        return None, False
+    if p.grad is None:
+        p.grad = torch.empty_like(p)
+        return p.grad, False
+    return p.grad, True
+
+
+def conv_layout(g):
+    """wgrad output layout (s_i, s_tap, s_c) of a [Cout, Cin, R, S] gradient."""
+    s = g.stride()
+    if g.shape[2] > 1 and s[2] != g.shape[3] * s[3]:
+        raise ValueError("unsupported weight-gradient strides")
+    return (s[0], s[3], s[1])
+
+
+def convT_layout(g):
+    s = g.stride()
+    if s[2] != 2 * s[3]:
+        raise ValueError("unsupported ConvTranspose weight-gradient strides")
+    return (s[0], s[3], s[1])
+
+
+def wgrad3x3(dy, srcs, w, M, cvalid=None):
+    g, acc = grad_sink(w)
+    if g is None:
+        return
+    co = dy.shape[1]
+    cin = sum(s.shape[1] for s in srcs)
+    K.gemm_wgrad(K.gather1x1([dy]), K.gather3x3(srcs), co, 9 * cin, g, conv_layout(g), M.d, acc,
+                 cvalid=cvalid)
+
+
+def wgrad1x1(dy, srcs, w, M):
+    g, acc = grad_sink(w)
+    if g is None:
+        return
+    cin = sum(s.shape[1] for s in srcs)
+    K.gemm_wgrad(K.gather1x1([dy]), K.gather1x1(srcs), dy.shape[1], cin, g, conv_layout(g), M.d, acc)
+
+
+def bias_grad(dy, b, M, window=None):
+    g, acc = grad_sink(b)
+    if g is not None:
+        K.chan_sum(dy, g, acc, M.d, window)
+
+
+# ----------------------------------------------------------------------------
+# BatchNorm2d: stats from the GEMM epilogue -> (scale, shift, mean, invstd)
+# ----------------------------------------------------------------------------
+def bn_coef(bn, st, C_):
+    if bn.training:
+        if st is None:
+            raise RuntimeError("train-mode BatchNorm needs GEMM statistics")
+        mom = 0.1 if bn.momentum is None else bn.momentum
+        track = bn.track_running_stats and bn.running_mean is not None
+        return K.bn_finalize(st, C_, bn.weight, bn.bias,
+                             bn.running_mean if track else None,
+                             bn.running_var if track else None,
+                             bn.num_batches_tracked if track else None, mom if track else 0.0,
+                             bn.eps)
+    return K.bn_eval(C_, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+
+
+def bn_bwd(dy, x, coef, bn, relu, M, dx=None):
+    if not bn.training:
+        raise NotImplementedError("backward through eval-mode BatchNorm")
+    gw, accw = grad_sink(bn.weight)
+    gb, accb = grad_sink(bn.bias)
+    if gw is not None and gb is not None and accw != accb:
+        raise RuntimeError("inconsistent BatchNorm grad state")
+    if dx is None:
+        dx = torch.empty_like(x)
+    K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, accw or accb, dx, K.dcode(x.dtype))
+    return dx
+
+
+# ----------------------------------------------------------------------------
+# DoubleConv  (unet_parts.py:32-49; DecoderBlock conv1/conv2 unet_resnet.py:59-69)
+#   conv3x3(no bias) -> BN -> ReLU -> conv3x3(no bias) -> BN -> ReLU
+# ----------------------------------------------------------------------------
+def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None):
+    N, _, H, W = srcs[0].shape
+    co = conv.out_channels
+    y = M.act(N, co, H, W)
+    st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad), co, y, M.d,
+                    stats=bn.training)
+    coef = bn_coef(bn, st, co)
+    a = M.act(N, co, H, W)
+    K.bn_apply(y, a, coef, True, M.d)
+    return a, (y, coef)
+
+
+def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False):
+    y, coef = saved
+    dy = bn_bwd(da, y, coef, bn, True, M)
+    wgrad3x3(dy, srcs, conv.weight, M, cvalid)
+    M.notify([conv.weight, bn.weight, bn.bias])
+    if not need_dsrc:
+        return None
+    N, _, H, W = y.shape
+    # a channel-padded input (the 3-channel image) gets a gradient for its
+    # real channels only: the dgrad weights have conv.in_channels rows
+    cin = conv.in_channels
+    if dsrc is None:
+        dsrc = M.act(N, cin, H, W)
+    K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d), cin, dsrc, M.d, accumulate=dsrc_acc)
+    return dsrc
+
+
+def double_conv_fwd(M, seq, srcs, cin_pad=None):
+    conv1, bn1, _, conv2, bn2, _ = seq
+    a1, s1 = conv_bn_relu_fwd(M, srcs, conv1, bn1, cin_pad)
+    a2, s2 = conv_bn_relu_fwd(M, [a1], conv2, bn2)
+    return a2, (srcs, a1, s1, s2)
+
+
+def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None):
+    conv1, bn1, _, conv2, bn2, _ = seq
+    srcs, a1, s1, s2 = saved
+    da1 = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True)
+    return conv_bn_relu_bwd(M, srcs, conv1, bn1, s1, da1, need_dsrc, cvalid)
+
+
+# ----------------------------------------------------------------------------
+# Down (unet_parts.py:51-63): MaxPool2d(2) -> DoubleConv
+# ----------------------------------------------------------------------------
+def down_fwd(M, mod, x):
+    seq = mod.maxpool_conv[1].double_conv
+    xp = K.maxpool_fwd(x, M.d)
+    out, sdc = double_conv_fwd(M, seq, [xp])
+    return out, (x, sdc)
+
+
+def down_bwd(M, mod, saved, dout, add=None):
+    x, sdc = saved
+    seq = mod.maxpool_conv[1].double_conv
+    dxp = double_conv_bwd(M, seq, sdc, dout, True)
+    dx = torch.empty_like(x)
+    K.maxpool_bwd(x, dxp, dx, add, M.d)
+    return dx
+
+
+# ----------------------------------------------------------------------------
+# AttentionGate (unet_parts.py:7-30): x * sigmoid(BN(psi(relu(BN(W_g g) + BN(W_x x)))))
+# ----------------------------------------------------------------------------
+def attention_fwd(M, att, g, x):
+    N, _, H, W = x.shape
+    P = N * H * W
+    wg, bng = att.W_g[0], att.W_g[1]
+    wx, bnx = att.W_x[0], att.W_x[1]
+    wp, bnp = att.psi[0], att.psi[1]
+    F = wg.out_channels
+    ug = M.act(N, F, H, W)
+    stg = K.gemm_fwd(K.gather1x1([g]), w1x1_fwd(wg.weight, M.d), F, ug, M.d, bias=wg.bias,
+                     stats=bng.training)
+    ux = M.act(N, F, H, W)
+    stx = K.gemm_fwd(K.gather1x1([x]), w1x1_fwd(wx.weight, M.d), F, ux, M.d, bias=wx.bias,
+                     stats=bnx.training)
+    cg = bn_coef(bng, stg, F)
+    cx = bn_coef(bnx, stx, F)
+    tile = K.query("vu_attn_tile_rows")
+    tiles = (P + tile - 1) // tile
+    q = torch.empty((N, 1, H, W), dtype=torch.float32, device=x.device)
+    psum = torch.empty(tiles, dtype=torch.float32, device=x.device)
+    pm2 = torch.empty_like(psum)
+    K.call("vu_attn_psi_fwd", K.ptr(ug), K.ptr(ux), P, F, K.ptr(cg[0]), K.ptr(cg[1]), K.ptr(cx[0]),
+           K.ptr(cx[1]), K.ptr(wp.weight), K.ptr(wp.bias), K.ptr(q), K.ptr(psum), K.ptr(pm2), tile,
+           M.d, K.stream())
+    cq = bn_coef(bnp, K.Stats(psum.view(tiles, 1), pm2.view(tiles, 1), tiles, tile, P), 1)
+    pmap = torch.empty((N, 1, H, W), dtype=torch.float32, device=x.device)
+    out = M.act(N, x.shape[1], H, W)
+    K.call("vu_attn_gate_fwd", K.ptr(q), K.ptr(cq), K.ptr(x), K.pstride(x), P, x.shape[1],
+           K.ptr(pmap), K.ptr(out), K.pstride(out), M.d, K.stream())
+    _fire_psi_hooks(att.psi, pmap)
+    return out, (g, x, ug, ux, cg, cx, q, cq, pmap)
+
+
+def _fire_psi_hooks(psi, pmap):
+    """analyze_model.py:733-736 hooks AttentionGate.psi; keep them firing."""
+    if psi._forward_hooks:
+        for hook in list(psi._forward_hooks.values()):
+            hook(psi, (None,), pmap)
+
+
+def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
+    """Returns dx (skip gradient); adds the gate-input gradient into dg_out."""
+    g, x, ug, ux, cg, cx, q, cq, pmap = saved
+    N, _, H, W = x.shape
+    P = N * H * W
+    wg, bng = att.W_g[0], att.W_g[1]
+    wx, bnx = att.W_x[0], att.W_x[1]
+    wp, bnp = att.psi[0], att.psi[1]
+    F = wg.out_channels
+    dx = torch.empty_like(x)
+    dbnq = torch.empty((N, 1, H, W), dtype=torch.float32, device=x.device)
+    K.call("vu_attn_gate_bwd", K.ptr(dout), K.pstride(dout), K.ptr(x), K.pstride(x), K.ptr(pmap),
+           P, x.shape[1], K.ptr(dx), K.pstride(dx), K.ptr(dbnq), M.d, K.stream())
+    # BatchNorm2d(1) backward (fp32 single channel)
+    gw, accw = grad_sink(bnp.weight)
+    gb, _ = grad_sink(bnp.bias)
+    dq = torch.empty_like(q)
+    K.bn_backward(dbnq, q, cq, bnp.weight, False, gw, gb, accw, dq, F32)
+    # psi conv + ReLU backward -> ds (grad of g1 + x1)
+    ds = M.act(N, F, H, W)
+    gwp, accp = grad_sink(wp.weight)
+    gbp, _ = grad_sink(wp.bias)
+    ws = K.workspace_f32(K.query("vu_attn_psi_bwd_workspace_bytes", P, F), x.device)
+    K.call("vu_attn_psi_bwd", K.ptr(ug), K.ptr(ux), P, F, K.ptr(cg[0]), K.ptr(cg[1]),
+           K.ptr(cx[0]), K.ptr(cx[1]), K.ptr(wp.weight), K.ptr(dq), K.ptr(ds), K.ptr(gwp),
+           K.ptr(gbp), 1 if accp else 0, K.ptr(ws), M.d, K.stream())
+    dug = bn_bwd(ds, ug, cg, bng, False, M)
+    dux = bn_bwd(ds, ux, cx, bnx, False, M)
+    wgrad1x1(dug, [g], wg.weight, M)
+    bias_grad(dug, wg.bias, M)
+    wgrad1x1(dux, [x], wx.weight, M)
+    bias_grad(dux, wx.bias, M)
+    M.notify([wg.weight, wg.bias, wx.weight, wx.bias, wp.weight, wp.bias, bng.weight, bng.bias,
+              bnx.weight, bnx.bias, bnp.weight, bnp.bias])
+    # input gradients of the two 1x1 convs
+    if dg_out is not None:
+        dst, coff = dg_out
+        K.gemm_fwd(K.gather1x1([dug]), w1x1_dgrad(wg.weight, M.d), g.shape[1], dst, M.d,
+                   out_coff=coff, accumulate=dg_acc)
+    K.gemm_fwd(K.gather1x1([dux]), w1x1_dgrad(wx.weight, M.d), x.shape[1], dx, M.d, accumulate=True)
+    return dx
+
+
+# ----------------------------------------------------------------------------
+# Up (unet_parts.py:65-95): up(x1) -> F.pad -> attention(x1, x2) -> cat([x2, x1]) -> DoubleConv
+# ----------------------------------------------------------------------------
+def up_fwd(M, mod, x1, x2):
+    N, _, H, W = x2.shape
+    h, w = x1.shape[2], x1.shape[3]
+    bilinear = isinstance(mod.up, torch.nn.Upsample)
+    uh, uw = 2 * h, 2 * w
+    dy_, dx_ = H - uh, W - uw
+    if dy_ < 0 or dx_ < 0:
+        raise NotImplementedError("Up with an upsampled map larger than the skip (negative pad)")
+    py, px = dy_ // 2, dx_ // 2
+    if bilinear:
+        cu = x1.shape[1]
+        u = M.act(N, cu, H, W)
+        K.upsample_fwd(x1, u, uh, uw, py, px, M.d)
+    else:
+        cu = mod.up.out_channels
+        u = M.zeros(N, cu, H, W) if (dy_ or dx_) else M.act(N, cu, H, W)
+        K.gemm_fwd(K.gather1x1([x1]), wT_fwd(mod.up.weight, M.d), 4 * cu, u, M.d,
+                   bias=mod.up.bias, convT=(H, W, py, px, cu))
+    x2a, satt = attention_fwd(M, mod.attention, u, x2)
+    out, sdc = double_conv_fwd(M, mod.conv.double_conv, [x2a, u])
+    return out, (x1, x2, u, (py, px, uh, uw), satt, sdc)
+
+
+def up_bwd(M, mod, saved, dout):
+    x1, x2, u, (py, px, uh, uw), satt, sdc = saved
+    N, cs, H, W = x2.shape
+    cu = u.shape[1]
+    dcat = double_conv_bwd(M, mod.conv.double_conv, sdc, dout, True)
+    dx2a = dcat[:, :cs]
+    du = dcat[:, cs:]
+    dx2 = attention_bwd(M, mod.attention, satt, dx2a, (dcat, cs), True)
+    h, w = x1.shape[2], x1.shape[3]
+    if isinstance(mod.up, torch.nn.Upsample):
+        dx1 = torch.empty_like(x1)
+        K.upsample_bwd(du, dx1, uh, uw, py, px, False, M.d)
+    else:
+        g, acc = grad_sink(mod.up.weight)
+        if g is not None:
+            K.gemm_wgrad(K.gather1x1([x1]), K.gather_convT(du, N, h, w, py, px), x1.shape[1], 4 * cu,
+                         g, convT_layout(g), M.d, acc)
+        bias_grad(du, mod.up.bias, M, window=(py, px, uh, uw))
+        M.notify([mod.up.weight, mod.up.bias])
+        dx1 = torch.empty_like(x1)
+        K.gemm_fwd(K.gather_convT(du, N, h, w, py, px), wT_dgrad(mod.up.weight, M.d), x1.shape[1],
+                   dx1, M.d)
+    return dx1, dx2
+
+
+# ----------------------------------------------------------------------------
+# OutConv (unet_parts.py:97-103): 1x1 conv + bias, fp32 logits
+# ----------------------------------------------------------------------------
+def outconv_fwd(M, conv, x):
+    N, Cc, H, W = x.shape
+    J = conv.out_channels
+    y = torch.empty((N, J, H, W), dtype=torch.float32, device=x.device, memory_format=K.CL)
+    K.call("vu_pointwise_fwd", K.ptr(x), K.pstride(x), N * H * W, Cc, J, K.ptr(conv.weight),
+           K.ptr(conv.bias), K.ptr(y), J, M.d, K.stream())
+    return y, (x,)
+
+
+def outconv_bwd(M, conv, saved, dy):
+    (x,) = saved
+    N, Cc, H, W = x.shape
+    J = conv.out_channels
+    dy = dy.float().contiguous(memory_format=K.CL)
+    gw, acc = grad_sink(conv.weight)
+    gb, _ = grad_sink(conv.bias)
+    dx = torch.empty_like(x)
+    ws = K.workspace_f32(K.query("vu_pointwise_bwd_workspace_bytes", N * H * W, Cc, J), x.device)
+    K.call("vu_pointwise_bwd", K.ptr(x), K.pstride(x), K.ptr(dy), J, N * H * W, Cc, J,
+           K.ptr(conv.weight), K.ptr(dx), K.pstride(dx), K.ptr(gw), K.ptr(gb), 1 if acc else 0,
+           K.ptr(ws), M.d, K.stream())
+    M.notify([conv.weight, conv.bias])
+    return dx
+
+
+# ----------------------------------------------------------------------------
+# external tensors -> NHWC storage
+# ----------------------------------------------------------------------------
+def to_act(M, x, cpad=None):
+    """Bring a caller tensor into NHWC storage of the mode's dtype (padding the
+    channel count to a multiple of 8 for the 3-channel image input)."""
+    N, Cc, H, W = x.shape
+    cp = cpad or Cc
+    if cp == Cc and x.dtype == M.tdtype and x.is_contiguous(memory_format=K.CL):
+        return x
+    return K.input_pack(x, cp, M.d)
+
+
+def from_act(dx, like):
+    """Gradient for a caller tensor of shape/dtype ``like``."""
+    if dx.shape[1] != like.shape[1]:
+        dx = dx[:, :like.shape[1]]
+    return dx.to(dtype=like.dtype)

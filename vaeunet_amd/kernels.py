@@ -1,0 +1,251 @@
+"""Host-side wrappers: torch tensors (device memory) -> C-ABI calls.
+
+Activations are torch tensors of logical shape [N, C, H, W] in
+``channels_last`` memory format, i.e. NHWC in HBM; a channel slice of such a
+tensor is still a valid NHWC view with a pixel stride (that is how the
+channel concat of unet_parts.py:94 is addressed without a copy).  Every
+function launches on the current HIP stream and never synchronises.
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import ptr, call, query, stream, VuGather, VuGemmFwd, VuGemmWgrad
+
+CL = torch.channels_last
+
+
+def dcode(dtype):
+    if dtype == torch.bfloat16:
+        return _lib.BF16
+    if dtype == torch.float32:
+        return _lib.F32
+    raise TypeError(f"unsupported activation dtype {dtype}")
+
+
+def empty_act(N, Cc, H, W, dtype, device):
+    return torch.empty((N, Cc, H, W), dtype=dtype, device=device, memory_format=CL)
+
+
+def zeros_act(N, Cc, H, W, dtype, device):
+    return torch.zeros((N, Cc, H, W), dtype=dtype, device=device, memory_format=CL)
+
+
+def pstride(t):
+    """Pixel stride (elements) of an NHWC view; validates the layout."""
+    N, Cc, H, W = t.shape
+    s = t.stride()
+    if Cc > 1 and s[1] != 1:
+        raise ValueError("activation must be channels_last (NHWC)")
+    ps = s[3] if W > 1 else (s[2] if H > 1 else (s[0] if N > 1 else Cc))
+    if W > 1 and H > 1 and s[2] != W * ps:
+        raise ValueError("non-dense NHWC view")
+    return ps
+
+
+def gather(srcs, N, H, W, R=1, S=1, sy=1, sx=1, dy=1, dx=1, oy=0, ox=0, Hs=None, Ws=None):
+    g = VuGather()
+    if not 1 <= len(srcs) <= 3:
+        raise ValueError("1..3 channel sources")
+    cend = 0
+    for i, t in enumerate(srcs):
+        g.src[i] = t.data_ptr()
+        g.stride[i] = pstride(t)
+        cend += t.shape[1]
+        g.cend[i] = cend
+    for i in range(len(srcs), 3):
+        g.src[i] = None
+        g.stride[i] = 0
+        g.cend[i] = cend
+    g.nsrc, g.C = len(srcs), cend
+    g.N, g.H, g.W = N, H, W
+    g.Hs = srcs[0].shape[2] if Hs is None else Hs
+    g.Ws = srcs[0].shape[3] if Ws is None else Ws
+    g.R, g.S, g.sy, g.sx, g.dy, g.dx, g.oy, g.ox = R, S, sy, sx, dy, dx, oy, ox
+    return g
+
+
+def gather3x3(srcs):
+    N, _, H, W = srcs[0].shape
+    return gather(srcs, N, H, W, R=3, S=3, oy=-1, ox=-1)
+
+
+def gather1x1(srcs):
+    N, _, H, W = srcs[0].shape
+    return gather(srcs, N, H, W)
+
+
+def gather_convT(du, N, h, w, py=0, px=0):
+    """A[m=(n,i,j)][k=(a*2+b)*C + c] = du[n, 2i+a+py, 2j+b+px, c]."""
+    return gather([du], N, h, w, R=2, S=2, sy=2, sx=2, oy=py, ox=px)
+
+
+class Stats:
+    """Per-row-tile BatchNorm partials produced by a GEMM epilogue."""
+
+    def __init__(self, psum, pm2, tiles, tile_rows, rows):
+        self.psum, self.pm2, self.tiles, self.tile_rows, self.rows = psum, pm2, tiles, tile_rows, rows
+
+
+def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
+             convT=None):
+    """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
+    the pixel-shuffle epilogue.  Returns Stats if requested."""
+    a = VuGemmFwd()
+    a.a = g
+    a.b = wmat.data_ptr()
+    a.ldb = wmat.shape[-1] if wmat.dim() == 2 else wmat.stride(0)
+    a.ncol = ncol
+    a.out = out.data_ptr()
+    a.out_stride = pstride(out)
+    a.out_coff = out_coff
+    if convT is not None:
+        a.out_mode = 1
+        a.oH, a.oW, a.opy, a.opx, a.cout = convT
+    else:
+        a.out_mode = 0
+    a.bias = bias.data_ptr() if bias is not None else None
+    a.accumulate = 1 if accumulate else 0
+    st = None
+    if stats:
+        rows = g.N * g.H * g.W
+        bm = query("vu_gemm_fwd_row_tile", C.byref(a), dtype)
+        tiles = (rows + bm - 1) // bm
+        psum = torch.empty((tiles, ncol), dtype=torch.float32, device=out.device)
+        pm2 = torch.empty_like(psum)
+        a.stat_sum, a.stat_m2 = psum.data_ptr(), pm2.data_ptr()
+        st = Stats(psum, pm2, tiles, bm, rows)
+    else:
+        a.stat_sum = a.stat_m2 = None
+    call("vu_gemm_fwd", C.byref(a), dtype, stream())
+    return st
+
+
+def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
+    """grad[i*s_i + (j//Cq)*s_tap + (j%Cq)*s_c] (+)= sum_m P[m][i] Q[m][j]."""
+    M = gp.N * gp.H * gp.W
+    bi = 64 if ni <= 64 else 128
+    tiles = ((ni + bi - 1) // bi) * ((nj + 127) // 128)
+    steps = (M + 63) // 64
+    splits = max(1, min(-(-1024 // tiles), steps // 4 if steps >= 8 else 1, 256))
+    mps = ((-(-M // splits)) + 63) // 64 * 64
+    splits = -(-M // mps)
+    slab = torch.empty((splits, ni, nj), dtype=torch.float32, device=grad.device)
+    w = VuGemmWgrad()
+    w.p, w.q, w.ni, w.nj, w.splits, w.m_per_split = gp, gq, ni, nj, splits, mps
+    w.out = slab.data_ptr()
+    call("vu_gemm_wgrad", C.byref(w), dtype, stream())
+    s_i, s_tap, s_c = layout
+    call("vu_slab_reduce", ptr(slab), splits, ni, nj, gq.C, gq.C if cvalid is None else cvalid,
+         s_i, s_tap, s_c, ptr(grad),
+         1 if accumulate else 0, stream())
+    return slab
+
+
+def permute4(src, base, strides, dims, d3v, dtype):
+    out = torch.empty(dims, dtype=torch.bfloat16 if dtype == _lib.BF16 else torch.float32,
+                      device=src.device)
+    call("vu_permute4", ptr(src), base, *strides, *dims, d3v, ptr(out), dtype, stream())
+    return out
+
+
+def bn_finalize(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps):
+    dev = st.psum.device
+    coef = torch.empty((4, C_), dtype=torch.float32, device=dev)
+    ws = torch.empty(query("vu_bn_finalize_workspace_bytes", st.tiles, C_) // 4 + 1,
+                     dtype=torch.float32, device=dev)
+    call("vu_bn_finalize", ptr(st.psum), ptr(st.pm2), st.tiles, st.tile_rows, st.rows, C_,
+         ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), momentum, eps,
+         ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(nbt), ptr(ws), stream())
+    return coef  # rows: scale, shift, mean, invstd
+
+
+def bn_eval(C_, gamma, beta, rmean, rvar, eps):
+    coef = torch.empty((4, C_), dtype=torch.float32, device=rmean.device)
+    call("vu_bn_eval_coeffs", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), eps, C_,
+         ptr(coef[0]), ptr(coef[1]), stream())
+    return coef
+
+
+def bn_apply(x, y, coef, relu, dtype):
+    N, Cc, H, W = x.shape
+    call("vu_bn_apply", ptr(x), pstride(x), ptr(y), pstride(y), N * H * W, Cc,
+         ptr(coef[0]), ptr(coef[1]), 1 if relu else 0, dtype, stream())
+    return y
+
+
+def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype):
+    """dx = BN(+ReLU) backward; writes/accumulates dgamma, dbeta."""
+    N, Cc, H, W = x.shape
+    P = N * H * W
+    dev = x.device
+    k = torch.empty((3, Cc), dtype=torch.float32, device=dev)
+    ws = torch.empty(query("vu_reduce_workspace_bytes", P, Cc) // 4 + 1, dtype=torch.float32,
+                     device=dev)
+    call("vu_bn_bwd_reduce", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
+         ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
+         ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype, stream())
+    call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
+         ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
+         stream())
+    return dx
+
+
+def chan_sum(x, out, acc, dtype, window=None):
+    N, Cc, H, W = x.shape
+    y0, x0, Hr, Wr = window if window is not None else (0, 0, H, W)
+    ws = torch.empty(query("vu_reduce_workspace_bytes", N * Hr * Wr, Cc) // 4 + 1,
+                     dtype=torch.float32, device=x.device)
+    call("vu_chan_sum", ptr(x), pstride(x), N, H, W, y0, x0, Hr, Wr, Cc, ptr(out),
+         1 if acc else 0, ptr(ws), dtype, stream())
+
+
+def copy(x, y, accumulate=False):
+    N, Cc, H, W = x.shape
+    call("vu_copy", ptr(x), pstride(x), dcode(x.dtype), ptr(y), pstride(y), dcode(y.dtype),
+         N * H * W, Cc, 1 if accumulate else 0, stream())
+
+
+def input_pack(x, Cp, dtype):
+    N, Cc, H, W = x.shape
+    if x.dtype != torch.float32:
+        x = x.float()
+    y = empty_act(N, Cp, H, W, torch.bfloat16 if dtype == _lib.BF16 else torch.float32, x.device)
+    s = x.stride()
+    call("vu_input_pack", ptr(x), s[0], s[1], s[2], s[3], N, Cc, H, W, Cp, ptr(y), dtype, stream())
+    return y
+
+
+def maxpool_fwd(x, dtype):
+    N, Cc, H, W = x.shape
+    y = empty_act(N, Cc, H // 2, W // 2, x.dtype, x.device)
+    call("vu_maxpool2_fwd", ptr(x), pstride(x), N, H, W, Cc, ptr(y), pstride(y), dtype, stream())
+    return y
+
+
+def maxpool_bwd(x, dy, dx, add, dtype):
+    N, Cc, H, W = x.shape
+    call("vu_maxpool2_bwd", ptr(x), pstride(x), ptr(dy), pstride(dy), N, H, W, Cc, ptr(dx),
+         pstride(dx), ptr(add), pstride(add) if add is not None else 0, dtype, stream())
+    return dx
+
+
+def upsample_fwd(x, out, Ho, Wo, py, px, dtype):
+    N, Cc, Hi, Wi = x.shape
+    Hp, Wp = out.shape[2], out.shape[3]
+    call("vu_upsample_fwd", ptr(x), pstride(x), N, Hi, Wi, Cc, ptr(out), pstride(out), Ho, Wo,
+         Hp, Wp, py, px, dtype, stream())
+    return out
+
+
+def upsample_bwd(dy, dx, Ho, Wo, py, px, accumulate, dtype):
+    N, Cc, Hi, Wi = dx.shape
+    Hp, Wp = dy.shape[2], dy.shape[3]
+    call("vu_upsample_bwd", ptr(dy), pstride(dy), N, Hi, Wi, Cc, ptr(dx), pstride(dx), Ho, Wo,
+         Hp, Wp, py, px, 1 if accumulate else 0, dtype, stream())
+    return dx
+
+
+def workspace_f32(nbytes, device):
+    return torch.empty(max(1, nbytes // 4 + 1), dtype=torch.float32, device=device)
