@@ -1,0 +1,179 @@
+"""Benchmark: whole-node images/sec of the VAE-U-Net training step.
+
+Workload (BASELINE.json configs[1], metric quoted on it):
+  UNet(n_channels=3, n_classes=2, bilinear=False), synthetic 3x512x512 batches,
+  batch 8 per GPU, bf16 (torch.autocast, the train.py:385 path), one step =
+  forward + CombinedLoss + backward (+ RCCL gradient all-reduce when N>1) +
+  clip_grad_norm_(1.0) + AdamW(lr 1e-4, wd 1e-5) step + zero_grad.
+  (train.py:381-411; the optimizer runs every step here, not every 2nd.)
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 the driver
+uses torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE from the env).
+Rank 0 prints ONE JSON line (see README / DESIGN.md §Measurement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+# algorithmic FLOPs of the 3x3 convolutions per 512x512 image:
+# fwd 368.13 + dgrad 367.22 + wgrad 368.13 GFLOP (inc.0 included)
+CONV3_GFLOP_PER_IMG = 1103.5
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--classes", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    return ap.parse_args()
+
+
+def synthetic(B, S, C, rank, dev):
+    g = torch.Generator().manual_seed(1000 + rank)
+    x = torch.rand(B, 3, S, S, generator=g)
+    m = (torch.rand(B, 1, S, S, generator=g) < 0.0085).float()
+    t = torch.cat([1 - m, m], 1) if C == 2 else m
+    return (x.to(dev).contiguous(memory_format=torch.channels_last),
+            t.to(dev).contiguous(memory_format=torch.channels_last))
+
+
+def cpu_baseline(args, n_steps):
+    """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py)
+    timed on this host on a bounded sample: batch 1 at the same 3x512x512 /
+    2-class config, fp32, full train step (fwd, CombinedLoss, bwd, clip, AdamW)."""
+    from oracle import cpu_ref as R
+    from vaeunet_amd import UNet
+    from vaeunet_amd.init import seeded_init_
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(threads, 16))
+    torch.set_num_threads(threads)
+    model = R.UNetRef(seeded_init_(UNet(3, args.classes), 0).state_dict())
+    opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
+    x, t = synthetic(1, args.size, args.classes, 0, "cpu")
+    x, t = x.contiguous(), t.contiguous()
+    R.train_step(model, opt, x, t)  # warmup
+    t0 = time.perf_counter()
+    for _ in range(n_steps):
+        R.train_step(model, opt, x, t)
+    dt = time.perf_counter() - t0
+    return {"value": round(n_steps / dt, 4), "unit": "images/sec", "cores": threads,
+            "kind": "port",
+            "sample": f"{n_steps} fp32 train steps of UNet(3,{args.classes}) on 1x3x{args.size}x"
+                      f"{args.size} (oracle/cpu_ref.py, torch CPU, {threads} threads)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from vaeunet_amd import UNet, kernels as K
+    from vaeunet_amd.init import seeded_init_
+    from vaeunet_amd.loss import CombinedLoss
+    from vaeunet_amd import parallel
+
+    model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
+    model.train()
+    reducer = parallel.attach(model) if world > 1 else None
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-5, foreach=True)
+    crit = CombinedLoss()
+    x, t = synthetic(args.batch, args.size, args.classes, rank, dev)
+
+    def step():
+        if reducer is not None:
+            reducer.prepare()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(x)
+            loss = crit(logits, t)
+        loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0, foreach=True)
+        opt.step()
+        opt.zero_grad(set_to_none=reducer is None)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms = dt / args.steps * 1e3
+    imgs = args.batch * world * args.steps / dt
+
+    roof = None
+    if not args.no_roofline:
+        # live per-launch HIP-event timing of the 3x3 implicit-GEMM kernels over
+        # 2 further steps (events on the launch stream, one pair per launch)
+        K.TIMER = K.LaunchTimer()
+        for _ in range(2):
+            step()
+        summ = K.TIMER.summary()
+        K.TIMER = None
+        fl = sum(v[0] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
+        tm = sum(v[1] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
+        n = sum(v[2] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
+        achieved = fl / (tm * 1e-3) / 1e12 if tm > 0 else 0.0
+        roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "kernel": "gemm_fwd_kernel+gemm_wgrad_kernel (3x3 conv fwd/dgrad/wgrad, inc.0 excluded)",
+                "launches_per_step": n // 2,
+                "per_kind": {k: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1),
+                                 "ms_per_step": round(v[1] / 2, 3)} for k, v in sorted(summ.items())}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.cpu_sample_steps)
+
+    if rank == 0:
+        line = {"metric": "images/sec (whole node) at 3x512x512 bs=8/GPU", "value": round(imgs, 2),
+                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+                "config": {"workload": f"UNet(3,{args.classes}) train step (fwd+CombinedLoss+bwd"
+                                       "+clip+AdamW), random-init weights",
+                           "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
+                           "global_batch": args.batch * world, "parallelism": f"dp{world}"},
+                "loss": round(float(loss.item()), 6),
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

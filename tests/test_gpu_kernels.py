@@ -1,0 +1,255 @@
+"""Kernel-level parity: each HIP kernel vs a plain PyTorch fp32 CPU reference
+of the same op (floating-point kernels, cdna guide: torch fp32 reference).
+
+fp32 storage mode must match to fp32 rounding (MFMA f32 = exact fma chain,
+different summation order); bf16 storage mode within bf16 tolerances.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+CL = torch.channels_last
+
+
+def _k():
+    from vaeunet_amd import kernels as K, engine as E
+    return K, E
+
+
+def _dt(mode):
+    return torch.float32 if mode == "f32" else torch.bfloat16
+
+
+def _code(mode):
+    return 0 if mode == "f32" else 1
+
+
+def _tol(mode):
+    return (2e-5, 2e-5) if mode == "f32" else (2e-2, 2e-2)
+
+
+def _act(t, mode):
+    return t.to(DEV, _dt(mode)).contiguous(memory_format=CL)
+
+
+def _close(got, ref, mode, scale_floor=1e-3, what=""):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    err = (got - ref).abs().max().item()
+    scale = max(ref.abs().max().item(), scale_floor)
+    rtol = 2e-5 if mode == "f32" else 1.5e-2
+    assert err <= rtol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+CONV_CASES = [
+    # (N, [cin per source], H, W, cout)
+    (2, [64], 16, 16, 64),
+    (2, [8], 9, 7, 16),
+    (2, [32, 32], 12, 10, 48),
+    (1, [128], 32, 32, 128),
+    (8, [64], 128, 128, 64),      # BM=128, BN=64 path
+    (4, [64, 64], 128, 128, 128),  # BM=128, BN=128 path, two sources
+    (2, [24, 8, 16], 6, 6, 40),    # three sources, ragged
+]
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv3x3_fwd_dgrad_wgrad(mode, case):
+    K, E = _k()
+    N, cins, H, W, co = case
+    g = torch.Generator().manual_seed(1)
+    xs = [torch.randn(N, c, H, W, generator=g) for c in cins]
+    cin = sum(cins)
+    w = torch.randn(co, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    # round inputs to the storage dtype so the reference sees the same values
+    xs = [x.to(_dt(mode)).float() for x in xs]
+    wq = w.to(_dt(mode)).float()
+    ref = F.conv2d(torch.cat(xs, 1), wq, padding=1)
+    d = _code(mode)
+    srcs = [_act(x, mode) for x in xs]
+    wdev = w.to(DEV)
+    out = K.empty_act(N, co, H, W, _dt(mode), DEV)
+    st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(wdev, d), co, out, d, stats=True)
+    _close(out, ref, mode, what="fwd")
+    # statistics: combine partial (sum, M2) -> mean/var, compare with the stored values
+    stored = out.float().cpu()
+    n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                     dtype=torch.float64)
+    s = st.psum.double().cpu()
+    mean = s.sum(0) / n.sum()
+    m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+    var = m2.sum(0) / n.sum()
+    torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(var.float(), stored.var((0, 2, 3), unbiased=False), rtol=1e-4, atol=1e-5)
+    # input gradient
+    dy = torch.randn(N, co, H, W, generator=g).to(_dt(mode)).float()
+    dref = torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1)
+    dx = K.empty_act(N, cin, H, W, _dt(mode), DEV)
+    K.gemm_fwd(K.gather3x3([_act(dy, mode)]), E.w3x3_dgrad(wdev, d), cin, dx, d)
+    _close(dx, dref, mode, what="dgrad")
+    # weight gradient, contiguous and channels_last parameter layouts
+    wref = torch.nn.grad.conv2d_weight(torch.cat(xs, 1), (co, cin, 3, 3), dy, padding=1)
+    for fmt in (torch.contiguous_format, CL):
+        gw = torch.zeros(co, cin, 3, 3, device=DEV).contiguous(memory_format=fmt)
+        K.gemm_wgrad(K.gather1x1([_act(dy, mode)]), K.gather3x3(srcs), co, 9 * cin, gw,
+                     E.conv_layout(gw), d, False)
+        _close(gw, wref, mode, what=f"wgrad {fmt}")
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("case", [(2, 64, 4, 4, 32, 8, 8), (2, 64, 4, 4, 32, 9, 10),
+                                  (8, 128, 64, 64, 64, 128, 128)])
+def test_conv_transpose(mode, case):
+    """ConvTranspose2d(k2,s2)+bias then F.pad into the skip canvas (unet_parts.py:76,88)."""
+    K, E = _k()
+    N, ci, h, w, co, H, W = case
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(N, ci, h, w, generator=g).to(_dt(mode)).float()
+    wt = (torch.randn(ci, co, 2, 2, generator=g) / ci ** 0.5)
+    b = torch.randn(co, generator=g) * 0.1
+    wq = wt.to(_dt(mode)).float()
+    dyp, dxp = H - 2 * h, W - 2 * w
+    py, px = dyp // 2, dxp // 2
+    xr = x.clone().requires_grad_(True)
+    wr = wq.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = F.pad(F.conv_transpose2d(xr, wr, br, stride=2), [px, dxp - px, py, dyp - py])
+    d = _code(mode)
+    u = K.zeros_act(N, co, H, W, _dt(mode), DEV)
+    K.gemm_fwd(K.gather1x1([_act(x, mode)]), E.wT_fwd(wt.to(DEV), d), 4 * co, u, d,
+               bias=b.to(DEV), convT=(H, W, py, px, co))
+    _close(u, ref, mode, what="convT fwd")
+    du = torch.randn(N, co, H, W, generator=g).to(_dt(mode)).float()
+    ref.backward(du)
+    dua = _act(du, mode)
+    dx = K.empty_act(N, ci, h, w, _dt(mode), DEV)
+    K.gemm_fwd(K.gather_convT(dua, N, h, w, py, px), E.wT_dgrad(wt.to(DEV), d), ci, dx, d)
+    _close(dx, xr.grad, mode, what="convT dgrad")
+    gw = torch.zeros(ci, co, 2, 2, device=DEV)
+    K.gemm_wgrad(K.gather1x1([_act(x, mode)]), K.gather_convT(dua, N, h, w, py, px), ci, 4 * co, gw,
+                 E.convT_layout(gw), d, False)
+    _close(gw, wr.grad, mode, what="convT wgrad")
+    gb = torch.zeros(co, device=DEV)
+    K.chan_sum(dua, gb, False, d, window=(py, px, 2 * h, 2 * w))
+    _close(gb, br.grad, mode, what="convT bias grad")
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("shape", [(2, 16, 8, 8), (2, 8, 11, 9), (2, 3, 5, 7)])
+def test_maxpool(mode, shape):
+    K, _ = _k()
+    g = torch.Generator().manual_seed(3)
+    # small integers: plenty of exact ties (first max in scan order wins)
+    x = torch.randint(-3, 3, shape, generator=g).float()
+    xr = x.clone().requires_grad_(True)
+    ref = F.max_pool2d(xr, 2)
+    d = _code(mode)
+    xa = _act(x, mode)
+    y = K.maxpool_fwd(xa, d)
+    _close(y, ref, mode, what="pool fwd")
+    dy = torch.randn(ref.shape, generator=g).to(_dt(mode)).float()
+    ref.backward(dy)
+    add = torch.randn(shape, generator=g).to(_dt(mode)).float()
+    dx = torch.empty_like(xa)
+    K.maxpool_bwd(xa, _act(dy, mode), dx, _act(add, mode), d)
+    _close(dx, xr.grad + add, mode, what="pool bwd")
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("case", [(2, 16, 4, 4, 8, 8, 8, 8), (2, 8, 5, 4, 10, 8, 11, 9),
+                                  (1, 32, 16, 16, 33, 31, 33, 31), (2, 8, 1, 1, 6, 6, 6, 6)])
+def test_upsample_bilinear(mode, case):
+    K, _ = _k()
+    N, C_, hi, wi, ho, wo, Hp, Wp = case
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(N, C_, hi, wi, generator=g).to(_dt(mode)).float()
+    xr = x.clone().requires_grad_(True)
+    py, px = (Hp - ho) // 2, (Wp - wo) // 2
+    up = F.interpolate(xr, size=(ho, wo), mode="bilinear", align_corners=True)
+    ref = F.pad(up, [px, Wp - wo - px, py, Hp - ho - py])
+    d = _code(mode)
+    out = K.empty_act(N, C_, Hp, Wp, _dt(mode), DEV)
+    K.upsample_fwd(_act(x, mode), out, ho, wo, py, px, d)
+    _close(out, ref, mode, what="upsample fwd")
+    dy = torch.randn(N, C_, Hp, Wp, generator=g).to(_dt(mode)).float()
+    ref.backward(dy)
+    dx = K.empty_act(N, C_, hi, wi, _dt(mode), DEV)
+    K.upsample_bwd(_act(dy, mode), dx, ho, wo, py, px, False, d)
+    _close(dx, xr.grad, mode, what="upsample bwd")
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("shape", [(4, 64, 16, 16), (2, 24, 5, 7), (8, 128, 64, 64)])
+def test_batchnorm_train(mode, relu, shape):
+    """BatchNorm2d train mode (+ReLU) fwd/bwd and running stats vs torch."""
+    K, E = _k()
+    N, C_, H, W = shape
+    g = torch.Generator().manual_seed(5)
+    y = (torch.randn(shape, generator=g) * 3 + 1).to(_dt(mode)).float()
+    bn = torch.nn.BatchNorm2d(C_)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn_dev = torch.nn.BatchNorm2d(C_).to(DEV)
+    bn_dev.load_state_dict(bn.state_dict())
+    yr = y.clone().requires_grad_(True)
+    ref = bn(yr)
+    if relu:
+        ref = torch.relu(ref)
+    d = _code(mode)
+    ya = _act(y, mode)
+    out = K.empty_act(N, C_, H, W, _dt(mode), DEV)
+    # statistics through an identity 1x1 GEMM epilogue
+    eye = torch.eye(C_, device=DEV)
+    st = K.gemm_fwd(K.gather1x1([ya]), E.w1x1_fwd(eye.view(C_, C_, 1, 1), d), C_, out, d, stats=True)
+    coef = E.bn_coef(bn_dev, st, C_)
+    a = torch.empty_like(out)
+    K.bn_apply(out, a, coef, relu, d)
+    _close(a, ref, mode, what="bn fwd")
+    torch.testing.assert_close(bn_dev.running_mean.cpu(), bn.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn_dev.running_var.cpu(), bn.running_var, rtol=1e-4, atol=1e-5)
+    assert int(bn_dev.num_batches_tracked) == 1
+    da = torch.randn(shape, generator=g).to(_dt(mode)).float()
+    ref.backward(da)
+    dx = E.bn_bwd(_act(da, mode), out, coef, bn_dev, relu, E.Mode(d, torch.device(DEV)))
+    _close(dx, yr.grad, mode, scale_floor=1e-2, what="bn bwd")
+    torch.testing.assert_close(bn_dev.weight.grad.cpu(), bn.weight.grad, rtol=2e-3, atol=1e-3)
+    torch.testing.assert_close(bn_dev.bias.grad.cpu(), bn.bias.grad, rtol=2e-3, atol=1e-3)
+
+
+def test_loss_kernels_vs_oracle():
+    from vaeunet_amd.loss import CombinedLoss, dice_loss, kl_with_free_bits
+    from oracle import cpu_ref as R
+    g = torch.Generator().manual_seed(6)
+    for shape, p in [((2, 1, 64, 64), 0.02), ((3, 2, 16, 16), 0.3), ((2, 1, 8, 8), 0.0)]:
+        x = torch.randn(shape, generator=g) * 3
+        t = (torch.rand(shape, generator=g) < p).float()
+        xr = x.clone().requires_grad_(True)
+        ref = R.combined_loss(xr, t)
+        ref.backward()
+        xd = x.to(DEV).requires_grad_(True)
+        out = CombinedLoss()(xd, t.to(DEV))
+        out.backward()
+        assert abs(out.item() - ref.item()) < 1e-5
+        torch.testing.assert_close(xd.grad.cpu(), xr.grad, rtol=1e-4, atol=1e-8)
+        assert abs(dice_loss(x.to(DEV), t.to(DEV)).item() - R.dice_loss(x, t).item()) < 1e-6
+    mu = torch.randn(8, 32, generator=g)
+    lv = torch.randn(8, 32, generator=g)
+    mu[0, 0] = 0.0
+    lv[0, 0] = 0.0
+    for fb in (1e-3, 0.0, 0.5):
+        m, v = mu.clone().requires_grad_(True), lv.clone().requires_grad_(True)
+        ref = R.kl_with_free_bits(m, v, fb)
+        ref.backward()
+        md, vd = mu.to(DEV).requires_grad_(True), lv.to(DEV).requires_grad_(True)
+        out = kl_with_free_bits(md, vd, free_bits=fb)
+        (2.0 * out).backward()
+        assert abs(out.item() - ref.item()) < 1e-5 * max(1.0, abs(ref.item()))
+        torch.testing.assert_close(md.grad.cpu(), 2 * m.grad, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(vd.grad.cpu(), 2 * v.grad, rtol=1e-5, atol=1e-7)

@@ -1,0 +1,146 @@
+"""Module-level parity on the GPU: the drop-in modules (fp32 parity mode)
+against the reference's own golden fixtures, and against the CPU oracle at
+larger sizes; bf16 (autocast) mode against the fp32 oracle with the
+tolerances stated per test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load, state_of, relerr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+BLOCKS = {
+    "doubleconv_8_16": ("DoubleConv", (8, 16)),
+    "doubleconv_3_16_mid8": ("DoubleConv", (3, 16, 8)),
+    "down_16_32": ("Down", (16, 32)),
+    "down_odd_16_32": ("Down", (16, 32)),
+    "up_64_32_convT": ("Up", (64, 32, False)),
+    "up_64_32_bilinear": ("Up", (64, 32, True)),
+    "up_odd_64_32_convT": ("Up", (64, 32, False)),
+    "up_odd_64_32_bilinear": ("Up", (64, 32, True)),
+    "attention_32_32_16": ("AttentionGate", (32, 32, 16)),
+    "outconv_16_2": ("OutConv", (16, 2)),
+}
+
+
+def _build(name):
+    import vaeunet_amd.unet_parts as P
+    cls, args = BLOCKS[name]
+    return getattr(P, cls)(*args)
+
+
+@pytest.mark.parametrize("name", sorted(BLOCKS))
+def test_block_fp32_matches_reference(name):
+    rec = load(name)
+    mod = _build(name)
+    st = state_of(rec)
+    missing = mod.load_state_dict(st, strict=False)
+    assert not missing.unexpected_keys
+    assert all("num_batches" in k for k in missing.missing_keys)
+    mod = mod.to(DEV).train()
+    n_in = len([k for k in rec if k.startswith("in")])
+    ins = [torch.from_numpy(rec[f"in{i}"]).to(DEV).requires_grad_(True) for i in range(n_in)]
+    out = mod(*ins)
+    assert out.dtype == torch.float32
+    assert relerr(out.detach().cpu(), rec["out"]) < 1e-4
+    out.backward(torch.from_numpy(rec["gout"]).to(DEV))
+    for i, t in enumerate(ins):
+        assert relerr(t.grad.cpu(), rec[f"gin{i}"]) < 2e-3, f"input grad {i}"
+    gmax = max(float(np.abs(rec[f"grad.{k}"]).max()) for k, _ in mod.named_parameters())
+    for k, p in mod.named_parameters():
+        np.testing.assert_allclose(p.grad.cpu().numpy(), rec[f"grad.{k}"], rtol=2e-3,
+                                   atol=2e-5 * gmax, err_msg=k)
+    for k, b in mod.named_buffers():
+        if f"buf.{k}" in rec:
+            assert relerr(b.cpu(), rec[f"buf.{k}"]) < 1e-4, k
+        if k.endswith("num_batches_tracked"):
+            assert int(b) == 1
+
+
+def _unet(nc, bil):
+    from vaeunet_amd import UNet
+    from vaeunet_amd.init import seeded_init_
+    return seeded_init_(UNet(3, nc, bilinear=bil), 0)
+
+
+@pytest.mark.parametrize("tag,nc,bil", [("unet_c1_64", 1, False), ("unet_c2_64", 2, False),
+                                        ("unet_c1_bilinear_64", 1, True)])
+def test_unet_train_step_fp32_matches_reference(tag, nc, bil):
+    """train.py:381-411 (tiny config) with the HIP path in fp32 parity mode."""
+    from vaeunet_amd.loss import CombinedLoss
+    rec = load(tag)
+    model = _unet(nc, bil).to(DEV).to(memory_format=torch.channels_last).train()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-5)
+    x = torch.from_numpy(rec["x"]).to(DEV).contiguous(memory_format=torch.channels_last)
+    t = torch.from_numpy(rec["target"]).to(DEV)
+    logits = model(x)
+    loss = CombinedLoss()(logits, t)
+    loss.backward()
+    lg = logits.detach().cpu()
+    # per-pixel logits within 1e-3 (north_star), class maps bit-exact
+    assert relerr(lg, rec["logits"]) < 1e-3
+    if nc > 1:
+        np.testing.assert_array_equal(lg.argmax(1).numpy(), rec["argmax"])
+    else:
+        np.testing.assert_array_equal((lg > 0).numpy(), rec["argmax"])
+    assert abs(loss.item() - float(rec["loss"])) < 1e-3
+    gn = np.array([float(p.grad.double().norm()) for p in model.parameters()])
+    big = rec["gnorm"] > 1e-3 * rec["gnorm"].max()
+    np.testing.assert_allclose(gn[big], rec["gnorm"][big], rtol=1e-2)
+    total = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    assert abs(total.item() - float(rec["total_norm"])) < 2e-3 * float(rec["total_norm"])
+    opt.step()
+    for k, b in model.named_buffers():
+        if f"buf.{k}" in rec:
+            assert relerr(b.cpu(), rec[f"buf.{k}"]) < 1e-3, k
+
+
+def test_unet_bf16_autocast_vs_oracle():
+    """Speed mode (autocast -> bf16 storage, fp32 accumulation) vs the fp32
+    oracle: logits within 5e-2 relative, loss within 1e-2."""
+    from vaeunet_amd.loss import CombinedLoss
+    from oracle import cpu_ref as R
+    rec = load("unet_c1_64")
+    model = _unet(1, False).to(DEV).train()
+    x = torch.from_numpy(rec["x"]).to(DEV)
+    t = torch.from_numpy(rec["target"]).to(DEV)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        logits = model(x)
+        loss = CombinedLoss()(logits, t)
+    loss.backward()
+    assert relerr(logits.detach().float().cpu(), rec["logits"]) < 5e-2
+    assert abs(loss.item() - float(rec["loss"])) < 1e-2
+    for p in model.parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all()
+
+
+def test_unet_512_fp32_vs_oracle():
+    """Full-resolution case (3x512x512, B=1) against the CPU oracle: logits
+    within 1e-3, argmax bit-exact, loss within 1e-3."""
+    from vaeunet_amd.loss import CombinedLoss
+    from oracle import cpu_ref as R
+    torch.manual_seed(0)
+    model = _unet(2, False)
+    state = model.state_dict()
+    ref = R.UNetRef(state)
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(1, 3, 512, 512, generator=g)
+    m = (torch.rand(1, 1, 512, 512, generator=g) < 0.0085).float()
+    t = torch.cat([1 - m, m], 1)
+    lref = ref.forward(x, True)
+    loss_ref = R.combined_loss(lref, t)
+    model = model.to(DEV).to(memory_format=torch.channels_last).train()
+    lg = model(x.to(DEV).contiguous(memory_format=torch.channels_last))
+    loss = CombinedLoss()(lg, t.to(DEV))
+    lgc = lg.detach().cpu()
+    assert relerr(lgc, lref.detach()) < 1e-3
+    am, amr = lgc.argmax(1), lref.detach().argmax(1)
+    margin = (lref[:, 0] - lref[:, 1]).abs().detach()
+    flips = (am != amr)
+    # bit-exact class map except where the reference itself is within fp32
+    # noise of a tie
+    assert int((flips & (margin > 1e-4)).sum()) == 0
+    assert abs(loss.item() - loss_ref.item()) < 1e-3

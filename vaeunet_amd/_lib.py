@@ -77,7 +77,7 @@ _SIGS = {
     "vu_pointwise_bwd_workspace_bytes": (_l, [_l, _i, _i]),
     "vu_pointwise_bwd": (_i, [_p, _l, _p, _l, _l, _i, _i, _p, _p, _l, _p, _p, _i, _p, _i, _p]),
     "vu_loss_workspace_bytes": (_l, []),
-    "vu_bce_dice_fwd2": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p]),
+    "vu_bce_dice_fwd2": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p, _p]),
     "vu_bce_dice_bwd": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p]),
     "vu_kl_free_bits2": (_i, [_p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
     "vu_sumsq": (_i, [_p, _l, _p, _p, _p]),

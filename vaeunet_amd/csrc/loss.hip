@@ -58,7 +58,7 @@ __global__ void bce_dice_stage1(const float* x, const float* t, int64_t n, doubl
 }
 
 __global__ void bce_dice_stage2(const double* ws, int nblk, int64_t n, double* sums, float smooth, float w_bce,
-                                float w_dice, float* loss) {
+                                float w_dice, float* loss, float* parts) {
   if (threadIdx.x != 0) return;
   double s[4] = {0, 0, 0, 0};
   for (int b = 0; b < nblk; ++b)
@@ -71,8 +71,7 @@ __global__ void bce_dice_stage2(const double* ws, int nblk, int64_t n, double* s
     float dice = (2.f * I + smooth) / (sp + st + smooth);
     float dl = 1.f - dice;
     loss[0] = w_bce * bce + w_dice * dl;
-    loss[1] = bce;
-    loss[2] = dl;
+    if (parts) { parts[0] = bce; parts[1] = dl; }
   }
 }
 
@@ -164,17 +163,19 @@ int nblocks(int64_t n) {
 extern "C" int64_t vu_loss_workspace_bytes() { return (int64_t)LNB * 4 * sizeof(double); }
 
 extern "C" int vu_bce_dice_fwd2(const float* logits, const float* target, int64_t n, double* sums, float smooth,
-                                float w_bce, float w_dice, float* loss, double* workspace, void* stream) {
+                                float w_bce, float w_dice, float* loss, float* parts, double* workspace,
+                                void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int nb = nblocks(n);
   hipLaunchKernelGGL(bce_dice_stage1, dim3(nb), dim3(LBLK), 0, st, logits, target, n, workspace);
-  hipLaunchKernelGGL(bce_dice_stage2, dim3(1), dim3(64), 0, st, workspace, nb, n, sums, smooth, w_bce, w_dice, loss);
+  hipLaunchKernelGGL(bce_dice_stage2, dim3(1), dim3(64), 0, st, workspace, nb, n, sums, smooth, w_bce, w_dice, loss,
+                     parts);
   return (int)hipGetLastError();
 }
 
 extern "C" int vu_bce_dice_fwd(const float* logits, const float* target, int64_t n, double* sums, double* workspace,
                                void* stream) {
-  return vu_bce_dice_fwd2(logits, target, n, sums, 1.f, 0.5f, 0.5f, nullptr, workspace, stream);
+  return vu_bce_dice_fwd2(logits, target, n, sums, 1.f, 0.5f, 0.5f, nullptr, nullptr, workspace, stream);
 }
 
 extern "C" int vu_bce_dice_bwd(const float* logits, const float* target, int64_t n, const double* sums, float smooth,

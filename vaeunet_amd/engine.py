@@ -234,7 +234,8 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     cin = conv.in_channels
     if dsrc is None:
         dsrc = M.act(N, cin, H, W)
-    K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d), cin, dsrc, M.d, accumulate=dsrc_acc)
+    K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d), cin, dsrc, M.d, accumulate=dsrc_acc,
+               kind="dgrad")
     return dsrc
 
 

@@ -29,7 +29,7 @@ def empty_act(N, Cc, H, W, dtype, device):
 
 
 def zeros_act(N, Cc, H, W, dtype, device):
-    return torch.zeros((N, Cc, H, W), dtype=dtype, device=device, memory_format=CL)
+    return torch.empty((N, Cc, H, W), dtype=dtype, device=device, memory_format=CL).zero_()
 
 
 def pstride(t):
@@ -63,6 +63,10 @@ def gather(srcs, N, H, W, R=1, S=1, sy=1, sx=1, dy=1, dx=1, oy=0, ox=0, Hs=None,
     g.Hs = srcs[0].shape[2] if Hs is None else Hs
     g.Ws = srcs[0].shape[3] if Ws is None else Ws
     g.R, g.S, g.sy, g.sx, g.dy, g.dx, g.oy, g.ox = R, S, sy, sx, dy, dx, oy, ox
+    # the struct holds raw device pointers: keep the source tensors alive until
+    # the launch that consumes this descriptor has been enqueued, otherwise
+    # the caching allocator may hand their memory to the next allocation
+    g._refs = list(srcs)
     return g
 
 
@@ -81,6 +85,51 @@ def gather_convT(du, N, h, w, py=0, px=0):
     return gather([du], N, h, w, R=2, S=2, sy=2, sx=2, oy=py, ox=px)
 
 
+class LaunchTimer:
+    """Optional per-launch HIP-event timing of the GEMM kernels (bench.py's
+    roofline leg).  Events are recorded on the current stream — the stream
+    the kernels are launched on — so they bracket exactly one launch."""
+
+    def __init__(self):
+        self.recs = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for tag, flops, s, e in self.recs:
+            ms = s.elapsed_time(e)
+            d = out.setdefault(tag, [0, 0.0, 0])
+            d[0] += flops
+            d[1] += ms
+            d[2] += 1
+        return out
+
+
+TIMER = None
+
+
+def _timed(tag, flops, fn):
+    if TIMER is None:
+        return fn()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    r = fn()
+    e.record()
+    TIMER.recs.append((tag, flops, s, e))
+    return r
+
+
+def _gemm_tag(g, kind):
+    if g.R == 3 and g.C >= 16:
+        return f"conv3x3_{kind}"
+    if g.R == 3:
+        return f"conv3x3_image_{kind}"
+    if g.R == 2:
+        return f"convT_{kind}"
+    return f"gemm1x1_{kind}"
+
+
 class Stats:
     """Per-row-tile BatchNorm partials produced by a GEMM epilogue."""
 
@@ -89,7 +138,7 @@ class Stats:
 
 
 def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
-             convT=None):
+             convT=None, kind="fwd"):
     """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
     the pixel-shuffle epilogue.  Returns Stats if requested."""
     a = VuGemmFwd()
@@ -118,7 +167,10 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
         st = Stats(psum, pm2, tiles, bm, rows)
     else:
         a.stat_sum = a.stat_m2 = None
-    call("vu_gemm_fwd", C.byref(a), dtype, stream())
+    M = g.N * g.H * g.W
+    _timed(_gemm_tag(g, kind),
+           2 * M * ncol * g.R * g.S * g.C,
+           lambda: call("vu_gemm_fwd", C.byref(a), dtype, stream()))
     return st
 
 
@@ -135,7 +187,8 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
     w = VuGemmWgrad()
     w.p, w.q, w.ni, w.nj, w.splits, w.m_per_split = gp, gq, ni, nj, splits, mps
     w.out = slab.data_ptr()
-    call("vu_gemm_wgrad", C.byref(w), dtype, stream())
+    _timed(_gemm_tag(gq, "wgrad"), 2 * M * ni * nj,
+           lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()))
     s_i, s_tap, s_c = layout
     call("vu_slab_reduce", ptr(slab), splits, ni, nj, gq.C, gq.C if cvalid is None else cvalid,
          s_i, s_tap, s_c, ptr(grad),
