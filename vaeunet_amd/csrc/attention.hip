@@ -147,7 +147,10 @@ __global__ void gate_bwd_kernel(const T* dout, int64_t dos, const T* x, int64_t 
   }
 }
 
-// ds[p,c] = dq[p]*wpsi[c]*(s>0); partial dwpsi[c] over the tile; partial dbpsi
+// ds[p,c] = dq[p]*wpsi[c]*(s>0); per-block partials of dwpsi[c] and dbpsi
+// (grid-stride over 256-pixel tiles, so at most MAXB partial rows)
+constexpr int MAXB = 1024;
+
 template <typename T>
 __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg, const float* tg,
                                const float* sx, const float* tx, const float* wpsi, const float* dq, T* ds,
@@ -157,7 +160,6 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
   const int lpp = F >> 3, ppw = 64 / lpp;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int sub = lane % lpp, slot = lane / lpp;
-  const int64_t p0 = (int64_t)blockIdx.x * TILE;
   const int c = sub * 8;
   float wsg[8], wtg[8], wsx[8], wtx[8], wp[8], dw[8];
 #pragma unroll
@@ -166,23 +168,25 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
     dw[k] = 0.f;
   }
   float db = 0.f;
-  for (int i = w * ppw + slot; i < TILE; i += 4 * ppw) {
-    int64_t p = p0 + i;
-    if (p >= P) continue;
-    float g = dq[p];
-    if (sub == 0) db += g;
-    float a[8], bb[8];
-    load8<T>(ug + p * F + c, a);
-    load8<T>(ux + p * F + c, bb);
-    Vec8<T> o;
+  for (int64_t p0 = (int64_t)blockIdx.x * TILE; p0 < P; p0 += (int64_t)gridDim.x * TILE) {
+    for (int i = w * ppw + slot; i < TILE; i += 4 * ppw) {
+      int64_t p = p0 + i;
+      if (p >= P) continue;
+      float g = dq[p];
+      if (sub == 0) db += g;
+      float a[8], bb[8];
+      load8<T>(ug + p * F + c, a);
+      load8<T>(ux + p * F + c, bb);
+      Vec8<T> o;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float s = a[k] * wsg[k] + wtg[k] + bb[k] * wsx[k] + wtx[k];
-      bool on = s > 0.f;
-      dw[k] += on ? g * s : 0.f;
-      o.set(k, on ? g * wp[k] : 0.f);
+      for (int k = 0; k < 8; ++k) {
+        float s = a[k] * wsg[k] + wtg[k] + bb[k] * wsx[k] + wtx[k];
+        bool on = s > 0.f;
+        dw[k] += on ? g * s : 0.f;
+        o.set(k, on ? g * wp[k] : 0.f);
+      }
+      o.store(ds + p * F + c);
     }
-    o.store(ds + p * F + c);
   }
 #pragma unroll
   for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = dw[k];
@@ -192,8 +196,7 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
   for (int cc = threadIdx.x; cc < F; cc += 256) {
     int sb_ = cc >> 3, k = cc & 7;
     float s = 0.f;
-    for (int t = 0; t < 256; ++t)
-      if (((t & 63) % lpp) == sb_) s += sh[t * 8 + k];
+    for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
     part[(int64_t)blockIdx.x * (F + 1) + cc] = s;
   }
   if (threadIdx.x == 0) {
@@ -203,13 +206,20 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
   }
 }
 
+// column sums of [nblk][width] partials: 64 columns x 4 row lanes, fp64
 __global__ void part_final(const float* part, int nblk, int width, float* out, int n_out, float* out2,
                            int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= width) return;
+  __shared__ double sh[4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   double s = 0;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * width + c];
-  float* o = c < n_out ? out + c : out2 + (c - n_out);
+  if (c < width)
+    for (int b = q; b < nblk; b += 4) s += part[(int64_t)b * width + c];
+  sh[q][cl] = s;
+  __syncthreads();
+  if (q != 0 || c >= width) return;
+  s = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
+  float* o = c < n_out ? (out ? out + c : nullptr) : (out2 ? out2 + (c - n_out) : nullptr);
   if (o == nullptr) return;
   *o = accumulate ? *o + (float)s : (float)s;
 }
@@ -254,57 +264,57 @@ __global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t d
   const int ppw = 64 / lpp;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int sub = lane % lpp, slot = lane / lpp;
-  const int64_t p0 = (int64_t)blockIdx.x * TILE;
   const int c = sub * 8;
   const int width = J * C + J;
-  for (int j = 0; j < J; ++j) {
-    // one pass per output column j keeps registers small (J <= 4)
-    float dw[8];
+  float dw[4][8], db[4], wr[4][8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dw[k] = 0.f;
-    float dbj = 0.f;
+  for (int j = 0; j < 4; ++j) {
+    db[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dw[j][k] = 0.f; wr[j][k] = j < J ? w[j * C + c + k] : 0.f; }
+  }
+  for (int64_t p0 = (int64_t)blockIdx.x * TILE; p0 < P; p0 += (int64_t)gridDim.x * TILE) {
     for (int i = wv * ppw + slot; i < TILE; i += 4 * ppw) {
       int64_t p = p0 + i;
       if (p >= P) continue;
-      float g = dy[p * dys + j];
-      if (sub == 0) dbj += g;
+      float g[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = j < J ? dy[p * dys + j] : 0.f;
       float f[8];
       load8<T>(x + p * xs + c, f);
+      Vec8<T> o;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) dw[k] += g * f[k];
+      for (int k = 0; k < 8; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { dw[j][k] += g[j] * f[k]; s += g[j] * wr[j][k]; }
+        o.set(k, s);
+      }
+      o.store(dx + p * dxs + c);
+      if (sub == 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) db[j] += g[j];
     }
+  }
+  for (int j = 0; j < J; ++j) {
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = dw[k];
+    for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = dw[j][k];
     __syncthreads();
     for (int cc = threadIdx.x; cc < C; cc += 256) {
       int sb_ = cc >> 3, k = cc & 7;
       float s = 0.f;
-      for (int t = 0; t < 256; ++t)
-        if (((t & 63) % lpp) == sb_) s += sh[t * 8 + k];
+      for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
       part[(int64_t)blockIdx.x * width + j * C + cc] = s;
     }
     __syncthreads();
-    sh[threadIdx.x] = dbj;
+    sh[threadIdx.x] = db[j];
     __syncthreads();
     if (threadIdx.x == 0) {
       float s = 0.f;
       for (int t = 0; t < 256; ++t) s += sh[t];
       part[(int64_t)blockIdx.x * width + J * C + j] = s;
     }
-    __syncthreads();
-  }
-  // dx
-  for (int i = wv * ppw + slot; i < TILE; i += 4 * ppw) {
-    int64_t p = p0 + i;
-    if (p >= P) continue;
-    Vec8<T> o;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float s = 0.f;
-      for (int j = 0; j < J; ++j) s += dy[p * dys + j] * w[j * C + c + k];
-      o.set(k, s);
-    }
-    o.store(dx + p * dxs + c);
   }
 }
 
@@ -356,7 +366,8 @@ extern "C" int vu_attn_gate_bwd(const void* dout, int64_t dos, const void* x, in
 }
 
 extern "C" int64_t vu_attn_psi_bwd_workspace_bytes(int64_t P, int F) {
-  return ((P + TILE - 1) / TILE) * (F + 1) * (int64_t)sizeof(float);
+  int64_t nb = (P + TILE - 1) / TILE;
+  return (nb < MAXB ? nb : MAXB) * (F + 1) * (int64_t)sizeof(float);
 }
 
 extern "C" int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F, const float* sg, const float* tg,
@@ -366,12 +377,13 @@ extern "C" int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F,
   if (F % 8 != 0 || !pow2(F / 8) || F / 8 > 64 || F > 2048) return (int)hipErrorInvalidValue;
   int nblk = (int)((P + TILE - 1) / TILE);
   if (nblk == 0) return 0;
+  if (nblk > MAXB) nblk = MAXB;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL((psi_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
                        sx, tx, wpsi, dq, (T*)ds, workspace);
   })
-  hipLaunchKernelGGL(part_final, dim3((F + 1 + 63) / 64), dim3(64), 0, st, workspace, nblk, F + 1, dwpsi, F, dbpsi,
+  hipLaunchKernelGGL(part_final, dim3((F + 1 + 63) / 64), dim3(256), 0, st, workspace, nblk, F + 1, dwpsi, F, dbpsi,
                      accumulate);
   return (int)hipGetLastError();
 }
@@ -389,7 +401,8 @@ extern "C" int vu_pointwise_fwd(const void* x, int64_t xs, int64_t P, int C, int
 }
 
 extern "C" int64_t vu_pointwise_bwd_workspace_bytes(int64_t P, int C, int J) {
-  return ((P + TILE - 1) / TILE) * (int64_t)(J * C + J) * (int64_t)sizeof(float);
+  int64_t nb = (P + TILE - 1) / TILE;
+  return (nb < MAXB ? nb : MAXB) * (int64_t)(J * C + J) * (int64_t)sizeof(float);
 }
 
 extern "C" int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int64_t dys, int64_t P, int C, int J,
@@ -399,12 +412,13 @@ extern "C" int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int6
     return (int)hipErrorInvalidValue;
   int nblk = (int)((P + TILE - 1) / TILE);
   if (nblk == 0) return 0;
+  if (nblk > MAXB) nblk = MAXB;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL((pw_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w, (T*)dx,
                        dxs, workspace);
   })
-  hipLaunchKernelGGL(part_final, dim3((J * C + J + 63) / 64), dim3(64), 0, st, workspace, nblk, J * C + J, dw, J * C,
+  hipLaunchKernelGGL(part_final, dim3((J * C + J + 63) / 64), dim3(256), 0, st, workspace, nblk, J * C + J, dw, J * C,
                      db, accumulate);
   return (int)hipGetLastError();
 }

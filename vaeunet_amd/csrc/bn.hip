@@ -11,6 +11,11 @@
 // formula in fp64 in a fixed order, so results are bitwise reproducible.
 // Backward needs two per-channel sums (sum dz, sum dz*xhat): a two-stage
 // deterministic reduction (fp32 per block, fp64 across blocks).
+//
+// Memory-bound layout rule used by every kernel here: a thread owns one
+// fixed 8-channel vector (16 B bf16 / 32 B fp32) for its whole life, so the
+// per-channel coefficients live in registers and the pixel loop is a pure
+// load-FMA-store stream; a block covers 256/V pixels per pass (V = C/8).
 #include "common.h"
 #include "../../include/vaeunet.h"
 
@@ -87,21 +92,32 @@ __global__ void bn_eval_kernel(const float* gamma, const float* beta, const floa
   shift[c] = b - rm[c] * g * invstd;
 }
 
-// ---- elementwise apply: y = relu?(x*scale+shift), 8 channels per thread ----
+// Fixed-channel mapping: V = C/8 vectors per pixel, V a power of two <= 256.
+struct ChanMap {
+  int V, R, cv, row;
+  VU_DEV ChanMap(int C) {
+    V = C >> 3;
+    R = 256 / V;
+    cv = threadIdx.x & (V - 1);
+    row = threadIdx.x / V;
+  }
+};
+
 template <typename T>
 __global__ void bn_apply_kernel(const T* x, int64_t xs, T* y, int64_t ys, int64_t P, int C,
                                 const float* scale, const float* shift, int relu) {
-  int V = C >> 3;
-  int64_t tot = P * V;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t p = e / V;
-    int c = (int)(e - p * V) * 8;
+  ChanMap cm(C);
+  const int c = cm.cv * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sc[i] = scale[c + i]; sh[i] = shift[c + i]; }
+  const int64_t step = (int64_t)gridDim.x * cm.R;
+  for (int64_t p = (int64_t)blockIdx.x * cm.R + cm.row; p < P; p += step) {
     Vec8<T> v;
     v.load(x + p * xs + c);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float z = v.get(i) * scale[c + i] + shift[c + i];
+      float z = v.get(i) * sc[i] + sh[i];
       v.set(i, relu ? fmaxf(z, 0.f) : z);
     }
     v.store(y + p * ys + c);
@@ -109,9 +125,9 @@ __global__ void bn_apply_kernel(const T* x, int64_t xs, T* y, int64_t ys, int64_
 }
 
 // ---- per-channel partial reductions ----
-// MODE 0: s0 = sum x
+// MODE 0: s0 = sum x (over an optional pixel window)
 // MODE 1: s0 = sum dz, s1 = sum dz*xhat; dz = dy*(z>0 if relu), xhat=(x-mean)*invstd
-constexpr int RED_PB = 2048;  // pixels per block
+constexpr int RED_MAXBLK = 1024;
 
 struct RedArgs {
   const void* a; int64_t as;   // x (mode 0) or dy (mode 1)
@@ -133,54 +149,48 @@ VU_DEV int64_t win_pix(const RedArgs& r, int64_t p) {
 template <typename T, int MODE>
 __global__ void chan_partial_kernel(RedArgs r) {
   __shared__ float sh[2][256 * 8];
-  const int V = r.C >> 3;            // vectors per pixel (<= 256)
-  const int R = 256 / V;             // pixels per pass
-  const int t = threadIdx.x;
-  const int cv = t % V, row = t / V;
-  const bool act = row < R;
-  float s0[8], s1[8];
+  ChanMap cm(r.C);
+  const int c = cm.cv * 8;
+  float s0[8], s1[8], sc[8], sf[8], mu[8], is[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s0[i] = 0.f; s1[i] = 0.f; }
-  const int c = cv * 8;
-  int64_t pb = (int64_t)blockIdx.x * RED_PB, pe = pb + RED_PB;
-  if (pe > r.P) pe = r.P;
-  if (act) {
-    for (int64_t p = pb + row; p < pe; p += R) {
-      Vec8<T> va;
-      va.load(reinterpret_cast<const T*>(r.a) + win_pix(r, p) * r.as + c);
-      if (MODE == 0) {
+  for (int i = 0; i < 8; ++i) {
+    s0[i] = 0.f; s1[i] = 0.f;
+    if (MODE == 1) {
+      sc[i] = r.scale[c + i]; sf[i] = r.shift[c + i]; mu[i] = r.mean[c + i]; is[i] = r.invstd[c + i];
+    }
+  }
+  const int64_t step = (int64_t)gridDim.x * cm.R;
+  for (int64_t p = (int64_t)blockIdx.x * cm.R + cm.row; p < r.P; p += step) {
+    Vec8<T> va;
+    va.load(reinterpret_cast<const T*>(r.a) + win_pix(r, p) * r.as + c);
+    if (MODE == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s0[i] += va.get(i);
-      } else {
-        Vec8<T> vb;
-        vb.load(reinterpret_cast<const T*>(r.b) + p * r.bs + c);
+      for (int i = 0; i < 8; ++i) s0[i] += va.get(i);
+    } else {
+      Vec8<T> vb;
+      vb.load(reinterpret_cast<const T*>(r.b) + p * r.bs + c);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float xv = vb.get(i);
-          float dz = va.get(i);
-          if (r.relu && !(xv * r.scale[c + i] + r.shift[c + i] > 0.f)) dz = 0.f;
-          float xh = (xv - r.mean[c + i]) * r.invstd[c + i];
-          s0[i] += dz;
-          s1[i] += dz * xh;
-        }
+      for (int i = 0; i < 8; ++i) {
+        float xv = vb.get(i);
+        float dz = va.get(i);
+        if (r.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+        s0[i] += dz;
+        s1[i] += dz * ((xv - mu[i]) * is[i]);
       }
     }
   }
-  // reduce over the R rows in fixed order
-  if (act) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { sh[0][row * r.C + c + i] = s0[i]; sh[1][row * r.C + c + i] = s1[i]; }
-  }
+  for (int i = 0; i < 8; ++i) { sh[0][cm.row * r.C + c + i] = s0[i]; sh[1][cm.row * r.C + c + i] = s1[i]; }
   __syncthreads();
-  for (int cc = t; cc < r.C; cc += 256) {
+  for (int cc = threadIdx.x; cc < r.C; cc += 256) {
     float a0 = 0.f, a1 = 0.f;
-    for (int q = 0; q < R; ++q) { a0 += sh[0][q * r.C + cc]; a1 += sh[1][q * r.C + cc]; }
+    for (int q = 0; q < cm.R; ++q) { a0 += sh[0][q * r.C + cc]; a1 += sh[1][q * r.C + cc]; }
     r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + cc] = a0;
-    r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + cc] = a1;
+    if (MODE == 1) r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + cc] = a1;
   }
 }
 
-// scalar fallback for C % 8 != 0 (C <= 256)
+// scalar fallback for channel counts that are not 8 x power-of-two (C <= 256)
 template <typename T, int MODE>
 __global__ void chan_partial_scalar(RedArgs r) {
   __shared__ float sh[2][256];
@@ -188,10 +198,9 @@ __global__ void chan_partial_scalar(RedArgs r) {
   const int t = threadIdx.x, c = t % r.C, row = t / r.C;
   const bool act = row < R;
   float s0 = 0.f, s1 = 0.f;
-  int64_t pb = (int64_t)blockIdx.x * RED_PB, pe = pb + RED_PB;
-  if (pe > r.P) pe = r.P;
   if (act) {
-    for (int64_t p = pb + row; p < pe; p += R) {
+    const int64_t step = (int64_t)gridDim.x * R;
+    for (int64_t p = (int64_t)blockIdx.x * R + row; p < r.P; p += step) {
       float av = ld1<T>(reinterpret_cast<const T*>(r.a) + win_pix(r, p) * r.as + c);
       if (MODE == 0) s0 += av;
       else {
@@ -214,54 +223,71 @@ __global__ void chan_partial_scalar(RedArgs r) {
   }
 }
 
-// stage 2: per channel, sum partials in fp64 in block order
+// stage 2: 256 threads = 64 channels x 4 block-lanes, fp64, fixed order
+template <int NQ>
+VU_DEV void colsum2(const float* part, int nblk, int C, int c, double* out) {
+  __shared__ double sh[NQ][4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  double s[NQ];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) s[k] = 0.0;
+  if (c < C)
+    for (int b = q; b < nblk; b += 4)
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) s[k] += part[((int64_t)b * 2 + k) * C + c];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) sh[k][q][cl] = s[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) out[k] = sh[k][0][cl] + sh[k][1][cl] + sh[k][2][cl] + sh[k][3][cl];
+}
+
 __global__ void chan_final_sum(const float* part, int nblk, int C, float* out, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0;
-  for (int b = 0; b < nblk; ++b) s += part[((int64_t)b * 2) * C + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
+  int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s[1];
+  colsum2<1>(part, nblk, C, c, s);
+  if (threadIdx.x < 64 && c < C) out[c] = accumulate ? out[c] + (float)s[0] : (float)s[0];
 }
 
 __global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, int accumulate,
                              float* coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s0 = 0, s1 = 0;
-  for (int b = 0; b < nblk; ++b) {
-    s0 += part[((int64_t)b * 2 + 0) * C + c];
-    s1 += part[((int64_t)b * 2 + 1) * C + c];
-  }
+  int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s[2];
+  colsum2<2>(part, nblk, C, c, s);
+  if (threadIdx.x >= 64 || c >= C) return;
   float g = gamma ? gamma[c] : 1.f;
   float is = invstd[c];
   float k1 = g * is;
   coef[c] = k1;
-  coef[C + c] = (float)(-(double)k1 * is * s1 / (double)P);
-  coef[2 * C + c] = (float)(-(double)k1 * s0 / (double)P);
-  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s1 : (float)s1;
-  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s0 : (float)s0;
+  coef[C + c] = (float)(-(double)k1 * is * s[1] / (double)P);
+  coef[2 * C + c] = (float)(-(double)k1 * s[0] / (double)P);
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s[1] : (float)s[1];
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s[0] : (float)s[0];
 }
 
 template <typename T>
 __global__ void bn_bwd_apply_kernel(const T* dy, int64_t dys, const T* x, int64_t xs, int64_t P, int C,
                                     const float* scale, const float* shift, const float* mean,
                                     const float* coef, int relu, T* dx, int64_t dxs) {
-  int V = C >> 3;
-  int64_t tot = P * V;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int64_t p = e / V;
-    int c = (int)(e - p * V) * 8;
+  ChanMap cm(C);
+  const int c = cm.cv * 8;
+  float sc[8], sf[8], mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[c + i]; sf[i] = shift[c + i]; mu[i] = mean[c + i];
+    k1[i] = coef[c + i]; k2[i] = coef[C + c + i]; k3[i] = coef[2 * C + c + i];
+  }
+  const int64_t step = (int64_t)gridDim.x * cm.R;
+  for (int64_t p = (int64_t)blockIdx.x * cm.R + cm.row; p < P; p += step) {
     Vec8<T> vd, vx, vo;
     vd.load(dy + p * dys + c);
     vx.load(x + p * xs + c);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      int cc = c + i;
       float xv = vx.get(i), dz = vd.get(i);
-      if (relu && !(xv * scale[cc] + shift[cc] > 0.f)) dz = 0.f;
-      vo.set(i, coef[cc] * dz + coef[C + cc] * (xv - mean[cc]) + coef[2 * C + cc]);
+      if (relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+      vo.set(i, k1[i] * dz + k2[i] * (xv - mu[i]) + k3[i]);
     }
     vo.store(dx + p * dxs + c);
   }
@@ -302,30 +328,44 @@ inline unsigned ew_grid(int64_t work) {
   return (unsigned)g;
 }
 
-inline bool vec8_ok(int C, int64_t s0, int64_t s1, int64_t s2 = 0) {
-  return C % 8 == 0 && s0 % 8 == 0 && s1 % 8 == 0 && s2 % 8 == 0;
+inline bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+// vectorised fixed-channel path: C = 8 * 2^k <= 2048, strides multiples of 8
+inline bool chanmap_ok(int C, int64_t s0, int64_t s1, int64_t s2 = 0) {
+  return C % 8 == 0 && pow2(C / 8) && C / 8 <= 256 && s0 % 8 == 0 && s1 % 8 == 0 && s2 % 8 == 0;
+}
+
+// blocks for a fixed-channel stream over P pixels: ~16 pixel rows per thread
+inline unsigned chan_grid(int64_t P, int C, int maxblk) {
+  int R = 256 / (C / 8);
+  int64_t g = (P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
+  if (g > maxblk) g = maxblk;
+  if (g < 1) g = 1;
+  return (unsigned)g;
 }
 
 template <typename T, int MODE>
 int launch_partial(const RedArgs& r, hipStream_t st, int& nblk) {
-  nblk = (int)((r.P + RED_PB - 1) / RED_PB);
-  if (nblk < 1) nblk = 1;
-  bool vec = r.C % 8 == 0 && r.as % 8 == 0 && (MODE == 0 || r.bs % 8 == 0) && r.C / 8 <= 256;
-  if (vec)
+  bool vec = chanmap_ok(r.C, r.as, MODE == 0 ? 8 : r.bs);
+  if (vec) {
+    nblk = (int)chan_grid(r.P, r.C, RED_MAXBLK);
     hipLaunchKernelGGL((chan_partial_kernel<T, MODE>), dim3(nblk), dim3(256), 0, st, r);
-  else if (r.C <= 256)
+  } else if (r.C <= 256) {
+    int R = 256 / r.C;
+    int64_t g = (r.P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
+    nblk = (int)(g > RED_MAXBLK ? RED_MAXBLK : (g < 1 ? 1 : g));
     hipLaunchKernelGGL((chan_partial_scalar<T, MODE>), dim3(nblk), dim3(256), 0, st, r);
-  else
+  } else {
     return (int)hipErrorInvalidValue;
+  }
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
 extern "C" int64_t vu_reduce_workspace_bytes(int64_t P, int C) {
-  int64_t nblk = (P + RED_PB - 1) / RED_PB;
-  if (nblk < 1) nblk = 1;
-  return nblk * 2 * C * (int64_t)sizeof(float);
+  (void)P;
+  return (int64_t)RED_MAXBLK * 2 * C * (int64_t)sizeof(float);
 }
 
 extern "C" int64_t vu_bn_finalize_workspace_bytes(int tiles, int C) {
@@ -366,17 +406,17 @@ extern "C" int vu_bn_apply(const void* x, int64_t xs, void* y, int64_t ys, int64
                            void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (P * C == 0) return 0;
-  bool vec = vec8_ok(C, xs, ys);
+  bool vec = chanmap_ok(C, xs, ys);
   if (dtype == VU_BF16) {
     if (vec)
-      hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+      hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(chan_grid(P, C, 8192)), dim3(256), 0, st,
                          (const bf16_t*)x, xs, (bf16_t*)y, ys, P, C, scale, shift, relu);
     else
       hipLaunchKernelGGL(bn_apply_scalar<bf16_t>, dim3(ew_grid(P * C)), dim3(256), 0, st,
                          (const bf16_t*)x, xs, (bf16_t*)y, ys, P, C, scale, shift, relu);
   } else {
     if (vec)
-      hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+      hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(chan_grid(P, C, 8192)), dim3(256), 0, st,
                          (const float*)x, xs, (float*)y, ys, P, C, scale, shift, relu);
     else
       hipLaunchKernelGGL(bn_apply_scalar<float>, dim3(ew_grid(P * C)), dim3(256), 0, st,
@@ -395,7 +435,7 @@ extern "C" int vu_bn_bwd_reduce(const void* dy, int64_t dys, const void* x, int6
   int nblk = 0, rc;
   rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk) : launch_partial<float, 1>(r, st, nblk);
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64), dim3(64), 0, st, workspace, nblk, C, P,
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64), dim3(256), 0, st, workspace, nblk, C, P,
                      gamma, invstd, dgamma, dbeta, accumulate, coef);
   return (int)hipGetLastError();
 }
@@ -406,10 +446,10 @@ extern "C" int vu_bn_bwd_apply(const void* dy, int64_t dys, const void* x, int64
                                void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (P * C == 0) return 0;
-  bool vec = vec8_ok(C, dys, xs, dxs);
+  bool vec = chanmap_ok(C, dys, xs, dxs);
   if (dtype == VU_BF16) {
     if (vec)
-      hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(chan_grid(P, C, 8192)), dim3(256), 0, st,
                          (const bf16_t*)dy, dys, (const bf16_t*)x, xs, P, C, scale, shift, mean, coef,
                          relu, (bf16_t*)dx, dxs);
     else
@@ -418,7 +458,7 @@ extern "C" int vu_bn_bwd_apply(const void* dy, int64_t dys, const void* x, int64
                          relu, (bf16_t*)dx, dxs);
   } else {
     if (vec)
-      hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_grid(P * C / 8)), dim3(256), 0, st,
+      hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(chan_grid(P, C, 8192)), dim3(256), 0, st,
                          (const float*)dy, dys, (const float*)x, xs, P, C, scale, shift, mean, coef,
                          relu, (float*)dx, dxs);
     else
@@ -438,7 +478,7 @@ extern "C" int vu_chan_sum(const void* x, int64_t stride, int N, int H, int W, i
   int nblk = 0, rc;
   rc = dtype == VU_BF16 ? launch_partial<bf16_t, 0>(r, st, nblk) : launch_partial<float, 0>(r, st, nblk);
   if (rc) return rc;
-  hipLaunchKernelGGL(chan_final_sum, dim3((C + 63) / 64), dim3(64), 0, st, workspace, nblk, C, out,
+  hipLaunchKernelGGL(chan_final_sum, dim3((C + 63) / 64), dim3(256), 0, st, workspace, nblk, C, out,
                      accumulate);
   return (int)hipGetLastError();
 }
