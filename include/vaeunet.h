@@ -52,6 +52,9 @@ typedef struct VuGather {
  * out_mode 0: out[m*out_stride + out_coff + j]
  * out_mode 1: ConvTranspose 2x2/s2 pixel shuffle, j = (a*2+b)*cout + co ->
  *             out pixel (n, 2h+a+opy, 2w+b+opx) of an (oH, oW) image.
+ * out_mode 2: stride-2 sub-lattice: row m -> out pixel (n, 2h+opy, 2w+opx)
+ *             of an (oH, oW) image (one parity class of a stride-2 conv's
+ *             input gradient, ResNet encoder of unet_resnet.py:131).
  * stat_sum/stat_m2 (optional): per (row tile, column) sum and centered M2 of
  * the stored (dtype-rounded) values, for BatchNorm (unet_parts.py:41,44). */
 typedef struct VuGemmFwd {
@@ -171,6 +174,8 @@ int vu_upsample_bwd(const void* dy, int64_t dys, int N, int Hi, int Wi, int C,
                     int py, int px, int accumulate, int dtype, void* stream);
 
 /* ---- attention gate (unet_parts.py:7-30) ------------------------------- */
+/* pixels per statistics tile of vu_attn_psi_fwd */
+int64_t vu_attn_tile_rows(void);
 /* q[p] = bpsi + sum_c wpsi[c] * relu(ug[p,c]*sg[c]+tg[c] + ux[p,c]*sx[c]+tx[c])
  * plus per-tile (sum, M2) of q for BatchNorm2d(1). */
 int vu_attn_psi_fwd(const void* ug, const void* ux, int64_t P, int F,
@@ -178,7 +183,7 @@ int vu_attn_psi_fwd(const void* ug, const void* ux, int64_t P, int F,
                     const float* tx, const float* wpsi, const float* bpsi,
                     float* q, float* psum, float* pm2, int64_t tile_rows,
                     int dtype, void* stream);
-/* p = sigmoid(q*s + t); out[p,c] = x[p,c] * p  (also stores p) */
+/* p = sigmoid(q*st[0] + st[1]); out[p,c] = x[p,c] * p  (also stores p) */
 int vu_attn_gate_fwd(const float* q, const float* st, const void* x,
                      int64_t xs, int64_t P, int C, float* pmap, void* out,
                      int64_t os, int dtype, void* stream);
@@ -188,36 +193,49 @@ int vu_attn_gate_bwd(const void* dout, int64_t dos, const void* x, int64_t xs,
                      const float* pmap, int64_t P, int C, void* dx,
                      int64_t dxs, float* dqpre, int dtype, void* stream);
 /* backward through psi conv + relu: given dq[p] (grad of q), produce
- * ds[p,c] = dq[p]*wpsi[c]*(s>0) as bf16/fp32 for both BN branches (same
- * tensor), dwpsi[c] partials and dbpsi. */
+ * ds[p,c] = dq[p]*wpsi[c]*(s>0) (the gradient of both BN branches), and
+ * dwpsi[c], dbpsi (deterministic partial reduction). */
+int64_t vu_attn_psi_bwd_workspace_bytes(int64_t P, int F);
 int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F,
                     const float* sg, const float* tg, const float* sx,
                     const float* tx, const float* wpsi, const float* dq,
                     void* ds, float* dwpsi, float* dbpsi, int accumulate,
                     float* workspace, int dtype, void* stream);
 
-/* ---- 1x1 conv with a tiny output (OutConv, psi) ------------------------- */
+/* ---- 1x1 conv with a tiny output (OutConv unet_parts.py:97-103,
+ *      final_conv unet_resnet.py:189) -------------------------------------- */
 /* y[p*ys + j] = b[j] + sum_c x[p*xs+c] w[j*C+c], j < J <= 4, y fp32 */
 int vu_pointwise_fwd(const void* x, int64_t xs, int64_t P, int C, int J,
                      const float* w, const float* b, float* y, int64_t ys,
                      int dtype, void* stream);
-/* dx[p,c] = sum_j dy[p,j] w[j,c];  dw[j,c] += sum_p dy x;  db[j] += sum_p dy */
+/* dx[p,c] = sum_j dy[p,j] w[j,c];  dw[j,c] (+)= sum_p dy x;  db[j] (+)= sum_p dy */
+int64_t vu_pointwise_bwd_workspace_bytes(int64_t P, int C, int J);
 int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int64_t dys,
                      int64_t P, int C, int J, const float* w, void* dx,
                      int64_t dxs, float* dw, float* db, int accumulate,
                      float* workspace, int dtype, void* stream);
 
 /* ---- loss (utils/loss.py) ---------------------------------------------- */
+int64_t vu_loss_workspace_bytes(void);
 /* sums[0..3] = {sum BCE-with-logits, sum sigmoid*t, sum sigmoid, sum t} over
- * n elements (fp64 accumulation, deterministic) */
+ * n elements (fp64, deterministic); loss[0] = w_bce*BCE_mean + w_dice*(1-dice)
+ * (CombinedLoss, loss.py:44-63), parts = {BCE_mean, 1-dice} (optional). */
+int vu_bce_dice_fwd2(const float* logits, const float* target, int64_t n,
+                     double* sums, float smooth, float w_bce, float w_dice,
+                     float* loss, float* parts, double* workspace,
+                     void* stream);
 int vu_bce_dice_fwd(const float* logits, const float* target, int64_t n,
                     double* sums, double* workspace, void* stream);
-/* grad = g * d/dlogit (w_bce*BCE_mean + w_dice*(1-dice)) */
+/* grad = g * d/dlogit (w_bce*BCE_mean + w_dice*(1-dice)), g = *gscale */
 int vu_bce_dice_bwd(const float* logits, const float* target, int64_t n,
                     const double* sums, float smooth, float w_bce,
                     float w_dice, const float* gscale, float* grad,
                     void* stream);
-/* kl_with_free_bits (loss.py:148-170), B x L, forward + grads */
+/* kl_with_free_bits (loss.py:148-170), B x L: value and/or grads (scaled by
+ * *gscale when given) */
+int vu_kl_free_bits2(const float* mu, const float* logvar, int B, int L,
+                     float free_bits, const float* gscale, float* value,
+                     float* gmu, float* glogvar, void* stream);
 int vu_kl_free_bits(const float* mu, const float* logvar, int B, int L,
                     float free_bits, float* value, float* gmu, float* glogvar,
                     void* stream);
@@ -226,6 +244,45 @@ int vu_kl_free_bits(const float* mu, const float* logvar, int B, int L,
 /* sum of squares of n fp32 values into out (fp64, deterministic) */
 int vu_sumsq(const float* x, int64_t n, double* out, double* workspace,
              void* stream);
+
+/* ---- VAE-U-Net (unet/unet_resnet.py) ----------------------------------- */
+/* ResNet34 stem max-pool 3x3/s2/p1 (timm resnet34, unet_resnet.py:131):
+ * idx receives the window argmax (0..8, first max wins) per output element */
+int vu_maxpool3s2_fwd(const void* x, int64_t xs, int N, int H, int W, int C,
+                      void* y, int64_t ys, uint8_t* idx, int dtype,
+                      void* stream);
+int vu_maxpool3s2_bwd(const void* dy, int64_t dys, const uint8_t* idx, int N,
+                      int H, int W, int C, void* dx, int64_t dxs,
+                      int accumulate, int dtype, void* stream);
+/* BasicBlock tail: out = relu(y*sc+sh + (r*rsc+rsh | r)) */
+int vu_bn_add_relu(const void* y, int64_t ys, const float* sc, const float* sh,
+                   const void* r, int64_t rs, const float* rsc,
+                   const float* rsh, int64_t P, int C, void* out, int64_t os,
+                   int dtype, void* stream);
+/* g = dout * (out > 0) */
+int vu_relu_mask(const void* dout, int64_t ds, const void* out, int64_t os,
+                 int64_t P, int C, void* g, int64_t gs, int dtype,
+                 void* stream);
+/* out[n][c] (+)= scale * sum over the HW pixels of sample n (avg-pool head,
+ * latent-broadcast backward) */
+int vu_sample_sum(const void* x, int64_t xs, int N, int HW, int C, float scale,
+                  float* out, int accumulate, int dtype, void* stream);
+/* y[n,p,c] (+)= scale * v[n][c]: interpolate(z[...,None,None], align_corners)
+ * as an exact broadcast (unet_resnet.py:217-221, 93) */
+int vu_sample_broadcast(const float* v, int N, int HW, int C, float scale,
+                        void* y, int64_t ys, int accumulate, int dtype,
+                        void* stream);
+/* mu/logvar heads after pooling: y[b][j] = bias[j] + sum_k x[b][k] w[j][k] */
+int vu_linear_small_fwd(const float* x, int B, int K, const float* w,
+                        const float* bias, int J, float* y, void* stream);
+int vu_linear_small_bwd(const float* x, int B, int K, const float* w, int J,
+                        const float* dy, float* dx, int dx_acc, float* dw,
+                        float* db, int w_acc, void* stream);
+/* reparameterize (unet_resnet.py:191-194): z = mu + eps*exp(0.5*logvar) */
+int vu_reparam_fwd(const float* mu, const float* lv, const float* eps, int n,
+                   float* z, void* stream);
+int vu_reparam_bwd(const float* lv, const float* eps, const float* dz, int n,
+                   float* dmu, float* dlv, int accumulate, void* stream);
 
 #ifdef __cplusplus
 }

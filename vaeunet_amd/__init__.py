@@ -6,3 +6,4 @@ Drop-in surface (same names / signatures / state_dict keys as the reference):
 """
 from .unet_model import UNet  # noqa: F401
 from .unet_parts import AttentionGate, DoubleConv, Down, Up, OutConv  # noqa: F401
+from .unet_resnet import UNetResNet, DecoderBlock  # noqa: F401,E402

@@ -239,6 +239,13 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
     T* dst;
     if (p.out_mode == 0) {
       dst = out + m * p.out_stride + p.out_coff + gj;
+    } else if (p.out_mode == 2) {
+      // stride-2 sub-lattice (input gradient of a stride-2 conv, one parity)
+      int hw = g.H * g.W;
+      int n = (int)(m / hw);
+      int rem = (int)(m - (int64_t)n * hw);
+      int h = rem / g.W, w = rem - (rem / g.W) * g.W;
+      dst = out + (((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx) * p.out_stride + p.out_coff + gj;
     } else {
       int hw = g.H * g.W;
       int n = (int)(m / hw);
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
       v.store(dst);
     } else {
       for (int q = 0; q < 8 && gj + q < p.ncol; ++q) {
-        if (p.out_mode == 0) st1<T>(dst + q, p.accumulate ? ld1<T>(dst + q) + src[q] : src[q]);
+        if (p.out_mode != 1) st1<T>(dst + q, p.accumulate ? ld1<T>(dst + q) + src[q] : src[q]);
         else {
           // scalar scatter (ragged cout)
           int jj = gj + q, ab = jj / p.cout, co = jj - ab * p.cout;

@@ -138,9 +138,10 @@ class Stats:
 
 
 def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
-             convT=None, kind="fwd"):
+             convT=None, kind="fwd", strided=None):
     """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
-    the pixel-shuffle epilogue.  Returns Stats if requested."""
+    the pixel-shuffle epilogue, strided=(oH,oW,opy,opx) the stride-2 sub-lattice one.
+    Returns Stats if requested."""
     a = VuGemmFwd()
     a.a = g
     a.b = wmat.data_ptr()
@@ -152,6 +153,10 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     if convT is not None:
         a.out_mode = 1
         a.oH, a.oW, a.opy, a.opx, a.cout = convT
+    elif strided is not None:
+        a.out_mode = 2
+        a.oH, a.oW, a.opy, a.opx = strided
+        a.cout = ncol
     else:
         a.out_mode = 0
     a.bias = bias.data_ptr() if bias is not None else None

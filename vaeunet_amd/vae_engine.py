@@ -1,0 +1,395 @@
+"""Fused sequences for the VAE-U-Net (unet/unet_resnet.py:31-279).
+
+* ResNet34 encoder (timm ``resnet34`` features_only, unet_resnet.py:131-137):
+  7x7/s2 stem + BN + ReLU, 3x3/s2 max-pool, BasicBlocks [3, 4, 6, 3].  All
+  convolutions run on the implicit-GEMM kernels; stride-2 convolutions get
+  their input gradient as four parity-class GEMMs (out_mode 2), so no
+  zero-inserted tensor is ever built.
+* VAE bottleneck: the conv1x1 + AdaptiveAvgPool2d heads (unet_resnet.py:
+  140-147) are computed as a per-sample channel mean followed by a [L x C]
+  map (pool and 1x1 conv commute), reparameterisation (191-194), and the
+  latent broadcast ``interpolate(z[..., None, None], size, align_corners=True)``
+  which is an exact per-sample broadcast (217-221, 93).
+* DecoderBlock (31-101): bilinear(align_corners) to the skip size, attention
+  gate, z_proj, three-source channel concat fed straight into conv1's K loop.
+"""
+import torch
+
+from . import engine as E
+from . import kernels as K
+from ._lib import F32
+
+
+# ---------------------------------------------------------------------------
+# generic convolution (square kernel k, stride s, padding p, no dilation)
+# ---------------------------------------------------------------------------
+def _geom(conv):
+    return conv.kernel_size[0], conv.stride[0], conv.padding[0]
+
+
+def conv_gather(srcs, conv):
+    N, _, H, W = srcs[0].shape
+    k, s, p = _geom(conv)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    return K.gather(srcs, N, Ho, Wo, R=k, S=k, sy=s, sx=s, oy=-p, ox=-p), Ho, Wo
+
+
+def conv_fwd(M, srcs, conv, stats, cin_pad=None):
+    g, Ho, Wo = conv_gather(srcs, conv)
+    co = conv.out_channels
+    y = M.act(srcs[0].shape[0], co, Ho, Wo)
+    st = K.gemm_fwd(g, E.w3x3_fwd(conv.weight, M.d, cin_pad), co, y, M.d,
+                    bias=conv.bias, stats=stats)
+    return y, st
+
+
+def conv_wgrad(M, dy, srcs, conv, cvalid=None):
+    gw, acc = E.grad_sink(conv.weight)
+    if gw is not None:
+        g, _, _ = conv_gather(srcs, conv)
+        K.gemm_wgrad(K.gather1x1([dy]), g, dy.shape[1], g.R * g.S * g.C, gw, E.conv_layout(gw), M.d,
+                     acc, cvalid=cvalid)
+    if conv.bias is not None:
+        E.bias_grad(dy, conv.bias, M)
+
+
+def _parity_w(w, py, px, p, d):
+    """Input-gradient weights of one parity class of a stride-2 conv:
+    B[ci][(ry*Sx + rx)*Cout + co] over the taps r = py+p (mod 2), descending."""
+    co, ci, k, _ = w.shape
+    ry = [r for r in range(k) if (r - py - p) % 2 == 0]
+    rx = [r for r in range(k) if (r - px - p) % 2 == 0]
+    if not ry or not rx:
+        return None, ry, rx
+
+    def build():
+        s = w.stride()
+        base = max(ry) * s[2] + max(rx) * s[3]
+        return K.permute4(w.detach(), base, (s[1], -2 * s[2], -2 * s[3], s[0]),
+                          (ci, len(ry), len(rx), co), co, d).view(ci, -1)
+    return E._cached(w, ("wpar", d, py, px), build), ry, rx
+
+
+def conv_dgrad(M, dy, conv, dx, accumulate):
+    """dx (N, Cin, H, W) (+)= conv input gradient of dy."""
+    k, s, p = _geom(conv)
+    N, ci, H, W = dx.shape
+    if s == 1:
+        if 2 * p != k - 1:
+            raise NotImplementedError("stride-1 conv input gradient needs 'same' padding")
+        g = K.gather([dy], N, H, W, R=k, S=k, oy=p - (k - 1), ox=p - (k - 1))
+        K.gemm_fwd(g, E.w3x3_dgrad(conv.weight, M.d), ci, dx, M.d, accumulate=accumulate,
+                   kind="dgrad")
+        return dx
+    if s != 2:
+        raise NotImplementedError("only stride 1 and 2 convolutions")
+    if not accumulate:
+        dx.zero_()
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    for py in (0, 1):
+        for px in (0, 1):
+            wmat, ry, rx = _parity_w(conv.weight, py, px, p, M.d)
+            hp, wp = (H - py + 1) // 2, (W - px + 1) // 2
+            if wmat is None or hp <= 0 or wp <= 0:
+                continue
+            oy = (py + p - max(ry)) // 2
+            ox = (px + p - max(rx)) // 2
+            g = K.gather([dy], N, hp, wp, R=len(ry), S=len(rx), oy=oy, ox=ox, Hs=Ho, Ws=Wo)
+            K.gemm_fwd(g, wmat, ci, dx, M.d, accumulate=True, kind="dgrad",
+                       strided=(H, W, py, px))
+    return dx
+
+
+# ---------------------------------------------------------------------------
+# ResNet34 BasicBlock (timm) and encoder
+# ---------------------------------------------------------------------------
+def basic_fwd(M, blk, x):
+    train = blk.bn1.training
+    y1, st1 = conv_fwd(M, [x], blk.conv1, train)
+    c1 = E.bn_coef(blk.bn1, st1, y1.shape[1])
+    a1 = torch.empty_like(y1)
+    K.bn_apply(y1, a1, c1, True, M.d)
+    y2, st2 = conv_fwd(M, [a1], blk.conv2, train)
+    c2 = E.bn_coef(blk.bn2, st2, y2.shape[1])
+    yd = cd = None
+    if blk.downsample is not None:
+        yd, std = conv_fwd(M, [x], blk.downsample[0], train)
+        cd = E.bn_coef(blk.downsample[1], std, yd.shape[1])
+    out = torch.empty_like(y2)
+    N, C_, H, W = y2.shape
+    r = yd if yd is not None else x
+    K.call("vu_bn_add_relu", K.ptr(y2), K.pstride(y2), K.ptr(c2[0]), K.ptr(c2[1]), K.ptr(r),
+           K.pstride(r), K.ptr(cd[0]) if cd is not None else None,
+           K.ptr(cd[1]) if cd is not None else None, N * H * W, C_, K.ptr(out), K.pstride(out),
+           M.d, K.stream())
+    return out, (x, y1, c1, a1, y2, c2, yd, cd, out)
+
+
+def basic_bwd(M, blk, saved, dout, need_dx=True):
+    x, y1, c1, a1, y2, c2, yd, cd, out = saved
+    N, C_, H, W = out.shape
+    g = torch.empty_like(out)
+    K.call("vu_relu_mask", K.ptr(dout), K.pstride(dout), K.ptr(out), K.pstride(out), N * H * W, C_,
+           K.ptr(g), K.pstride(g), M.d, K.stream())
+    dy2 = E.bn_bwd(g, y2, c2, blk.bn2, False, M)
+    conv_wgrad(M, dy2, [a1], blk.conv2)
+    da1 = conv_dgrad(M, dy2, blk.conv2, torch.empty_like(a1), False)
+    dy1 = E.bn_bwd(da1, y1, c1, blk.bn1, True, M)
+    conv_wgrad(M, dy1, [x], blk.conv1)
+    M.notify([blk.conv1.weight, blk.conv2.weight, blk.bn1.weight, blk.bn1.bias,
+              blk.bn2.weight, blk.bn2.bias])
+    dx = None
+    if need_dx:
+        dx = conv_dgrad(M, dy1, blk.conv1, torch.empty_like(x), False)
+    if blk.downsample is not None:
+        dyd = E.bn_bwd(g, yd, cd, blk.downsample[1], False, M)
+        conv_wgrad(M, dyd, [x], blk.downsample[0])
+        M.notify([blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias])
+        if need_dx:
+            conv_dgrad(M, dyd, blk.downsample[0], dx, True)
+    elif need_dx:
+        K.copy(g, dx, accumulate=True)
+    return dx
+
+
+def encoder_fwd(M, enc, xa, cin_pad):
+    train = enc.bn1.training
+    y0, st0 = conv_fwd(M, [xa], enc.conv1, train, cin_pad=cin_pad)
+    c0 = E.bn_coef(enc.bn1, st0, y0.shape[1])
+    f0 = torch.empty_like(y0)
+    K.bn_apply(y0, f0, c0, True, M.d)
+    N, C_, H, W = f0.shape
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    pm = M.act(N, C_, Ho, Wo)
+    idx = torch.empty((N, Ho, Wo, C_), dtype=torch.uint8, device=f0.device)
+    K.call("vu_maxpool3s2_fwd", K.ptr(f0), K.pstride(f0), N, H, W, C_, K.ptr(pm), K.pstride(pm),
+           K.ptr(idx), M.d, K.stream())
+    feats = [f0]
+    states = []
+    h = pm
+    for layer in (enc.layer1, enc.layer2, enc.layer3, enc.layer4):
+        ls = []
+        for blk in layer:
+            h, s = basic_fwd(M, blk, h)
+            ls.append(s)
+        states.append(ls)
+        feats.append(h)
+    return feats, (xa, y0, c0, f0, idx, states)
+
+
+def encoder_bwd(M, enc, state, dfeats, cvalid):
+    """dfeats: gradients of the five features (None = no gradient)."""
+    xa, y0, c0, f0, idx, states = state
+    layers = (enc.layer1, enc.layer2, enc.layer3, enc.layer4)
+    d = None
+    for li in range(3, -1, -1):
+        df = dfeats[li + 1]
+        if df is not None:
+            if d is None:
+                d = df
+            else:
+                K.copy(df, d, accumulate=True)
+        if d is None:
+            continue
+        for blk, s in zip(reversed(list(layers[li])), reversed(states[li])):
+            d = basic_bwd(M, blk, s, d)
+    N, C_, H, W = f0.shape
+    dfz = torch.empty_like(f0)
+    if d is not None:
+        K.call("vu_maxpool3s2_bwd", K.ptr(d), K.pstride(d), K.ptr(idx), N, H, W, C_, K.ptr(dfz),
+               K.pstride(dfz), 0, M.d, K.stream())
+    else:
+        dfz.zero_()
+    if dfeats[0] is not None:
+        K.copy(dfeats[0], dfz, accumulate=True)
+    dy0 = E.bn_bwd(dfz, y0, c0, enc.bn1, True, M)
+    conv_wgrad(M, dy0, [xa], enc.conv1, cvalid=cvalid)
+    M.notify([enc.conv1.weight, enc.bn1.weight, enc.bn1.bias])
+
+
+# ---------------------------------------------------------------------------
+# 1x1 conv + BN + ReLU on a latent broadcast (z_initial 150-154, z_proj 37-41)
+# ---------------------------------------------------------------------------
+def latent_map(M, z, N, H, W):
+    """[B, L] fp32 -> spatially constant NHWC [B, L, H, W] in the storage dtype."""
+    L = z.shape[1]
+    zb = M.act(N, L, H, W)
+    K.call("vu_sample_broadcast", K.ptr(z), N, H * W, L, 1.0, K.ptr(zb), K.pstride(zb), 0, M.d,
+           K.stream())
+    return zb
+
+
+def cbr1x1_fwd(M, seq, x):
+    conv, bn = seq[0], seq[1]
+    y, st = conv_fwd(M, [x], conv, bn.training)
+    c = E.bn_coef(bn, st, y.shape[1])
+    a = torch.empty_like(y)
+    K.bn_apply(y, a, c, True, M.d)
+    return a, (x, y, c)
+
+
+def cbr1x1_bwd(M, seq, saved, da):
+    conv, bn = seq[0], seq[1]
+    x, y, c = saved
+    dy = E.bn_bwd(da, y, c, bn, True, M)
+    conv_wgrad(M, dy, [x], conv)
+    M.notify([conv.weight, conv.bias, bn.weight, bn.bias])
+    dx = torch.empty_like(x)
+    K.gemm_fwd(K.gather1x1([dy]), E.w1x1_dgrad(conv.weight, M.d), x.shape[1], dx, M.d,
+               kind="dgrad")
+    return dx
+
+
+def sample_sum(M, x, scale=1.0, out=None, accumulate=False):
+    N, C_, H, W = x.shape
+    if out is None:
+        out = torch.empty((N, C_), dtype=torch.float32, device=x.device)
+    K.call("vu_sample_sum", K.ptr(x), K.pstride(x), N, H * W, C_, float(scale), K.ptr(out),
+           1 if accumulate else 0, K.dcode(x.dtype), K.stream())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# DecoderBlock (unet_resnet.py:31-101)
+# ---------------------------------------------------------------------------
+def decoder_fwd(M, blk, x, skip, z):
+    N = x.shape[0]
+    if skip is not None:
+        H, W = skip.shape[2], skip.shape[3]
+    else:
+        H, W = 2 * x.shape[2], 2 * x.shape[3]
+    xu = M.act(N, x.shape[1], H, W)
+    K.upsample_fwd(x, xu, H, W, 0, 0, M.d)
+    srcs = [xu]
+    satt = None
+    if skip is not None and blk.use_skip:
+        if blk.use_attention:
+            sk, satt = E.attention_fwd(M, blk.attention, xu, skip)
+        else:
+            sk = skip
+        srcs.append(sk)
+    szp = None
+    if blk.use_latent:
+        zb = latent_map(M, z, N, H, W)
+        zp, szp = cbr1x1_fwd(M, blk.z_proj, zb)
+        srcs.append(zp)
+    a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1])
+    a2, s2 = E.conv_bn_relu_fwd(M, [a1], blk.conv2[0], blk.conv2[1])
+    return a2, (x, skip, xu, srcs, satt, szp, a1, s1, s2)
+
+
+def decoder_bwd(M, blk, saved, dout):
+    """-> (dx, dskip or None, dz [B, L] fp32 or None)."""
+    x, skip, xu, srcs, satt, szp, a1, s1, s2 = saved
+    da1 = E.conv_bn_relu_bwd(M, [a1], blk.conv2[0], blk.conv2[1], s2, dout, True)
+    dsrc = E.conv_bn_relu_bwd(M, srcs, blk.conv1[0], blk.conv1[1], s1, da1, True)
+    cx = xu.shape[1]
+    off = cx
+    dskip = dz = None
+    if skip is not None and blk.use_skip:
+        cs = skip.shape[1]
+        dsk = dsrc[:, off:off + cs]
+        if blk.use_attention:
+            dskip = E.attention_bwd(M, blk.attention, satt, dsk, (dsrc, 0), True)
+        else:
+            dskip = dsk
+        off += cs
+    if blk.use_latent:
+        dzp = dsrc[:, off:]
+        dzb = cbr1x1_bwd(M, blk.z_proj, szp, dzp)
+        dz = sample_sum(M, dzb)
+    dx = torch.empty_like(x)
+    H, W = xu.shape[2], xu.shape[3]
+    K.upsample_bwd(dsrc[:, :cx], dx, H, W, 0, 0, False, M.d)
+    return dx, dskip, dz
+
+
+# ---------------------------------------------------------------------------
+# whole UNetResNet forward / backward (unet_resnet.py:196-240)
+# ---------------------------------------------------------------------------
+def vae_fwd(M, model, x, eps):
+    N, cin, Hin, Win = x.shape
+    cp = (cin + 7) // 8 * 8
+    xa = E.to_act(M, x, cp)
+    feats, senc = encoder_fwd(M, model.encoder, xa, cp)
+    f4 = feats[-1]
+    H4, W4 = f4.shape[2], f4.shape[3]
+    pooled = sample_sum(M, f4, 1.0 / (H4 * W4))
+    L = model.latent_dim
+    mu = torch.empty((N, L), dtype=torch.float32, device=x.device)
+    logvar = torch.empty_like(mu)
+    for head, out in ((model.mu_head[0], mu), (model.logvar_head[0], logvar)):
+        K.call("vu_linear_small_fwd", K.ptr(pooled), N, f4.shape[1], K.ptr(head.weight),
+               K.ptr(head.bias), L, K.ptr(out), K.stream())
+    sampling = model.latent_injection not in ("none", "inject_no_bottleneck")
+    if not sampling:
+        eps = None
+    z = torch.empty_like(mu)
+    K.call("vu_reparam_fwd", K.ptr(mu), K.ptr(logvar), K.ptr(eps), N * L, K.ptr(z), K.stream())
+    szi = None
+    if model.use_bottleneck:
+        h, szi = cbr1x1_fwd(M, model.z_initial, latent_map(M, z, N, H4, W4))
+    else:
+        h = f4
+    sdec = []
+    for i, blk in enumerate(model.decoder_blocks):
+        skip = feats[-(i + 2)] if (i < len(feats) - 1 and model.use_skip) else None
+        h, s = decoder_fwd(M, blk, h, skip, z)
+        sdec.append(s)
+    small, sfc = E.outconv_fwd(M, model.final_conv, h)
+    out = torch.empty((N, small.shape[1], Hin, Win), dtype=torch.float32, device=x.device,
+                      memory_format=torch.channels_last)
+    K.upsample_fwd(small, out, Hin, Win, 0, 0, F32)
+    return out, mu, logvar, (senc, feats, pooled, eps, logvar, szi, sdec, sfc, small, cin)
+
+
+def vae_bwd(M, model, state, dout, dmu, dlogvar):
+    senc, feats, pooled, eps, logvar, szi, sdec, sfc, small, cin = state
+    N = small.shape[0]
+    dsmall = torch.empty_like(small)
+    if dout is not None:
+        dout = dout.float().contiguous(memory_format=torch.channels_last)
+        K.upsample_bwd(dout, dsmall, dout.shape[2], dout.shape[3], 0, 0, False, F32)
+    else:
+        dsmall.zero_()
+    dh = E.outconv_bwd(M, model.final_conv, sfc, dsmall)
+    L = model.latent_dim
+    dz = torch.zeros((N, L), dtype=torch.float32, device=small.device)
+    dfeats = [None] * 5
+    for i in range(len(model.decoder_blocks) - 1, -1, -1):
+        dh, dskip, dzi = decoder_bwd(M, model.decoder_blocks[i], sdec[i], dh)
+        if dskip is not None:
+            dfeats[3 - i] = dskip
+        if dzi is not None:
+            K.call("vu_sample_broadcast", K.ptr(dzi), 1, 1, N * L, 1.0, K.ptr(dz), N * L, 1, F32,
+                   K.stream())
+    if model.use_bottleneck:
+        dzs = cbr1x1_bwd(M, model.z_initial, szi, dh)
+        sample_sum(M, dzs, 1.0, out=dz, accumulate=True)
+        df4 = None
+    else:
+        df4 = dh
+    dmu_t = dmu.float().contiguous().clone() if dmu is not None else torch.zeros_like(dz)
+    dlv_t = dlogvar.float().contiguous().clone() if dlogvar is not None else torch.zeros_like(dz)
+    K.call("vu_reparam_bwd", K.ptr(logvar), K.ptr(eps), K.ptr(dz), N * L, K.ptr(dmu_t),
+           K.ptr(dlv_t), 1, K.stream())
+    f4 = feats[-1]
+    C4, HW4 = f4.shape[1], f4.shape[2] * f4.shape[3]
+    dpooled = torch.empty((N, C4), dtype=torch.float32, device=f4.device)
+    first = True
+    for head, dh_ in ((model.mu_head[0], dmu_t), (model.logvar_head[0], dlv_t)):
+        gw, acc = E.grad_sink(head.weight)
+        gb, _ = E.grad_sink(head.bias)
+        K.call("vu_linear_small_bwd", K.ptr(pooled), N, C4, K.ptr(head.weight), L, K.ptr(dh_),
+               K.ptr(dpooled), 0 if first else 1, K.ptr(gw), K.ptr(gb), 1 if acc else 0, K.stream())
+        first = False
+        M.notify([head.weight, head.bias])
+    if df4 is None:
+        df4 = M.act(N, C4, f4.shape[2], f4.shape[3])
+        K.call("vu_sample_broadcast", K.ptr(dpooled), N, HW4, C4, 1.0 / HW4, K.ptr(df4),
+               K.pstride(df4), 0, M.d, K.stream())
+    else:
+        K.call("vu_sample_broadcast", K.ptr(dpooled), N, HW4, C4, 1.0 / HW4, K.ptr(df4),
+               K.pstride(df4), 1, M.d, K.stream())
+    dfeats[4] = df4
+    encoder_bwd(M, model.encoder, senc, dfeats, cin)
