@@ -88,6 +88,8 @@ typedef struct VuGemmWgrad {
 int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream);
 int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype);  /* BM used */
 int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream);
+/* output tile (BI x BJ) the dispatcher picks for this problem (split-K sizing) */
+int vu_gemm_wgrad_tile(const VuGemmWgrad* args, int dtype, int* bi, int* bj);
 /* out[i*s_i + (j / C)*s_tap + (j % C)*s_c] (=|+=) sum_s slab[s][i][j],
  * skipping channels (j % C) >= cvalid (zero-padded input channels) */
 int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,

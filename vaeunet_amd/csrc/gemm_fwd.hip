@@ -20,6 +20,7 @@
 // stages the fp32 tile through LDS, computes per-tile BatchNorm partial
 // statistics (sum, centered M2) on the dtype-rounded values and writes
 // 16-byte coalesced rows.
+#include <stdlib.h>
 #include "common.h"
 #include "../../include/vaeunet.h"
 
@@ -319,8 +320,24 @@ int dispatch_fwd(const VuGemmFwd& p, hipStream_t st) {
 
 }  // namespace
 
+// large-tile LDS-DMA variant (gemm_fwd2.hip)
+int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st);
+
+static bool use_v2(int dtype) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VU_GEMM_V2");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode == 1 && dtype == VU_BF16;
+}
+
 extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
-  (void)dtype;
+  if (use_v2(dtype)) {
+    int bm = gemm_fwd_v2_bm(*args, dtype);
+    if (bm) return bm;
+  }
   return pick_bm(*args);
 }
 
@@ -332,5 +349,6 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
     if (g.cend[t] % epc != 0 || g.stride[t] % epc != 0) return (int)hipErrorInvalidValue;
   if ((args->ldb % epc) != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);
 }

@@ -1,0 +1,260 @@
+// Implicit-GEMM forward-type kernel, large-tile bf16 variant ("v2").
+//
+// Same contract as gemm_fwd.hip (out[m][j] = sum_k A[m][k] B[j][k], A an
+// im2col gather of up to three NHWC sources), used for the big bf16 layers
+// where the 128x128 register-staged kernel is LDS-write bound:
+//   * 8 waves (512 threads), block tile 256 x 128 (waves 4x2, 64x64 each) or
+//     256 x 64 (waves 8x1, 32x64 each) for the 64-channel layers;
+//   * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per
+//     lane, no VGPR staging, no ds_write): each lane computes its own gather
+//     address — zero padding and M/N tails point the lane at a 16-byte zero
+//     page — and the XOR swizzle is applied on the SOURCE chunk so the LDS
+//     image stays lane-linear (cdna_hip_programming §5.4 rule 21);
+//   * double-buffered LDS, one barrier per 64-deep K step, 16x16x32 bf16 MFMA,
+//     conflict-free ds_read_b128 fragment reads;
+//   * epilogue: fp32 tile staged through LDS, BatchNorm partial statistics on
+//     the bf16-rounded values, 16-byte coalesced stores (same as v1).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page[16];  // 16 B of zeros: padding lanes DMA from here
+
+namespace {
+
+constexpr int KB = 128;  // bytes of K per LDS row per step (64 bf16)
+typedef __attribute__((address_space(3))) void lds_void;
+
+VU_DEV int swz(int row, int chunk) { return row * KB + ((chunk ^ (row & 7)) << 4); }
+
+struct Pix { int n, h, w; bool ok; };
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd p) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int EPC = 8;                  // bf16 per 16-byte chunk
+  constexpr int BKE = 64;                 // K elements per step
+  constexpr int LA = BM * 8 / NT;         // A glds per thread per step
+  constexpr int LB = BN * 8 / NT;         // B glds per thread per step
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int ES = BN + 4;
+  constexpr int STAGE = (BM + BN) * KB;
+  constexpr int MAIN = 2 * STAGE;
+  constexpr int EPI = BM * ES * 4;
+  constexpr int RED = (NT / BN) * BN * 4;
+  constexpr int LDS_BYTES = (MAIN > EPI ? MAIN : EPI) + RED;
+  static_assert(LA >= 1 && LB >= 1, "tile too small for the thread count");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const VuGather& g = p.a;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  const int K = g.R * g.S * g.C;
+  const int mtiles = (int)((M + BM - 1) / BM);
+  const int ntiles = (p.ncol + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int n0 = nt * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int pchunk = lane & 7;  // physical chunk this lane writes
+
+  // rows this thread loads: row = (i*NT + tid) / 8
+  Pix pa[LA];
+#pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    int row = (i * NT + tid) >> 3;
+    int64_t m = m0 + row;
+    pa[i].ok = m < M;
+    int64_t mm = pa[i].ok ? m : 0;
+    int hw = g.H * g.W;
+    pa[i].n = (int)(mm / hw);
+    int rem = (int)(mm - (int64_t)pa[i].n * hw);
+    pa[i].h = rem / g.W;
+    pa[i].w = rem - pa[i].h * g.W;
+  }
+  const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
+  const void* zp = (const void*)vu_zero_page;
+
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * BKE;
+    const int tap = k0 / g.C;
+    const int r = tap / g.S, s = tap - (tap / g.S) * g.S;
+    const int cbase = k0 - tap * g.C;
+    const int t = (cbase >= g.cend[0]) + (g.nsrc > 2 && cbase >= g.cend[1]);
+    const int c0 = t == 0 ? 0 : g.cend[t - 1];
+    const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[t]);
+    const int64_t st = g.stride[t];
+    char* A = smem + buf * STAGE;
+    char* B = A + BM * KB;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      int row = (i * NT + tid) >> 3;
+      int lchunk = pchunk ^ (row & 7);
+      int hs = pa[i].h * g.sy + r * g.dy + g.oy;
+      int ws = pa[i].w * g.sx + s * g.dx + g.ox;
+      const void* gp = zp;
+      if (pa[i].ok && (unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws) {
+        int64_t pix = ((int64_t)pa[i].n * g.Hs + hs) * g.Ws + ws;
+        gp = src + pix * st + (cbase - c0) + lchunk * EPC;
+      }
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      int row = (i * NT + tid) >> 3;
+      int lchunk = pchunk ^ (row & 7);
+      int j = n0 + row;
+      const void* gp = zp;
+      if (j < p.ncol) gp = bmat + (int64_t)j * p.ldb + k0 + lchunk * EPC;
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  const int nk = K / BKE;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const char* A = smem + cur * STAGE;
+    const char* B = A + BM * KB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 af[TM], bf[TN];
+      const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *reinterpret_cast<const u32x4*>(A + swz(wm * (BM / WM) + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[j] = *reinterpret_cast<const u32x4*>(B + swz(wn * (BN / WN) + j * 16 + (lane & 15), ch));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                              __builtin_bit_cast(bf16x8, bf[j]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue (as gemm_fwd.hip) ----
+  float* E = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      int col = wn * (BN / WN) + j * 16 + (lane & 15);
+      int gj = n0 + col;
+      float bv = 0.f;
+      if (p.bias && gj < p.ncol) bv = p.bias[gj];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = wm * (BM / WM) + i * 16 + 4 * (lane >> 4) + r;
+        E[row * ES + col] = rnd<bf16_t>(acc[i][j][r] + bv);
+      }
+    }
+  __syncthreads();
+
+  const int rows_valid = (int)((M - m0) < BM ? (M - m0) : BM);
+  if (p.stat_sum) {
+    float* red = reinterpret_cast<float*>(smem + LDS_BYTES - RED);
+    constexpr int PARTS = NT / BN;
+    constexpr int RPP = BM / PARTS;
+    const int col = tid % BN, part = tid / BN;
+    float s = 0.f;
+    for (int r = part * RPP; r < (part + 1) * RPP; ++r)
+      if (r < rows_valid) s += E[r * ES + col];
+    red[part * BN + col] = s;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int q = 0; q < PARTS; ++q) tot += red[q * BN + col];
+    const float mean = tot / (float)rows_valid;
+    float m2 = 0.f;
+    for (int r = part * RPP; r < (part + 1) * RPP; ++r)
+      if (r < rows_valid) { float d = E[r * ES + col] - mean; m2 += d * d; }
+    __syncthreads();
+    red[part * BN + col] = m2;
+    __syncthreads();
+    if (part == 0 && n0 + col < p.ncol) {
+      float tm2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < PARTS; ++q) tm2 += red[q * BN + col];
+      p.stat_sum[(int64_t)mt * p.ncol + n0 + col] = tot;
+      p.stat_m2[(int64_t)mt * p.ncol + n0 + col] = tm2;
+    }
+  }
+
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  constexpr int CPR = BN / 8;
+  for (int e = tid; e < BM * CPR; e += NT) {
+    int row = e / CPR, cc = (e - row * CPR) * 8;
+    if (row >= rows_valid) continue;
+    int gj = n0 + cc;
+    if (gj >= p.ncol) continue;
+    int64_t m = m0 + row;
+    bf16_t* dst;
+    if (p.out_mode == 2) {
+      int hw = g.H * g.W;
+      int n = (int)(m / hw);
+      int rem = (int)(m - (int64_t)n * hw);
+      int h = rem / g.W, w = rem - (rem / g.W) * g.W;
+      dst = out + (((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx) * p.out_stride + p.out_coff + gj;
+    } else {
+      dst = out + m * p.out_stride + p.out_coff + gj;
+    }
+    const float* src = E + row * ES + cc;
+    Vec8<bf16_t> v;
+    if (p.accumulate) {
+      v.load(dst);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + src[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v.set(q, src[q]);
+    }
+    v.store(dst);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch(const VuGemmFwd& p, hipStream_t st) {
+  int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  int64_t nblk = ((M + BM - 1) / BM) * ((p.ncol + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_fwd_v2_kernel<BM, BN, WM, WN>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Row tile of the v2 kernel for this problem, or 0 when v2 does not apply
+// (fp32, unaligned channel groups, ConvT pixel-shuffle epilogue, ragged
+// column counts, or too few tiles to fill the chip).
+int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
+  const VuGather& g = p.a;
+  if (dtype != VU_BF16 || p.out_mode == 1) return 0;
+  if (g.C % 64 != 0) return 0;
+  for (int t = 0; t < g.nsrc; ++t)
+    if (g.cend[t] % 64 != 0 || g.stride[t] % 8 != 0) return 0;
+  if (p.ncol % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0) return 0;
+  int64_t M = (int64_t)g.N * g.H * g.W;
+  int bn = p.ncol <= 64 ? 64 : 128;
+  int64_t tiles = ((M + 255) / 256) * ((p.ncol + bn - 1) / bn);
+  if (tiles < 256) return 0;
+  return 256;
+}
+
+int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st) {
+  if (p.ncol <= 64) return launch<256, 64, 8, 1>(p, st);
+  return launch<256, 128, 4, 2>(p, st);
+}

@@ -14,6 +14,7 @@
 // the transposed reads bank-conflict free.  fp32: MFMA 16x16x4 f32, one
 // ds_read_b32 per operand (lanes on consecutive columns, rows padded).
 // Split-K over m writes fp32 slabs, reduced in a fixed order (deterministic).
+#include <stdlib.h>
 #include "common.h"
 #include "../../include/vaeunet.h"
 
@@ -283,6 +284,26 @@ __global__ void slab_reduce_kernel(const float* slab, int splits, int ni, int nj
 
 }  // namespace
 
+int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj);
+int gemm_wgrad_v2_launch(const VuGemmWgrad& p, hipStream_t st);
+
+static bool use_v2w(int dtype) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VU_GEMM_V2");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode == 1 && dtype == VU_BF16;
+}
+
+// output tile the dispatcher will use (host split-K heuristic)
+extern "C" int vu_gemm_wgrad_tile(const VuGemmWgrad* args, int dtype, int* bi, int* bj) {
+  if (use_v2w(dtype) && gemm_wgrad_v2_tile(*args, dtype, bi, bj)) return 2;
+  *bi = args->ni <= 64 ? 64 : 128;
+  *bj = 128;
+  return 1;
+}
+
 extern "C" int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream) {
   int epc = dtype == VU_BF16 ? 8 : 4;
   const VuGather* gs[2] = {&args->p, &args->q};
@@ -294,6 +315,8 @@ extern "C" int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream) {
   if (args->p.N != args->q.N || args->p.H != args->q.H || args->p.W != args->q.W)
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  int bi, bj;
+  if (use_v2w(dtype) && gemm_wgrad_v2_tile(*args, dtype, &bi, &bj)) return gemm_wgrad_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_wg<bf16_t>(*args, st) : dispatch_wg<float>(*args, st);
 }
 

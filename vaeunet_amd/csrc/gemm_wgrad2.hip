@@ -1,0 +1,236 @@
+// Weight-gradient GEMM, large-tile bf16 variant ("v2") — same contract as
+// gemm_wgrad.hip: slab[s][i][j] = sum_{m in split s} P[m][i] * Q[m][j].
+//
+//   * 8 waves (512 threads); output tile 128 x 256 (waves 2x4, 64x64 each)
+//     or 64 x 256 for the 64-channel layers (waves 1x8, 64x32 each);
+//   * 64 pixels per step, both operand images [m][col] filled by LDS-DMA
+//     (global_load_lds_dwordx4); each lane's (pixel, column chunk) is fixed
+//     for the whole launch, so its tap / channel / source decode is done once
+//     and only the pixel coordinates advance (by 64) per step;
+//   * the 32-byte-block XOR swizzle that makes the transposed
+//     ds_read_b64_tr_b16 fragment reads conflict-free is applied to the
+//     SOURCE column of each lane (the LDS image stays lane-linear);
+//   * deterministic split-K over pixels into fp32 slabs (vu_slab_reduce).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page[16];  // per code object
+
+namespace {
+
+constexpr int BMR = 64;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// 32-byte block swizzle (rows >= 256 B): f(m) spreads the 8 rows a 32-lane
+// half reads (4 consecutive + 4 rows 8 apart) over 8 distinct bank blocks.
+// 128-B rows (4 blocks): the two 32-lane groups' rows are paired by parity.
+template <int RB> VU_DEV int fsw(int m) {
+  return RB >= 256 ? ((m & 3) | ((m >> 1) & 4)) : (((m >> 1) & 1) | ((m >> 2) & 2));
+}
+
+template <int RB> VU_DEV int tr_off(int m, int col) {
+  return m * RB + (((col >> 4) ^ fsw<RB>(m)) << 5) + ((col & 15) << 1);
+}
+
+struct Col {
+  int r, s, t;
+  int64_t coff;
+  bool ok;
+};
+
+VU_DEV Col decode_col(const VuGather& g, int col, int ncols) {
+  Col d;
+  d.ok = col < ncols;
+  int cc = d.ok ? col : 0;
+  int tap = cc / g.C, ch = cc - tap * g.C;
+  d.r = tap / g.S;
+  d.s = tap - d.r * g.S;
+  d.t = (ch >= g.cend[0]) + (g.nsrc > 2 && ch >= g.cend[1]);
+  d.coff = ch - (d.t == 0 ? 0 : g.cend[d.t - 1]);
+  return d;
+}
+
+template <int BI, int BJ, int WI, int WJ>
+__global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWgrad p) {
+  constexpr int NT = WI * WJ * 64;
+  constexpr int RBP = BI * 2, RBQ = BJ * 2;          // LDS row bytes
+  constexpr int CPI = BI / 8, CPJ = BJ / 8;          // 16-byte chunks per row
+  constexpr int LI = BMR * CPI / NT, LJ = BMR * CPJ / NT;
+  constexpr int TI = BI / WI / 16, TJ = BJ / WJ / 16;
+  constexpr int STAGE = BMR * (RBP + RBQ);
+  static_assert(LI >= 1 && LJ >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const VuGather& gp = p.p;
+  const VuGather& gq = p.q;
+  const int64_t M = (int64_t)gp.N * gp.H * gp.W;
+  const int itiles = (p.ni + BI - 1) / BI, jtiles = (p.nj + BJ - 1) / BJ;
+  const int ntile = itiles * jtiles;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile;
+  const int tile = bid - split * ntile;
+  const int it = tile / jtiles, jt = tile - it * jtiles;
+  const int i0 = it * BI, j0 = jt * BJ;
+  const int64_t mbeg = (int64_t)split * p.m_per_split;
+  const int64_t mend = (mbeg + p.m_per_split < M) ? mbeg + p.m_per_split : M;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wi = wid / WJ, wj = wid - (wid / WJ) * WJ;
+  const void* zp = (const void*)vu_zero_page;
+
+  // per-thread fixed (row-in-step, column) assignment of every DMA slot
+  int prow[LI], qrow[LJ];
+  Col pcd[LI], qcd[LJ];
+#pragma unroll
+  for (int k = 0; k < LI; ++k) {
+    int q = k * NT + tid;
+    prow[k] = q / CPI;
+    int pc = q - prow[k] * CPI;
+    int lcol = ((((pc >> 1) ^ fsw<RBP>(prow[k])) << 1) | (pc & 1)) * 8;
+    pcd[k] = decode_col(gp, i0 + lcol, p.ni);
+  }
+#pragma unroll
+  for (int k = 0; k < LJ; ++k) {
+    int q = k * NT + tid;
+    qrow[k] = q / CPJ;
+    int pc = q - qrow[k] * CPJ;
+    int lcol = ((((pc >> 1) ^ fsw<RBQ>(qrow[k])) << 1) | (pc & 1)) * 8;
+    qcd[k] = decode_col(gq, j0 + lcol, p.nj);
+  }
+  int pn[LI], ph[LI], pw[LI], qn[LJ], qh[LJ], qw[LJ];
+  auto decode = [&](int64_t m, int& n, int& h, int& w) {
+    int hw = gp.H * gp.W;
+    int64_t mm = m < M ? m : 0;
+    n = (int)(mm / hw);
+    int rem = (int)(mm - (int64_t)n * hw);
+    h = rem / gp.W;
+    w = rem - h * gp.W;
+  };
+  auto advance = [&](int& n, int& h, int& w) {
+    w += BMR;
+    while (w >= gp.W) { w -= gp.W; if (++h == gp.H) { h = 0; ++n; } }
+  };
+#pragma unroll
+  for (int k = 0; k < LI; ++k) decode(mbeg + prow[k], pn[k], ph[k], pw[k]);
+#pragma unroll
+  for (int k = 0; k < LJ; ++k) decode(mbeg + qrow[k], qn[k], qh[k], qw[k]);
+
+  auto src_of = [&](const VuGather& g, const Col& d, int n, int h, int w, bool mok) -> const void* {
+    if (!mok || !d.ok) return zp;
+    int hs = h * g.sy + d.r * g.dy + g.oy;
+    int ws = w * g.sx + d.s * g.dx + g.ox;
+    if ((unsigned)hs >= (unsigned)g.Hs || (unsigned)ws >= (unsigned)g.Ws) return zp;
+    const bf16_t* base = reinterpret_cast<const bf16_t*>(g.src[d.t]);
+    return base + (((int64_t)n * g.Hs + hs) * g.Ws + ws) * g.stride[d.t] + d.coff;
+  };
+
+  auto stage = [&](int64_t mb, int buf) {
+    char* Pb = smem + buf * STAGE;
+    char* Qb = Pb + BMR * RBP;
+#pragma unroll
+    for (int k = 0; k < LI; ++k) {
+      const void* s = src_of(gp, pcd[k], pn[k], ph[k], pw[k], mb + prow[k] < mend);
+      __builtin_amdgcn_global_load_lds(s, (lds_void*)(Pb + (k * NT + wid * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < LJ; ++k) {
+      const void* s = src_of(gq, qcd[k], qn[k], qh[k], qw[k], mb + qrow[k] < mend);
+      __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < LI; ++k) advance(pn[k], ph[k], pw[k]);
+#pragma unroll
+    for (int k = 0; k < LJ; ++k) advance(qn[k], qh[k], qw[k]);
+  };
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+
+  const int nsteps = mend > mbeg ? (int)((mend - mbeg + BMR - 1) / BMR) : 0;
+  if (nsteps > 0) stage(mbeg, 0);
+  __syncthreads();
+  const int g4 = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nsteps) stage(mbeg + (int64_t)(st + 1) * BMR, cur ^ 1);
+    const char* Pb = smem + cur * STAGE;
+    const char* Qb = Pb + BMR * RBP;
+#pragma unroll
+    for (int ks = 0; ks < BMR / 32; ++ks) {
+      u32x4 af[TI], bf[TJ];
+      const int m = ks * 32 + 8 * g4 + qd;
+#pragma unroll
+      for (int a = 0; a < TI; ++a) {
+        int col = wi * (BI / WI) + a * 16 + 4 * pp;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Pb + tr_off<RBP>(m, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Pb + tr_off<RBP>(m + 4, col)));
+        u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        af[a] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+      }
+#pragma unroll
+      for (int b = 0; b < TJ; ++b) {
+        int col = wj * (BJ / WJ) + b * 16 + 4 * pp;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qb + tr_off<RBQ>(m, col)));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qb + tr_off<RBQ>(m + 4, col)));
+        u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        bf[b] = u32x4{l2[0], l2[1], h2[0], h2[1]};
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int a = 0; a < TI; ++a)
+#pragma unroll
+        for (int b = 0; b < TJ; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+  }
+
+  float* out = p.out + (int64_t)split * p.ni * p.nj;
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int b = 0; b < TJ; ++b) {
+      int j = j0 + wj * (BJ / WJ) + b * 16 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int i = i0 + wi * (BI / WI) + a * 16 + 4 * g4 + r;
+        if (i < p.ni && j < p.nj) out[(int64_t)i * p.nj + j] = acc[a][b][r];
+      }
+    }
+}
+
+template <int BI, int BJ, int WI, int WJ>
+int launch(const VuGemmWgrad& p, hipStream_t st) {
+  int itiles = (p.ni + BI - 1) / BI, jtiles = (p.nj + BJ - 1) / BJ;
+  int64_t nblk = (int64_t)itiles * jtiles * p.splits;
+  if (nblk <= 0) return 0;
+  hipLaunchKernelGGL((gemm_wgrad_v2_kernel<BI, BJ, WI, WJ>), dim3((unsigned)nblk), dim3(WI * WJ * 64), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Output tile (BI, BJ) of the v2 kernel for this problem, or 0 if it does not apply.
+int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
+  if (dtype != VU_BF16) return 0;
+  const VuGather* gs[2] = {&p.p, &p.q};
+  for (auto g : gs)
+    for (int t = 0; t < g->nsrc; ++t)
+      if (g->cend[t] % 8 || g->stride[t] % 8) return 0;
+  int64_t M = (int64_t)p.p.N * p.p.H * p.p.W;
+  if (M < 4096) return 0;
+  *bi = p.ni <= 64 ? 64 : 128;
+  *bj = 256;
+  return 1;
+}
+
+int gemm_wgrad_v2_launch(const VuGemmWgrad& p, hipStream_t st) {
+  if (p.ni <= 64) return launch<64, 256, 1, 8>(p, st);
+  return launch<128, 256, 2, 4>(p, st);
+}

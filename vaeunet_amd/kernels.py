@@ -182,15 +182,30 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
 def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
     """grad[i*s_i + (j//Cq)*s_tap + (j%Cq)*s_c] (+)= sum_m P[m][i] Q[m][j]."""
     M = gp.N * gp.H * gp.W
-    bi = 64 if ni <= 64 else 128
-    tiles = ((ni + bi - 1) // bi) * ((nj + 127) // 128)
+    w = VuGemmWgrad()
+    w.p, w.q, w.ni, w.nj = gp, gq, ni, nj
+    bi, bj = C.c_int(0), C.c_int(0)
+    kind = query("vu_gemm_wgrad_tile", C.byref(w), dtype, C.byref(bi), C.byref(bj))
+    tiles = ((ni + bi.value - 1) // bi.value) * ((nj + bj.value - 1) // bj.value)
+    # split-K over pixels: pick the split count whose block count fills whole
+    # waves of resident blocks best (v2: 1 block/CU, v1: 2 blocks/CU)
+    slots = 256 if kind == 2 else 512
     steps = (M + 63) // 64
-    splits = max(1, min(-(-1024 // tiles), steps // 4 if steps >= 8 else 1, 256))
+    smax = max(1, min(256, steps // 4))
+    best = (-1.0, 1)
+    for s in range(1, smax + 1):
+        blocks = tiles * s
+        waves = -(-blocks // slots)
+        if waves > 8:
+            break
+        eff = blocks / (waves * slots)
+        if eff > best[0] + 1e-9:
+            best = (eff, s)
+    splits = best[1]
     mps = ((-(-M // splits)) + 63) // 64 * 64
     splits = -(-M // mps)
     slab = torch.empty((splits, ni, nj), dtype=torch.float32, device=grad.device)
-    w = VuGemmWgrad()
-    w.p, w.q, w.ni, w.nj, w.splits, w.m_per_split = gp, gq, ni, nj, splits, mps
+    w.splits, w.m_per_split = splits, mps
     w.out = slab.data_ptr()
     _timed(_gemm_tag(gq, "wgrad"), 2 * M * ni * nj,
            lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()))
