@@ -206,22 +206,16 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
   }
 }
 
-// column sums of [nblk][width] partials: 64 columns x 4 row lanes, fp64
+// column sums of [nblk][width] partials (colsum32: fp64, fixed order)
 __global__ void part_final(const float* part, int nblk, int width, float* out, int n_out, float* out2,
                            int accumulate) {
-  __shared__ double sh[4][64];
-  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double s = 0;
-  if (c < width)
-    for (int b = q; b < nblk; b += 4) s += part[(int64_t)b * width + c];
-  sh[q][cl] = s;
-  __syncthreads();
-  if (q != 0 || c >= width) return;
-  s = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  double s[1];
+  colsum32<1>(part, nblk, width, 0, c, c < width, s);
+  if (threadIdx.x >= 32 || c >= width) return;
   float* o = c < n_out ? (out ? out + c : nullptr) : (out2 ? out2 + (c - n_out) : nullptr);
   if (o == nullptr) return;
-  *o = accumulate ? *o + (float)s : (float)s;
+  *o = accumulate ? *o + (float)s[0] : (float)s[0];
 }
 
 // ---- tiny-output pointwise conv ----
@@ -383,7 +377,7 @@ extern "C" int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F,
     hipLaunchKernelGGL((psi_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
                        sx, tx, wpsi, dq, (T*)ds, workspace);
   })
-  hipLaunchKernelGGL(part_final, dim3((F + 1 + 63) / 64), dim3(256), 0, st, workspace, nblk, F + 1, dwpsi, F, dbpsi,
+  hipLaunchKernelGGL(part_final, dim3((F + 1 + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, F + 1, dwpsi, F, dbpsi,
                      accumulate);
   return (int)hipGetLastError();
 }
@@ -418,7 +412,7 @@ extern "C" int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int6
     hipLaunchKernelGGL((pw_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w, (T*)dx,
                        dxs, workspace);
   })
-  hipLaunchKernelGGL(part_final, dim3((J * C + J + 63) / 64), dim3(256), 0, st, workspace, nblk, J * C + J, dw, J * C,
+  hipLaunchKernelGGL(part_final, dim3((J * C + J + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, J * C + J, dw, J * C,
                      db, accumulate);
   return (int)hipGetLastError();
 }

@@ -7,8 +7,8 @@
 // (unet_parts.py:42,45) whose backward masks by output > 0.
 //
 // Statistics come from the producing GEMM's epilogue as per-row-tile (sum,
-// centered M2) pairs; vu_bn_finalize combines them with Chan's parallel
-// formula in fp64 in a fixed order, so results are bitwise reproducible.
+// centered M2) pairs; vu_bn_finalize combines them about the group mean in
+// fp64 in a fixed order, so results are bitwise reproducible.
 // Backward needs two per-channel sums (sum dz, sum dz*xhat): a two-stage
 // deterministic reduction (fp32 per block, fp64 across blocks).
 //
@@ -21,38 +21,54 @@
 
 namespace {
 
-VU_DEV void chan_combine(double& n, double& m, double& M2, double nb, double mb, double M2b) {
-  double nn = n + nb;
-  if (nb <= 0.0) return;
-  double d = mb - m;
-  m += d * nb / nn;
-  M2 += M2b + d * d * n * nb / nn;
-  n = nn;
-}
-
+// Combining per-tile (sum, centered M2) pairs without a division per tile:
+// for a group of tiles with mean m, M2 = sum_t [M2_t + n_t (m_t - m)^2]
+// (exact, and as stable as Chan's pairwise update since every deviation is
+// taken from the group mean).  Stage 1 does this for blocks of tiles (two
+// passes over the block's tiles, the second from L2), stage 2 for the blocks.
 // stage 1: grid (ceil(C/64), S), 256 threads = 64 channels x 4 tile lanes
 __global__ void bn_stats_stage1(const float* psum, const float* pm2, int tiles, int64_t tile_rows,
                                 int64_t rows, int C, int S, double* ws) {
-  __shared__ double sh[3][4][64];
+  __shared__ double sh[4][64];
   int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
   int c = blockIdx.x * 64 + cl;
+  bool ok = c < C;
   int per = (tiles + S - 1) / S;
   int tb = blockIdx.y * per, te = min(tiles, tb + per);
-  double n = 0, m = 0, M2 = 0;
-  if (c < C) {
+  int64_t n_blk = te > tb ? min(rows, (int64_t)te * tile_rows) - (int64_t)tb * tile_rows : 0;
+  const double inv_full = 1.0 / (double)tile_rows;
+  auto tile_n = [&](int t) -> int64_t {
+    int64_t nb = rows - (int64_t)t * tile_rows;
+    return nb > tile_rows ? tile_rows : nb;
+  };
+  // pass 1: block sum
+  double s0 = 0, s1 = 0;
+  if (ok) {
+    int t = tb + tl;
+    for (; t + 4 < te; t += 8) { s0 += psum[(int64_t)t * C + c]; s1 += psum[(int64_t)(t + 4) * C + c]; }
+    for (; t < te; t += 4) s0 += psum[(int64_t)t * C + c];
+  }
+  sh[tl][cl] = s0 + s1;
+  __syncthreads();
+  double m = n_blk > 0 ? (sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]) / (double)n_blk : 0.0;
+  __syncthreads();
+  // pass 2: M2 about the block mean
+  double q0 = 0, q1 = 0;
+  if (ok) {
     for (int t = tb + tl; t < te; t += 4) {
-      int64_t nb = rows - (int64_t)t * tile_rows;
-      if (nb > tile_rows) nb = tile_rows;
-      double s = psum[(int64_t)t * C + c];
-      chan_combine(n, m, M2, (double)nb, s / (double)nb, (double)pm2[(int64_t)t * C + c]);
+      int64_t nt = tile_n(t);
+      double st = psum[(int64_t)t * C + c];
+      double mt = nt == tile_rows ? st * inv_full : st / (double)nt;
+      double d = mt - m;
+      double v = (double)pm2[(int64_t)t * C + c] + (double)nt * d * d;
+      if ((t - tb) & 4) q1 += v; else q0 += v;
     }
   }
-  sh[0][tl][cl] = n; sh[1][tl][cl] = m; sh[2][tl][cl] = M2;
+  sh[tl][cl] = q0 + q1;
   __syncthreads();
-  if (tl == 0 && c < C) {
-    for (int q = 1; q < 4; ++q) chan_combine(n, m, M2, sh[0][q][cl], sh[1][q][cl], sh[2][q][cl]);
+  if (tl == 0 && ok) {
     double* o = ws + ((int64_t)blockIdx.y * C + c) * 3;
-    o[0] = n; o[1] = m; o[2] = M2;
+    o[0] = (double)n_blk; o[1] = m; o[2] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
   }
 }
 
@@ -61,10 +77,18 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
                                 float* shift, float* smean, float* sinvstd, int64_t* nbt) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double n = 0, m = 0, M2 = 0;
+  double n = 0, sm = 0;
   for (int s = 0; s < S; ++s) {
     const double* o = ws + ((int64_t)s * C + c) * 3;
-    chan_combine(n, m, M2, o[0], o[1], o[2]);
+    n += o[0];
+    sm += o[0] * o[1];
+  }
+  double m = n > 0 ? sm / n : 0.0;
+  double M2 = 0;
+  for (int s = 0; s < S; ++s) {
+    const double* o = ws + ((int64_t)s * C + c) * 3;
+    double d = o[1] - m;
+    M2 += o[2] + o[0] * d * d;
   }
   double var = n > 0 ? M2 / n : 0.0;
   float invstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -223,39 +247,21 @@ __global__ void chan_partial_scalar(RedArgs r) {
   }
 }
 
-// stage 2: 256 threads = 64 channels x 4 block-lanes, fp64, fixed order
-template <int NQ>
-VU_DEV void colsum2(const float* part, int nblk, int C, int c, double* out) {
-  __shared__ double sh[NQ][4][64];
-  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  double s[NQ];
-#pragma unroll
-  for (int k = 0; k < NQ; ++k) s[k] = 0.0;
-  if (c < C)
-    for (int b = q; b < nblk; b += 4)
-#pragma unroll
-      for (int k = 0; k < NQ; ++k) s[k] += part[((int64_t)b * 2 + k) * C + c];
-#pragma unroll
-  for (int k = 0; k < NQ; ++k) sh[k][q][cl] = s[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < NQ; ++k) out[k] = sh[k][0][cl] + sh[k][1][cl] + sh[k][2][cl] + sh[k][3][cl];
-}
-
+// stage 2: fp64 column sums of the [nblk][2][C] partials (colsum32, fixed order)
 __global__ void chan_final_sum(const float* part, int nblk, int C, float* out, int accumulate) {
-  int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  int c = blockIdx.x * 32 + (threadIdx.x & 31);
   double s[1];
-  colsum2<1>(part, nblk, C, c, s);
-  if (threadIdx.x < 64 && c < C) out[c] = accumulate ? out[c] + (float)s[0] : (float)s[0];
+  colsum32<1>(part, nblk, 2 * (int64_t)C, C, c, c < C, s);
+  if (threadIdx.x < 32 && c < C) out[c] = accumulate ? out[c] + (float)s[0] : (float)s[0];
 }
 
 __global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, int accumulate,
                              float* coef) {
-  int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  int c = blockIdx.x * 32 + (threadIdx.x & 31);
   double s[2];
-  colsum2<2>(part, nblk, C, c, s);
-  if (threadIdx.x >= 64 || c >= C) return;
+  colsum32<2>(part, nblk, 2 * (int64_t)C, C, c, c < C, s);
+  if (threadIdx.x >= 32 || c >= C) return;
   float g = gamma ? gamma[c] : 1.f;
   float is = invstd[c];
   float k1 = g * is;
@@ -435,7 +441,7 @@ extern "C" int vu_bn_bwd_reduce(const void* dy, int64_t dys, const void* x, int6
   int nblk = 0, rc;
   rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk) : launch_partial<float, 1>(r, st, nblk);
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 63) / 64), dim3(256), 0, st, workspace, nblk, C, P,
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, C, P,
                      gamma, invstd, dgamma, dbeta, accumulate, coef);
   return (int)hipGetLastError();
 }
@@ -478,7 +484,7 @@ extern "C" int vu_chan_sum(const void* x, int64_t stride, int N, int H, int W, i
   int nblk = 0, rc;
   rc = dtype == VU_BF16 ? launch_partial<bf16_t, 0>(r, st, nblk) : launch_partial<float, 0>(r, st, nblk);
   if (rc) return rc;
-  hipLaunchKernelGGL(chan_final_sum, dim3((C + 63) / 64), dim3(256), 0, st, workspace, nblk, C, out,
+  hipLaunchKernelGGL(chan_final_sum, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, C, out,
                      accumulate);
   return (int)hipGetLastError();
 }

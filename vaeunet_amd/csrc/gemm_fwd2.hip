@@ -38,7 +38,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int ES = BN + 4;
   constexpr int STAGE = (BM + BN) * KB;
-  constexpr int MAIN = 2 * STAGE;
+  constexpr int NSTAGE = 3;               // LDS ring: DMA runs two K steps ahead
+  constexpr int MAIN = NSTAGE * STAGE;
   constexpr int EPI = BM * ES * 4;
   constexpr int RED = (NT / BN) * BN * 4;
   constexpr int LDS_BYTES = (MAIN > EPI ? MAIN : EPI) + RED;
@@ -118,11 +119,21 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 
   const int nk = K / BKE;
+  // Pipeline: stage kt+2 is issued right after the barrier of step kt, into
+  // the ring slot step kt-1 just finished reading.  Each thread's own DMA is
+  // retired by a COUNTED vmcnt (the NL loads of the newest stage may stay in
+  // flight), then the raw s_barrier makes every thread's landed bytes
+  // visible; no __syncthreads() (it would drain vmcnt to 0) in the loop.
+  constexpr int NL = LA + LB;
   stage(0, 0);
-  __syncthreads();
+  if (nk > 1) stage(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) stage(kt + 2, (kt + 2) % NSTAGE);
+    const int cur = kt % NSTAGE;
     const char* A = smem + cur * STAGE;
     const char* B = A + BM * KB;
 #pragma unroll
@@ -144,8 +155,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
                                                               __builtin_bit_cast(bf16x8, bf[j]), acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    __syncthreads();
   }
+  __syncthreads();  // every wave is done with the ring before the epilogue reuses it
 
   // ---- epilogue (as gemm_fwd.hip) ----
   float* E = reinterpret_cast<float*>(smem);

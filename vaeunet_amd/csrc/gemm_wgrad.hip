@@ -268,14 +268,29 @@ int dispatch_wg(const VuGemmWgrad& p, hipStream_t st) {
 }
 
 // slab reduce + permute into the parameter-gradient layout
+// Sum of the split-K slabs in a fixed order.  A 256-thread block covers 64
+// consecutive outputs x 4 split lanes; each lane keeps 4 independent
+// accumulators so its slab loads overlap (with many splits the serial chain,
+// not bandwidth, was the limit), then the 4 lanes fold in LDS.
 __global__ void slab_reduce_kernel(const float* slab, int splits, int ni, int nj, int C, int cvalid,
                                    int64_t s_i, int64_t s_tap, int64_t s_c, float* out, int accumulate) {
-  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t tot = (int64_t)ni * nj;
-  if (idx >= tot) return;
+  __shared__ float sh[4][64];
+  const int l = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t tot = (int64_t)ni * nj;
+  const int64_t idx = (int64_t)blockIdx.x * 64 + l;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (idx < tot) {
+    int k = q;
+    for (; k + 12 < splits; k += 16)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += slab[(int64_t)(k + 4 * u) * tot + idx];
+    for (; k < splits; k += 4) a[0] += slab[(int64_t)k * tot + idx];
+  }
+  sh[q][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (q != 0 || idx >= tot) return;
+  float s = (sh[0][l] + sh[1][l]) + (sh[2][l] + sh[3][l]);
   int i = (int)(idx / nj), j = (int)(idx - (int64_t)i * nj);
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += slab[(int64_t)k * tot + idx];
   int tap = j / C, c = j - tap * C;
   if (c >= cvalid) return;
   float* o = out + i * s_i + tap * s_tap + c * s_c;
@@ -324,7 +339,7 @@ extern "C" int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int
                               int64_t s_tap, int64_t s_c, float* out, int accumulate, void* stream) {
   int64_t tot = (int64_t)ni * nj;
   if (tot == 0) return 0;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0,
                      (hipStream_t)stream, slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate);
   return (int)hipGetLastError();
 }

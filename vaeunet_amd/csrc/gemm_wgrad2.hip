@@ -60,7 +60,8 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
   constexpr int TI = BI / WI / 16, TJ = BJ / WJ / 16;
   constexpr int STAGE = BMR * (RBP + RBQ);
   static_assert(LI >= 1 && LJ >= 1, "tile too small");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int NSTAGE = 3;  // LDS ring, DMA two steps ahead
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
   const VuGather& gp = p.p;
   const VuGather& gq = p.q;
@@ -151,12 +152,19 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
   const int nsteps = mend > mbeg ? (int)((mend - mbeg + BMR - 1) / BMR) : 0;
+  // counted-vmcnt ring (see gemm_fwd2.hip): stage st+2 issued after the
+  // barrier of step st into the slot step st-1 finished reading
+  constexpr int NL = LI + LJ;
   if (nsteps > 0) stage(mbeg, 0);
-  __syncthreads();
+  if (nsteps > 1) stage(mbeg + BMR, 1);
   const int g4 = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
   for (int st = 0; st < nsteps; ++st) {
-    const int cur = st & 1;
-    if (st + 1 < nsteps) stage(mbeg + (int64_t)(st + 1) * BMR, cur ^ 1);
+    if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + 2 < nsteps) stage(mbeg + (int64_t)(st + 2) * BMR, (st + 2) % NSTAGE);
+    const int cur = st % NSTAGE;
     const char* Pb = smem + cur * STAGE;
     const char* Qb = Pb + BMR * RBP;
 #pragma unroll
@@ -188,7 +196,6 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
               __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    __syncthreads();
   }
 
   float* out = p.out + (int64_t)split * p.ni * p.nj;

@@ -59,10 +59,12 @@ __global__ void bce_dice_stage1(const float* x, const float* t, int64_t n, doubl
 
 __global__ void bce_dice_stage2(const double* ws, int nblk, int64_t n, double* sums, float smooth, float w_bce,
                                 float w_dice, float* loss, float* parts) {
-  if (threadIdx.x != 0) return;
+  __shared__ double sh[4];
   double s[4] = {0, 0, 0, 0};
-  for (int b = 0; b < nblk; ++b)
+  for (int b = threadIdx.x; b < nblk; b += LBLK)
     for (int k = 0; k < 4; ++k) s[k] += ws[b * 4 + k];
+  for (int k = 0; k < 4; ++k) s[k] = block_sum_d(s[k], sh);
+  if (threadIdx.x != 0) return;
   for (int k = 0; k < 4; ++k) sums[k] = s[k];
   if (loss) {
     float bce = (float)(s[0] / (double)n);
@@ -145,9 +147,11 @@ __global__ void sumsq_stage1(const float* x, int64_t n, double* ws) {
 }
 
 __global__ void sum_stage2(const double* ws, int nblk, double* out, int accumulate) {
-  if (threadIdx.x != 0) return;
+  __shared__ double sh[4];
   double s = 0;
-  for (int b = 0; b < nblk; ++b) s += ws[b];
+  for (int b = threadIdx.x; b < nblk; b += LBLK) s += ws[b];
+  s = block_sum_d(s, sh);
+  if (threadIdx.x != 0) return;
   out[0] = accumulate ? out[0] + s : s;
 }
 
@@ -168,7 +172,7 @@ extern "C" int vu_bce_dice_fwd2(const float* logits, const float* target, int64_
   hipStream_t st = (hipStream_t)stream;
   int nb = nblocks(n);
   hipLaunchKernelGGL(bce_dice_stage1, dim3(nb), dim3(LBLK), 0, st, logits, target, n, workspace);
-  hipLaunchKernelGGL(bce_dice_stage2, dim3(1), dim3(64), 0, st, workspace, nb, n, sums, smooth, w_bce, w_dice, loss,
+  hipLaunchKernelGGL(bce_dice_stage2, dim3(1), dim3(LBLK), 0, st, workspace, nb, n, sums, smooth, w_bce, w_dice, loss,
                      parts);
   return (int)hipGetLastError();
 }
@@ -203,6 +207,6 @@ extern "C" int vu_sumsq(const float* x, int64_t n, double* out, double* workspac
   hipStream_t st = (hipStream_t)stream;
   int nb = nblocks(n);
   hipLaunchKernelGGL(sumsq_stage1, dim3(nb), dim3(LBLK), 0, st, x, n, workspace);
-  hipLaunchKernelGGL(sum_stage2, dim3(1), dim3(64), 0, st, workspace, nb, out, 0);
+  hipLaunchKernelGGL(sum_stage2, dim3(1), dim3(LBLK), 0, st, workspace, nb, out, 0);
   return (int)hipGetLastError();
 }
