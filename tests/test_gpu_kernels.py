@@ -55,6 +55,7 @@ CONV_CASES = [
     (4, [64, 64], 128, 128, 128),  # BM=128, BN=128 path, two sources
     (2, [24, 8, 16], 6, 6, 40),    # three sources, ragged
     (2, [64, 128], 16, 48, 96),    # bf16 halo kernel: 16x16 tiles, 3 chunks, column tail
+    (2, [128], 8, 64, 192),        # bf16 halo wgrad: 128-row co tiles with a 64-row tail
 ]
 
 

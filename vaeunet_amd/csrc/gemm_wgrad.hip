@@ -301,6 +301,8 @@ __global__ void slab_reduce_kernel(const float* slab, int splits, int ni, int nj
 
 int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj);
 int gemm_wgrad_v2_launch(const VuGemmWgrad& p, hipStream_t st);
+int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj);
+int gemm_wgrad_v3_launch(const VuGemmWgrad& p, hipStream_t st);
 
 static bool use_v2w(int dtype) {
   static int mode = -1;
@@ -311,8 +313,20 @@ static bool use_v2w(int dtype) {
   return mode == 1 && dtype == VU_BF16;
 }
 
-// output tile the dispatcher will use (host split-K heuristic)
+static bool use_v3w(int dtype) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VU_GEMM_V3");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode == 1 && use_v2w(dtype);
+}
+
+// Output tile the dispatcher will use (host split-K heuristic).  Returns the
+// kernel generation: 3 = halo kernel (splits must be whole 128-pixel tiles),
+// 2 = large-tile LDS-DMA kernel, 1 = register-staged kernel.
 extern "C" int vu_gemm_wgrad_tile(const VuGemmWgrad* args, int dtype, int* bi, int* bj) {
+  if (use_v3w(dtype) && gemm_wgrad_v3_tile(*args, dtype, bi, bj)) return 3;
   if (use_v2w(dtype) && gemm_wgrad_v2_tile(*args, dtype, bi, bj)) return 2;
   *bi = args->ni <= 64 ? 64 : 128;
   *bj = 128;
@@ -331,6 +345,8 @@ extern "C" int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream) {
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   int bi, bj;
+  if (use_v3w(dtype) && args->m_per_split % 128 == 0 && gemm_wgrad_v3_tile(*args, dtype, &bi, &bj))
+    return gemm_wgrad_v3_launch(*args, st);
   if (use_v2w(dtype) && gemm_wgrad_v2_tile(*args, dtype, &bi, &bj)) return gemm_wgrad_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_wg<bf16_t>(*args, st) : dispatch_wg<float>(*args, st);
 }

@@ -1,0 +1,253 @@
+// 3x3 / stride-1 / pad-1 convolution WEIGHT gradient over halo tiles ("v3",
+// bf16): slab[s][co][tap*C + ci] = sum_{pixels p of split s} dy[p][co] *
+// x[p + tap][ci].  Serves every DoubleConv / DecoderBlock 3x3 conv weight
+// gradient of the hot path (unet_parts.py:40,43) whose image width is a
+// multiple of 32.
+//
+// Why: the v2 kernel treats the nine taps as nine independent K columns and
+// gathers the shifted input separately for each, so every x pixel crosses
+// L2 -> LDS nine times (and dy once per column tile).  Here a block owns
+// (BI output channels) x (all 9 taps) x (one 64-channel input chunk) and
+// walks 4x32-pixel tiles of its pixel split; per tile it DMA-loads dy once
+// and the 6x34 x halo once, and all nine taps read the halo in place.
+//
+//   * 8 waves, 16x16x32 bf16 MFMA, both operands read with the transposed
+//     ds_read_b64_tr_b16 (pixels are the reduction dim);
+//   * halo rows are laid out with a 48-pixel pitch (34 used) so that a tap
+//     shift of r rows moves the address by a multiple of 16 rows: the 32-byte
+//     block swizzle (a function of the row's low 4 bits) is then unchanged and
+//     every tap / k-step offset is a compile-time immediate of the LDS read;
+//   * operands land by LDS-DMA with the swizzle applied to the SOURCE column,
+//     double-buffered per pixel tile; fp32 accumulators stay in registers
+//     across the split, then one slab write (vu_slab_reduce sums the splits in
+//     a fixed order: deterministic).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page_w3[16];
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int TW = 32, TH = 4, TP = TW * TH;   // pixel tile
+constexpr int HWP = 48;                        // halo row pitch (TW + 2 used)
+constexpr int HROWS = TH + 2;
+
+template <int RB> VU_DEV int fsw(int m) {
+  return RB >= 256 ? ((m & 3) | ((m >> 1) & 4)) : (((m >> 1) & 1) | ((m >> 2) & 2));
+}
+template <int RB> VU_DEV int tr_off(int m, int col) {
+  return m * RB + (((col >> 4) ^ fsw<RB>(m)) << 5) + ((col & 15) << 1);
+}
+// logical column of the 16-byte physical chunk pc of row m (source-side swizzle)
+template <int RB> VU_DEV int swz_col(int m, int pc) {
+  return ((((pc >> 1) ^ fsw<RB>(m)) << 1) | (pc & 1)) * 8;
+}
+
+VU_DEV u32x4 tr_frag(const char* base, int off_lo, int off_hi) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off_lo));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off_hi));
+  u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+  return u32x4{l2[0], l2[1], h2[0], h2[1]};
+}
+
+template <int BI>
+__global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
+  constexpr int NT = 512;
+  constexpr int RBP = BI * 2, CPI = BI / 8;
+  constexpr int LP = TP * CPI / NT;                       // dy DMA instrs per thread per tile
+  constexpr int NH = (HROWS * HWP * 8 + NT - 1) / NT;     // halo DMA instrs per thread per tile
+  constexpr int PB = TP * RBP, QB = NH * NT * 16;
+  constexpr int STAGE = PB + QB;
+  constexpr int TI = 2;                                   // co tiles per wave
+  constexpr int TJ = BI == 64 ? 1 : 2;                    // ci tiles per wave
+  constexpr int WCI = 4 / TJ;                             // waves along ci
+  static_assert(LP >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const VuGather& gp = p.p;   // dy, 1x1
+  const VuGather& gq = p.q;   // x, 3x3 halo
+  const int H = gq.H, W = gq.W;
+  const int tiles_w = W / TW, tiles_img = (H / TH) * tiles_w;
+  const int T = gq.N * tiles_img;
+  const int itiles = (p.ni + BI - 1) / BI, jch = gq.C / 64;
+  const int ntile = itiles * jch;
+  const int bid = xcd_remap(blockIdx.x, ntile * p.splits);
+  const int split = bid / ntile, tile = bid - split * ntile;
+  const int it = tile / jch, jc = tile - it * jch;
+  const int i0 = it * BI;
+  const int tps = (int)(p.m_per_split / TP);
+  const int t_beg = split * tps;
+  const int t_end = t_beg + tps < T ? t_beg + tps : T;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const void* zp = (const void*)vu_zero_page_w3;
+
+  // source of this block's 64-channel x chunk
+  const int cb = jc * 64;
+  const int qs = (cb >= gq.cend[0]) + (gq.nsrc > 2 && cb >= gq.cend[1]);
+  const bf16_t* xsrc = reinterpret_cast<const bf16_t*>(gq.src[qs]) + (cb - (qs == 0 ? 0 : gq.cend[qs - 1]));
+  const int64_t xst = gq.stride[qs];
+  const bf16_t* dsrc = reinterpret_cast<const bf16_t*>(gp.src[0]);
+  const int64_t dst_ = gp.stride[0];
+
+  // fixed per-thread DMA slot geometry
+  int p_ty[LP], p_tx[LP], p_col[LP];
+#pragma unroll
+  for (int k = 0; k < LP; ++k) {
+    int e = k * NT + tid, row = e / CPI, pc = e - row * CPI;
+    p_ty[k] = row / TW;
+    p_tx[k] = row - p_ty[k] * TW;
+    p_col[k] = i0 + swz_col<RBP>(row, pc);
+  }
+  int q_hy[NH], q_hx[NH], q_col[NH];
+#pragma unroll
+  for (int k = 0; k < NH; ++k) {
+    int e = k * NT + tid, hp = e >> 3, pc = e & 7;
+    q_hy[k] = hp / HWP;
+    q_hx[k] = hp - q_hy[k] * HWP;
+    q_col[k] = swz_col<128>(hp, pc);
+  }
+
+  auto stage = [&](int t, int buf) {
+    const int img = t / tiles_img, tr = t - img * tiles_img;
+    const int y0 = (tr / tiles_w) * TH, x0 = (tr - (tr / tiles_w) * tiles_w) * TW;
+    char* Pb = smem + buf * STAGE;
+    char* Qb = Pb + PB;
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const void* s = zp;
+      if (p_col[k] < p.ni) {
+        int64_t pix = ((int64_t)img * H + y0 + p_ty[k]) * W + x0 + p_tx[k];
+        s = dsrc + pix * dst_ + p_col[k];
+      }
+      __builtin_amdgcn_global_load_lds(s, (lds_void*)(Pb + (k * NT + wid * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int y = y0 - 1 + q_hy[k], x = x0 - 1 + q_hx[k];
+      const void* s = zp;
+      if (q_hy[k] < HROWS && q_hx[k] < TW + 2 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+        s = xsrc + (((int64_t)img * H + y) * W + x) * xst + q_col[k];
+      __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
+    }
+  };
+
+  // fragment read offsets (bytes; every k-step / tap shift is an immediate)
+  const int g4 = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
+  const int wco = wid / WCI, wci = wid - (wid / WCI) * WCI;   // co pair, ci group of this wave
+  int offA[TI][2];
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      offA[a][h] = tr_off<RBP>(8 * g4 + qd + 4 * h, (wco * TI + a) * 16 + 4 * pp);
+  int offB[TJ][2][3];
+#pragma unroll
+  for (int b = 0; b < TJ; ++b)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+        offB[b][h][s] = tr_off<128>(8 * g4 + qd + 4 * h + s, (wci * TJ + b) * 16 + 4 * pp);
+
+  f32x4 acc[TI][TJ][9];
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int b = 0; b < TJ; ++b)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[a][b][t] = f32x4{0, 0, 0, 0};
+
+  const int nsteps = t_end > t_beg ? t_end - t_beg : 0;
+  if (nsteps > 0) stage(t_beg, 0);
+  for (int st = 0; st < nsteps; ++st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
+    const char* Pb = smem + (st & 1) * STAGE;
+    const char* Qb = Pb + PB;
+#pragma unroll
+    for (int ks = 0; ks < TP / 32; ++ks) {
+      u32x4 af[TI];
+#pragma unroll
+      for (int a = 0; a < TI; ++a)
+        af[a] = tr_frag(Pb + ks * 32 * RBP, offA[a][0], offA[a][1]);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          u32x4 bf[TJ];
+#pragma unroll
+          for (int b = 0; b < TJ; ++b)
+            bf[b] = tr_frag(Qb + (ks + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int a = 0; a < TI; ++a)
+#pragma unroll
+            for (int b = 0; b < TJ; ++b)
+              acc[a][b][r * 3 + s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b][r * 3 + s], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+    }
+  }
+
+  float* out = p.out + (int64_t)split * p.ni * p.nj;
+#pragma unroll
+  for (int a = 0; a < TI; ++a)
+#pragma unroll
+    for (int b = 0; b < TJ; ++b)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int j = t * gq.C + cb + (wci * TJ + b) * 16 + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + (wco * TI + a) * 16 + 4 * g4 + r;
+          if (i < p.ni) out[(int64_t)i * p.nj + j] = acc[a][b][t][r];
+        }
+      }
+}
+
+template <int BI>
+int launch(const VuGemmWgrad& p, hipStream_t st) {
+  int64_t nblk = (int64_t)((p.ni + BI - 1) / BI) * (p.q.C / 64) * p.splits;
+  if (nblk <= 0) return 0;
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// (BI, BJ = 9*64) when the halo kernel serves this problem, else 0: bf16, dy
+// a plain 1x1 NHWC map, x a 3x3 stride-1 pad-1 gather of 64-channel aligned
+// sources over an image whose width is a multiple of 32 and height of 4.
+// Splits must then be whole 128-pixel tiles (m_per_split % 128 == 0).
+int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
+  const VuGather& a = p.p;
+  const VuGather& g = p.q;
+  if (dtype != VU_BF16) return 0;
+  if (a.nsrc != 1 || a.R != 1 || a.S != 1 || a.oy != 0 || a.ox != 0 || a.stride[0] % 8 || a.C != p.ni ||
+      p.ni % 8)
+    return 0;
+  if (g.R != 3 || g.S != 3 || g.sy != 1 || g.sx != 1 || g.dy != 1 || g.dx != 1 || g.oy != -1 || g.ox != -1 ||
+      g.Hs != g.H || g.Ws != g.W || a.N != g.N || a.H != g.H || a.W != g.W)
+    return 0;
+  if (g.C % 64 || p.nj != 9 * g.C) return 0;
+  for (int t = 0; t < g.nsrc; ++t)
+    if (g.cend[t] % 64 || g.stride[t] % 8) return 0;
+  if (g.W % TW || g.H % TH) return 0;
+  if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
+  *bi = p.ni <= 64 ? 64 : 128;
+  *bj = 9 * 64;
+  return 1;
+}
+
+int gemm_wgrad_v3_launch(const VuGemmWgrad& p, hipStream_t st) {
+  if (p.m_per_split % TP) return (int)hipErrorInvalidValue;
+  if (p.ni <= 64) return launch<64>(p, st);
+  return launch<128>(p, st);
+}

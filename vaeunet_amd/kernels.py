@@ -188,9 +188,11 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
     kind = query("vu_gemm_wgrad_tile", C.byref(w), dtype, C.byref(bi), C.byref(bj))
     tiles = ((ni + bi.value - 1) // bi.value) * ((nj + bj.value - 1) // bj.value)
     # split-K over pixels: pick the split count whose block count fills whole
-    # waves of resident blocks best (v2: 1 block/CU, v1: 2 blocks/CU)
-    slots = 256 if kind == 2 else 512
-    steps = (M + 63) // 64
+    # waves of resident blocks best (v2/v3: 1 block/CU, v1: 2 blocks/CU); the
+    # halo kernel (v3) splits in whole 128-pixel tiles, the others in 64 rows
+    slots = 256 if kind >= 2 else 512
+    gran = 128 if kind == 3 else 64
+    steps = (M + gran - 1) // gran
     smax = max(1, min(256, steps // 4))
     best = (-1.0, 1)
     for s in range(1, smax + 1):
@@ -202,7 +204,7 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
         if eff > best[0] + 1e-9:
             best = (eff, s)
     splits = best[1]
-    mps = ((-(-M // splits)) + 63) // 64 * 64
+    mps = ((-(-M // splits)) + gran - 1) // gran * gran
     splits = -(-M // mps)
     slab = torch.empty((splits, ni, nj), dtype=torch.float32, device=grad.device)
     w.splits, w.m_per_split = splits, mps
