@@ -1,19 +1,25 @@
 // Implicit-GEMM forward-type kernel, large-tile bf16 variant ("v2").
 //
 // Same contract as gemm_fwd.hip (out[m][j] = sum_k A[m][k] B[j][k], A an
-// im2col gather of up to three NHWC sources), used for the big bf16 layers
-// where the 128x128 register-staged kernel is LDS-write bound:
+// im2col gather of up to three NHWC sources), used for the bf16 GEMMs the
+// halo kernel (gemm_fwd3.hip) does not take: 1x1 convs (attention gates,
+// ConvTranspose2d as a GEMM with a pixel-shuffle store, input gradients of
+// 1x1 convs) and strided / parity-class gathers:
 //   * 8 waves (512 threads), block tile 256 x 128 (waves 4x2, 64x64 each) or
-//     256 x 64 (waves 8x1, 32x64 each) for the 64-channel layers;
+//     256 x 64 (waves 8x1, 32x64 each) for narrow outputs;
 //   * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per
 //     lane, no VGPR staging, no ds_write): each lane computes its own gather
-//     address — zero padding and M/N tails point the lane at a 16-byte zero
-//     page — and the XOR swizzle is applied on the SOURCE chunk so the LDS
-//     image stays lane-linear (cdna_hip_programming §5.4 rule 21);
-//   * double-buffered LDS, one barrier per 64-deep K step, 16x16x32 bf16 MFMA,
+//     address — zero padding, K / M / N tails point the lane at a 16-byte
+//     zero page — and the XOR swizzle is applied on the SOURCE chunk so the
+//     LDS image stays lane-linear (cdna_hip_programming §5.4 rule 21);
+//   * an NS-slot LDS ring (NS = min(3, K steps): short-K 1x1 GEMMs keep the
+//     footprint small so several blocks share a CU and hide each other's
+//     load latency), counted vmcnt + raw s_barrier, 16x16x32 bf16 MFMA,
 //     conflict-free ds_read_b128 fragment reads;
-//   * epilogue: fp32 tile staged through LDS, BatchNorm partial statistics on
-//     the bf16-rounded values, 16-byte coalesced stores (same as v1).
+//   * epilogue: the bf16-rounded tile staged in LDS (half the footprint of
+//     fp32), BatchNorm partial statistics on exactly those values, 16-byte
+//     coalesced stores; out_mode 1 scatters the ConvTranspose2d(k=2, s=2)
+//     pixel shuffle, out_mode 2 a stride-2 parity lattice.
 #include "common.h"
 #include "../../include/vaeunet.h"
 
@@ -28,7 +34,7 @@ VU_DEV int swz(int row, int chunk) { return row * KB + ((chunk ^ (row & 7)) << 4
 
 struct Pix { int n, h, w; bool ok; };
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd p) {
   constexpr int NT = WM * WN * 64;
   constexpr int EPC = 8;                  // bf16 per 16-byte chunk
@@ -36,11 +42,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
   constexpr int LA = BM * 8 / NT;         // A glds per thread per step
   constexpr int LB = BN * 8 / NT;         // B glds per thread per step
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  constexpr int ES = BN + 4;
+  constexpr int ES = BN + 8;              // bf16 epilogue row stride (16-byte aligned rows)
   constexpr int STAGE = (BM + BN) * KB;
-  constexpr int NSTAGE = 3;               // LDS ring: DMA runs two K steps ahead
+  constexpr int NSTAGE = NS;              // LDS ring: DMA runs NS-1 K steps ahead
   constexpr int MAIN = NSTAGE * STAGE;
-  constexpr int EPI = BM * ES * 4;
+  constexpr int EPI = BM * ES * 2;
   constexpr int RED = (NT / BN) * BN * 4;
   constexpr int LDS_BYTES = (MAIN > EPI ? MAIN : EPI) + RED;
   static_assert(LA >= 1 && LB >= 1, "tile too small for the thread count");
@@ -95,7 +101,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
       int hs = pa[i].h * g.sy + r * g.dy + g.oy;
       int ws = pa[i].w * g.sx + s * g.dx + g.ox;
       const void* gp = zp;
-      if (pa[i].ok && (unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws) {
+      if (pa[i].ok && (unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws &&
+          cbase + lchunk * EPC < g.cend[t]) {
         int64_t pix = ((int64_t)pa[i].n * g.Hs + hs) * g.Ws + ws;
         gp = src + pix * st + (cbase - c0) + lchunk * EPC;
       }
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
       int lchunk = pchunk ^ (row & 7);
       int j = n0 + row;
       const void* gp = zp;
-      if (j < p.ncol) gp = bmat + (int64_t)j * p.ldb + k0 + lchunk * EPC;
+      if (j < p.ncol && k0 + lchunk * EPC < K) gp = bmat + (int64_t)j * p.ldb + k0 + lchunk * EPC;
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
   };
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 
-  const int nk = K / BKE;
+  const int nk = (K + BKE - 1) / BKE;
   // Pipeline: stage kt+2 is issued right after the barrier of step kt, into
   // the ring slot step kt-1 just finished reading.  Each thread's own DMA is
   // retired by a COUNTED vmcnt (the NL loads of the newest stage may stay in
@@ -126,13 +133,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
   // visible; no __syncthreads() (it would drain vmcnt to 0) in the loop.
   constexpr int NL = LA + LB;
   stage(0, 0);
-  if (nk > 1) stage(1, 1);
+  if (NSTAGE >= 3 && nk > 1) stage(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    if (NSTAGE >= 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nk) stage(kt + 2, (kt + 2) % NSTAGE);
+    if (NSTAGE >= 3 && kt + 2 < nk) stage(kt + 2, (kt + 2) % NSTAGE);
+    else if (NSTAGE == 2 && kt + 1 < nk) stage(kt + 1, (kt + 1) % NSTAGE);
     const int cur = kt % NSTAGE;
     const char* A = smem + cur * STAGE;
     const char* B = A + BM * KB;
@@ -158,8 +166,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
   }
   __syncthreads();  // every wave is done with the ring before the epilogue reuses it
 
-  // ---- epilogue (as gemm_fwd.hip) ----
-  float* E = reinterpret_cast<float*>(smem);
+  // ---- epilogue: bf16-rounded tile in LDS, BN statistics, 16-byte stores ----
+  bf16_t* E = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -167,11 +175,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
       int col = wn * (BN / WN) + j * 16 + (lane & 15);
       int gj = n0 + col;
       float bv = 0.f;
-      if (p.bias && gj < p.ncol) bv = p.bias[gj];
+      if (p.bias && gj < p.ncol) bv = p.bias[p.out_mode == 1 ? gj % p.cout : gj];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int row = wm * (BM / WM) + i * 16 + 4 * (lane >> 4) + r;
-        E[row * ES + col] = rnd<bf16_t>(acc[i][j][r] + bv);
+        E[row * ES + col] = (bf16_t)f2bf(acc[i][j][r] + bv);
       }
     }
   __syncthreads();
@@ -182,9 +190,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
     constexpr int PARTS = NT / BN;
     constexpr int RPP = BM / PARTS;
     const int col = tid % BN, part = tid / BN;
+    const int r0 = part * RPP, r1 = min((part + 1) * RPP, rows_valid);
     float s = 0.f;
-    for (int r = part * RPP; r < (part + 1) * RPP; ++r)
-      if (r < rows_valid) s += E[r * ES + col];
+    for (int r = r0; r < r1; ++r) s += bf2f(E[r * ES + col]);
     red[part * BN + col] = s;
     __syncthreads();
     float tot = 0.f;
@@ -192,8 +200,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
     for (int q = 0; q < PARTS; ++q) tot += red[q * BN + col];
     const float mean = tot / (float)rows_valid;
     float m2 = 0.f;
-    for (int r = part * RPP; r < (part + 1) * RPP; ++r)
-      if (r < rows_valid) { float d = E[r * ES + col] - mean; m2 += d * d; }
+    for (int r = r0; r < r1; ++r) { float d = bf2f(E[r * ES + col]) - mean; m2 += d * d; }
     __syncthreads();
     red[part * BN + col] = m2;
     __syncthreads();
@@ -215,49 +222,73 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
     if (gj >= p.ncol) continue;
     int64_t m = m0 + row;
     bf16_t* dst;
-    if (p.out_mode == 2) {
+    if (p.out_mode == 0) {
+      dst = out + m * p.out_stride + p.out_coff + gj;
+    } else {
       int hw = g.H * g.W;
       int n = (int)(m / hw);
       int rem = (int)(m - (int64_t)n * hw);
       int h = rem / g.W, w = rem - (rem / g.W) * g.W;
-      dst = out + (((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx) * p.out_stride + p.out_coff + gj;
-    } else {
-      dst = out + m * p.out_stride + p.out_coff + gj;
+      if (p.out_mode == 2) {
+        dst = out + (((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx) * p.out_stride + p.out_coff + gj;
+      } else {
+        // ConvTranspose2d(k=2, s=2): column gj = (2a+b)*cout + co -> pixel (2h+a, 2w+b)
+        int ab = gj / p.cout, co = gj - ab * p.cout;
+        int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
+        dst = out + (((int64_t)n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
+      }
     }
-    const float* src = E + row * ES + cc;
     Vec8<bf16_t> v;
+    v.v = *reinterpret_cast<const u32x4*>(E + row * ES + cc);
     if (p.accumulate) {
-      v.load(dst);
+      Vec8<bf16_t> o;
+      o.load(dst);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v.set(q, v.get(q) + src[q]);
+      for (int q = 0; q < 8; ++q) o.set(q, o.get(q) + v.get(q));
+      o.store(dst);
     } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v.set(q, src[q]);
+      v.store(dst);
     }
-    v.store(dst);
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS>
 int launch(const VuGemmFwd& p, hipStream_t st) {
   int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
   int64_t nblk = ((M + BM - 1) / BM) * ((p.ncol + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_fwd_v2_kernel<BM, BN, WM, WN>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0, st, p);
+  hipLaunchKernelGGL((gemm_fwd_v2_kernel<BM, BN, WM, WN, NS>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0, st, p);
   return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_ns(const VuGemmFwd& p, hipStream_t st) {
+  const int nk = (p.a.R * p.a.S * p.a.C + 63) / 64;
+  if (nk == 1) return launch<BM, BN, WM, WN, 1>(p, st);
+  if (nk == 2) return launch<BM, BN, WM, WN, 2>(p, st);
+  return launch<BM, BN, WM, WN, 3>(p, st);
 }
 
 }  // namespace
 
 // Row tile of the v2 kernel for this problem, or 0 when v2 does not apply
-// (fp32, unaligned channel groups, ConvT pixel-shuffle epilogue, ragged
-// column counts, or too few tiles to fill the chip).
+// (fp32, channel groups not 64-aligned — a single 1x1 source may end on a
+// 32-channel boundary —, ragged column counts, or too few tiles to fill the
+// chip).
 int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
   const VuGather& g = p.a;
-  if (dtype != VU_BF16 || p.out_mode == 1) return 0;
-  if (g.C % 64 != 0) return 0;
-  for (int t = 0; t < g.nsrc; ++t)
-    if (g.cend[t] % 64 != 0 || g.stride[t] % 8 != 0) return 0;
-  if (p.ncol % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0) return 0;
+  if (dtype != VU_BF16) return 0;
+  const bool one = g.R == 1 && g.S == 1;
+  for (int t = 0; t < g.nsrc; ++t) {
+    const bool last = t == g.nsrc - 1;
+    if (g.stride[t] % 8 != 0) return 0;
+    if (g.cend[t] % 64 != 0 && !(one && last && g.cend[t] % 32 == 0)) return 0;
+  }
+  if (p.ncol % 8 != 0 || p.ldb % 8 != 0) return 0;
+  if (p.out_mode == 1) {
+    if (p.cout % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0) return 0;
+  } else if (p.out_stride % 8 != 0 || p.out_coff % 8 != 0) {
+    return 0;
+  }
   int64_t M = (int64_t)g.N * g.H * g.W;
   int bn = p.ncol <= 64 ? 64 : 128;
   int64_t tiles = ((M + 255) / 256) * ((p.ncol + bn - 1) / bn);
@@ -266,6 +297,6 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
 }
 
 int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st) {
-  if (p.ncol <= 64) return launch<256, 64, 8, 1>(p, st);
-  return launch<256, 128, 4, 2>(p, st);
+  if (p.ncol <= 64) return launch_ns<256, 64, 8, 1>(p, st);
+  return launch_ns<256, 128, 4, 2>(p, st);
 }

@@ -18,15 +18,17 @@ static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page[16];  // pe
 
 namespace {
 
-constexpr int BMR = 64;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// 32-byte block swizzle (rows >= 256 B): f(m) spreads the 8 rows a 32-lane
-// half reads (4 consecutive + 4 rows 8 apart) over 8 distinct bank blocks.
-// 128-B rows (4 blocks): the two 32-lane groups' rows are paired by parity.
+// 32-byte block swizzle: a 32-lane half of a transposed read touches 8 rows
+// (4 consecutive + 4 rows 8 apart), one 32-byte block each; f(m) spreads them
+// over the 8 bank blocks of the 256-byte bank window.  Rows >= 256 B: all
+// three row bits; 128-B rows (4 blocks): pairs by parity; 64-B rows (2
+// blocks): the two row quads.
 template <int RB> VU_DEV int fsw(int m) {
-  return RB >= 256 ? ((m & 3) | ((m >> 1) & 4)) : (((m >> 1) & 1) | ((m >> 2) & 2));
+  return RB >= 256 ? ((m & 3) | ((m >> 1) & 4))
+                   : RB == 128 ? (((m >> 1) & 1) | ((m >> 2) & 2)) : ((m >> 3) & 1);
 }
 
 template <int RB> VU_DEV int tr_off(int m, int col) {
@@ -51,7 +53,7 @@ VU_DEV Col decode_col(const VuGather& g, int col, int ncols) {
   return d;
 }
 
-template <int BI, int BJ, int WI, int WJ>
+template <int BI, int BJ, int WI, int WJ, int BMR>
 __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWgrad p) {
   constexpr int NT = WI * WJ * 64;
   constexpr int RBP = BI * 2, RBQ = BJ * 2;          // LDS row bytes
@@ -212,12 +214,12 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     }
 }
 
-template <int BI, int BJ, int WI, int WJ>
+template <int BI, int BJ, int WI, int WJ, int BMR>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int itiles = (p.ni + BI - 1) / BI, jtiles = (p.nj + BJ - 1) / BJ;
   int64_t nblk = (int64_t)itiles * jtiles * p.splits;
   if (nblk <= 0) return 0;
-  hipLaunchKernelGGL((gemm_wgrad_v2_kernel<BI, BJ, WI, WJ>), dim3((unsigned)nblk), dim3(WI * WJ * 64), 0, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_v2_kernel<BI, BJ, WI, WJ, BMR>), dim3((unsigned)nblk), dim3(WI * WJ * 64), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -232,12 +234,18 @@ int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
       if (g->cend[t] % 8 || g->stride[t] % 8) return 0;
   int64_t M = (int64_t)p.p.N * p.p.H * p.p.W;
   if (M < 4096) return 0;
+  // small outputs (the attention gates' 1x1 convs) get a tile that fits them
+  // instead of streaming zero columns through a 256-wide one
+  if (p.ni <= 32 && p.nj <= 64) { *bi = 32; *bj = 64; return 1; }
+  if (p.ni <= 64 && p.nj <= 128) { *bi = 64; *bj = 128; return 1; }
   *bi = p.ni <= 64 ? 64 : 128;
   *bj = 256;
   return 1;
 }
 
 int gemm_wgrad_v2_launch(const VuGemmWgrad& p, hipStream_t st) {
-  if (p.ni <= 64) return launch<64, 256, 1, 8>(p, st);
-  return launch<128, 256, 2, 4>(p, st);
+  if (p.ni <= 32 && p.nj <= 64) return launch<32, 64, 2, 4, 128>(p, st);
+  if (p.ni <= 64 && p.nj <= 128) return launch<64, 128, 2, 4, 128>(p, st);
+  if (p.ni <= 64) return launch<64, 256, 1, 8, 64>(p, st);
+  return launch<128, 256, 2, 4, 64>(p, st);
 }
