@@ -24,72 +24,115 @@ namespace {
 // Combining per-tile (sum, centered M2) pairs without a division per tile:
 // for a group of tiles with mean m, M2 = sum_t [M2_t + n_t (m_t - m)^2]
 // (exact, and as stable as Chan's pairwise update since every deviation is
-// taken from the group mean).  Stage 1 does this for blocks of tiles (two
-// passes over the block's tiles, the second from L2), stage 2 for the blocks.
-// stage 1: grid (ceil(C/64), S), 256 threads = 64 channels x 4 tile lanes
+// taken from the group mean).  Both stages hold their inputs in registers and
+// make the two passes (group mean, then M2 about it) over the registers: the
+// loads of a lane are independent and issue back to back (these launches are
+// latency-bound, not bandwidth-bound).
+constexpr int STATS_TPB = 32;   // tiles per stage-1 block (8 per lane)
+constexpr int STATS_MAXS = 256; // stage-1 blocks per channel group (8 per stage-2 lane)
+
+// stage 1: grid (ceil(C/64), S), 256 threads = 64 channels x 4 tile lanes.
+// A block reduces its tiles in rounds of STATS_TPB (one round unless the
+// problem has more than STATS_TPB * STATS_MAXS tiles); rounds merge with
+// Chan's pairwise update.
 __global__ void bn_stats_stage1(const float* psum, const float* pm2, int tiles, int64_t tile_rows,
                                 int64_t rows, int C, int S, double* ws) {
   __shared__ double sh[4][64];
-  int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
-  int c = blockIdx.x * 64 + cl;
-  bool ok = c < C;
-  int per = (tiles + S - 1) / S;
-  int tb = blockIdx.y * per, te = min(tiles, tb + per);
-  int64_t n_blk = te > tb ? min(rows, (int64_t)te * tile_rows) - (int64_t)tb * tile_rows : 0;
-  const double inv_full = 1.0 / (double)tile_rows;
-  auto tile_n = [&](int t) -> int64_t {
-    int64_t nb = rows - (int64_t)t * tile_rows;
-    return nb > tile_rows ? tile_rows : nb;
-  };
-  // pass 1: block sum
-  double s0 = 0, s1 = 0;
-  if (ok) {
-    int t = tb + tl;
-    for (; t + 4 < te; t += 8) { s0 += psum[(int64_t)t * C + c]; s1 += psum[(int64_t)(t + 4) * C + c]; }
-    for (; t < te; t += 4) s0 += psum[(int64_t)t * C + c];
-  }
-  sh[tl][cl] = s0 + s1;
-  __syncthreads();
-  double m = n_blk > 0 ? (sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]) / (double)n_blk : 0.0;
-  __syncthreads();
-  // pass 2: M2 about the block mean
-  double q0 = 0, q1 = 0;
-  if (ok) {
-    for (int t = tb + tl; t < te; t += 4) {
-      int64_t nt = tile_n(t);
-      double st = psum[(int64_t)t * C + c];
-      double mt = nt == tile_rows ? st * inv_full : st / (double)nt;
-      double d = mt - m;
-      double v = (double)pm2[(int64_t)t * C + c] + (double)nt * d * d;
-      if ((t - tb) & 4) q1 += v; else q0 += v;
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  const int per = (tiles + S - 1) / S;
+  const int tb0 = blockIdx.y * per, te0 = min(tiles, tb0 + per);
+  constexpr int U = STATS_TPB / 4;
+  double N = 0, Mn = 0, Q = 0;   // running (n, mean, M2) of the rounds so far
+  for (int tb = tb0; tb < te0; tb += STATS_TPB) {
+    const int te = min(te0, tb + STATS_TPB);
+    const int64_t n_r = min(rows, (int64_t)te * tile_rows) - (int64_t)tb * tile_rows;
+    float sv[U], mv[U];
+    double nv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tb + tl + 4 * u;
+      const bool in = ok && t < te;
+      sv[u] = in ? psum[(int64_t)t * C + c] : 0.f;
+      mv[u] = in ? pm2[(int64_t)t * C + c] : 0.f;
+      int64_t nt = rows - (int64_t)t * tile_rows;
+      nv[u] = in ? (double)(nt > tile_rows ? tile_rows : nt) : 0.0;
     }
+    double s = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += (double)sv[u];
+    sh[tl][cl] = s;
+    __syncthreads();
+    const double m = (sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]) / (double)n_r;
+    __syncthreads();
+    double q = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (nv[u] > 0) {
+        const double d = (double)sv[u] / nv[u] - m;
+        q += (double)mv[u] + nv[u] * d * d;
+      }
+    }
+    sh[tl][cl] = q;
+    __syncthreads();
+    const double q_r = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
+    __syncthreads();
+    const double nn = N + (double)n_r, d = m - Mn;
+    Q += q_r + d * d * N * (double)n_r / nn;
+    Mn += d * (double)n_r / nn;
+    N = nn;
   }
-  sh[tl][cl] = q0 + q1;
-  __syncthreads();
   if (tl == 0 && ok) {
     double* o = ws + ((int64_t)blockIdx.y * C + c) * 3;
-    o[0] = (double)n_blk; o[1] = m; o[2] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
+    o[0] = N; o[1] = Mn; o[2] = Q;
   }
 }
 
+// stage 2: 1024 threads = 32 channels x 32 lanes, <= 8 stage-1 partials per lane
 __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gamma, const float* beta,
                                 float* rmean, float* rvar, float momentum, float eps, float* scale,
                                 float* shift, float* smean, float* sinvstd, int64_t* nbt) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  __shared__ double sh[2][32][33];
+  const int cl = threadIdx.x & 31, q = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  const bool ok = c < C;
+  constexpr int U = STATS_MAXS / 32;
+  double nv[U], mv[U], qv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int sidx = q + 32 * u;
+    const bool in = ok && sidx < S;
+    const double* o = ws + ((int64_t)(in ? sidx : 0) * C + (ok ? c : 0)) * 3;
+    nv[u] = in ? o[0] : 0.0;
+    mv[u] = in ? o[1] : 0.0;
+    qv[u] = in ? o[2] : 0.0;
+  }
   double n = 0, sm = 0;
-  for (int s = 0; s < S; ++s) {
-    const double* o = ws + ((int64_t)s * C + c) * 3;
-    n += o[0];
-    sm += o[0] * o[1];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { n += nv[u]; sm += nv[u] * mv[u]; }
+  sh[0][q][cl] = n; sh[1][q][cl] = sm;
+  __syncthreads();
+#pragma unroll
+  for (int w = 16; w >= 1; w >>= 1) {
+    if (q < w) { sh[0][q][cl] += sh[0][q + w][cl]; sh[1][q][cl] += sh[1][q + w][cl]; }
+    __syncthreads();
   }
-  double m = n > 0 ? sm / n : 0.0;
+  n = sh[0][0][cl];
+  const double m = n > 0 ? sh[1][0][cl] / n : 0.0;
+  __syncthreads();
   double M2 = 0;
-  for (int s = 0; s < S; ++s) {
-    const double* o = ws + ((int64_t)s * C + c) * 3;
-    double d = o[1] - m;
-    M2 += o[2] + o[0] * d * d;
+#pragma unroll
+  for (int u = 0; u < U; ++u) { const double d = mv[u] - m; M2 += qv[u] + nv[u] * d * d; }
+  sh[0][q][cl] = M2;
+  __syncthreads();
+#pragma unroll
+  for (int w = 16; w >= 1; w >>= 1) {
+    if (q < w) sh[0][q][cl] += sh[0][q + w][cl];
+    __syncthreads();
   }
+  if (q != 0 || !ok) return;
+  M2 = sh[0][0][cl];
   double var = n > 0 ? M2 / n : 0.0;
   float invstd = (float)(1.0 / sqrt(var + (double)eps));
   float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
@@ -374,10 +417,15 @@ extern "C" int64_t vu_reduce_workspace_bytes(int64_t P, int C) {
   return (int64_t)RED_MAXBLK * 2 * C * (int64_t)sizeof(float);
 }
 
-extern "C" int64_t vu_bn_finalize_workspace_bytes(int tiles, int C) {
-  int S = (tiles + 63) / 64;
-  if (S > 64) S = 64;
+static int stats_blocks(int tiles) {
+  int S = (tiles + STATS_TPB - 1) / STATS_TPB;
+  if (S > STATS_MAXS) S = STATS_MAXS;
   if (S < 1) S = 1;
+  return S;
+}
+
+extern "C" int64_t vu_bn_finalize_workspace_bytes(int tiles, int C) {
+  int S = stats_blocks(tiles);
   return (int64_t)S * C * 3 * sizeof(double);
 }
 
@@ -387,13 +435,11 @@ extern "C" int vu_bn_finalize(const float* psum, const float* pm2, int tiles, in
                               float* scale, float* shift, float* save_mean, float* save_invstd,
                               int64_t* num_batches_tracked, float* workspace, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int S = (tiles + 63) / 64;
-  if (S > 64) S = 64;
-  if (S < 1) S = 1;
+  int S = stats_blocks(tiles);
   double* ws = reinterpret_cast<double*>(workspace);
   hipLaunchKernelGGL(bn_stats_stage1, dim3((C + 63) / 64, S), dim3(256), 0, st, psum, pm2, tiles,
                      tile_rows, rows, C, S, ws);
-  hipLaunchKernelGGL(bn_stats_stage2, dim3((C + 63) / 64), dim3(64), 0, st, ws, S, C, gamma, beta,
+  hipLaunchKernelGGL(bn_stats_stage2, dim3((C + 31) / 32), dim3(1024), 0, st, ws, S, C, gamma, beta,
                      running_mean, running_var, momentum, eps, scale, shift, save_mean, save_invstd,
                      num_batches_tracked);
   return (int)hipGetLastError();
