@@ -33,14 +33,16 @@ CONV3_GFLOP_PER_IMG = 1103.5
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--classes", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    ap.add_argument("--torch-optim", action="store_true",
+                    help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
     return ap.parse_args()
 
 
@@ -96,7 +98,14 @@ def main():
     model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
     model.train()
     reducer = parallel.attach(model) if world > 1 else None
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-5, foreach=True)
+    if args.torch_optim:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-5, foreach=True)
+        clip = lambda ps, m: torch.nn.utils.clip_grad_norm_(ps, m, foreach=True)  # noqa: E731
+    else:
+        # same math as torch.optim.AdamW / clip_grad_norm_ (tests/test_gpu_optim.py),
+        # one multi-tensor launch per phase
+        from vaeunet_amd.optim import FusedAdamW, clip_grad_norm_ as clip
+        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-5)
     crit = CombinedLoss()
     x, t = synthetic(args.batch, args.size, args.classes, rank, dev)
 
@@ -109,7 +118,7 @@ def main():
         loss.backward()
         if reducer is not None:
             reducer.finish()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0, foreach=True)
+        clip(model.parameters(), 1.0)
         opt.step()
         opt.zero_grad(set_to_none=reducer is None)
         return loss

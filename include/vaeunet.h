@@ -247,6 +247,41 @@ int vu_kl_free_bits(const float* mu, const float* logvar, int B, int L,
 int vu_sumsq(const float* x, int64_t n, double* out, double* workspace,
              void* stream);
 
+/* Multi-tensor table entry (device memory).  Replaces the foreach loops of
+ * torch.nn.utils.clip_grad_norm_ (train.py:408) and torch.optim.AdamW.step
+ * (train.py:409, optimizer built at train.py:334).  A tensor's param, grad
+ * and moment buffers share strides and are processed as flat fp32 storage of
+ * numel elements, cut into vu_mt_chunk_elems() chunks; chunk0 = number of
+ * chunks of all previous entries (entries in chunk order).  step_size =
+ * lr / (1 - beta1^step) and bc2_sqrt = sqrt(1 - beta2^step) per tensor. */
+typedef struct VuMtEntry {
+  void* param;
+  void* grad;
+  void* exp_avg;
+  void* exp_avg_sq;
+  int64_t numel;
+  int64_t chunk0;
+  float step_size;
+  float bc2_sqrt;
+} VuMtEntry;
+
+int64_t vu_mt_chunk_elems(void);
+/* ||grads||_2 over all entries (fp64 accumulation) -> *total_norm, and
+ * *clip_coef = min(1, max_norm / (total_norm + 1e-6)) (either may be NULL);
+ * workspace: nchunks doubles */
+int vu_mt_grad_norm(const VuMtEntry* table, int ntensors, int64_t nchunks,
+                    float max_norm, float* total_norm, float* clip_coef,
+                    double* workspace, void* stream);
+/* grads *= *coef (clip_grad_norm_'s in-place scaling) */
+int vu_mt_scale_grads(const VuMtEntry* table, int ntensors, int64_t nchunks,
+                      const float* coef, void* stream);
+/* one AdamW step over all entries; grads multiplied by *grad_scale when
+ * given (not written back); decay = 1 - lr*weight_decay */
+int vu_mt_adamw(const VuMtEntry* table, int ntensors, int64_t nchunks,
+                float decay, float one_minus_beta1, float beta2,
+                float one_minus_beta2, float eps, const float* grad_scale,
+                void* stream);
+
 /* ---- VAE-U-Net (unet/unet_resnet.py) ----------------------------------- */
 /* ResNet34 stem max-pool 3x3/s2/p1 (timm resnet34, unet_resnet.py:131):
  * idx receives the window argmax (0..8, first max wins) per output element */

@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 import torch
 
 from golden_util import load
@@ -95,3 +96,17 @@ def test_product_path_has_no_oracle_or_fallback():
         if fn.endswith(".py"):
             txt = open(os.path.join(pkg, fn)).read()
             assert "oracle" not in txt.replace("oracle/", "").replace("the oracle", ""), fn
+
+
+def test_optim_dense_layout_check():
+    """Host logic of the multi-tensor optimizer: which layouts walk as flat storage."""
+    from vaeunet_amd.optim import _is_dense, FusedAdamW
+    assert _is_dense(torch.empty(4, 3, 5, 5))
+    assert _is_dense(torch.empty(4, 3, 5, 5).contiguous(memory_format=torch.channels_last))
+    assert _is_dense(torch.empty(7))
+    assert not _is_dense(torch.empty(4, 6)[:, :3])
+    assert not _is_dense(torch.empty(4, 6).t()[::2])
+    with pytest.raises(NotImplementedError):
+        FusedAdamW([torch.nn.Parameter(torch.zeros(3))], amsgrad=True)
+    opt = FusedAdamW([torch.nn.Parameter(torch.zeros(3))], lr=1e-4, weight_decay=1e-5)
+    assert opt.param_groups[0]["betas"] == (0.9, 0.999) and opt.param_groups[0]["eps"] == 1e-8

@@ -42,6 +42,11 @@ class VuGemmWgrad(C.Structure):
                 ("splits", C.c_int32), ("m_per_split", _l), ("out", _p)]
 
 
+class VuMtEntry(C.Structure):
+    _fields_ = [("param", _p), ("grad", _p), ("exp_avg", _p), ("exp_avg_sq", _p),
+                ("numel", _l), ("chunk0", _l), ("step_size", _f), ("bc2_sqrt", _f)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "vu_gemm_fwd": (_i, [C.POINTER(VuGemmFwd), _i, _p]),
@@ -82,6 +87,10 @@ _SIGS = {
     "vu_bce_dice_bwd": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p]),
     "vu_kl_free_bits2": (_i, [_p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
     "vu_sumsq": (_i, [_p, _l, _p, _p, _p]),
+    "vu_mt_chunk_elems": (_l, []),
+    "vu_mt_grad_norm": (_i, [_p, _i, _l, _f, _p, _p, _p, _p]),
+    "vu_mt_scale_grads": (_i, [_p, _i, _l, _p, _p]),
+    "vu_mt_adamw": (_i, [_p, _i, _l, _f, _f, _f, _f, _f, _p, _p]),
     "vu_maxpool3s2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _p, _i, _p]),
     "vu_maxpool3s2_bwd": (_i, [_p, _l, _p, _i, _i, _i, _i, _p, _l, _i, _i, _p]),
     "vu_bn_add_relu": (_i, [_p, _l, _p, _p, _p, _l, _p, _p, _l, _i, _p, _l, _i, _p]),

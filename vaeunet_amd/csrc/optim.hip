@@ -1,0 +1,138 @@
+// Optimizer tail of the training step (train.py:406-411): global-norm
+// gradient clipping (torch.nn.utils.clip_grad_norm_, norm_type 2) and AdamW
+// (torch.optim.AdamW, decoupled weight decay, amsgrad off) as multi-tensor
+// launches: one table of tensors, one launch per phase instead of ~15
+// foreach launches per parameter group.
+//
+// Table layout (device memory, VuMtEntry per tensor): the tensors' storage is
+// processed linearly (params, grads and moments share strides), cut into
+// CHUNK-element chunks; entry.chunk0 is the prefix count of chunks so a block
+// finds its tensor by binary search.
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+namespace {
+
+constexpr int MT_THREADS = 256;
+constexpr int MT_CHUNK = 8192;  // elements per block (32 per thread)
+
+VU_DEV int find_tensor(const VuMtEntry* t, int n, int64_t chunk) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t[mid].chunk0 <= chunk) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// per-chunk sum of squares of the grads (fp64, fixed order inside the block)
+__global__ void mt_sumsq_kernel(const VuMtEntry* t, int n, double* part) {
+  __shared__ double sh[MT_THREADS / 64];
+  const int64_t chunk = blockIdx.x;
+  const int k = find_tensor(t, n, chunk);
+  const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
+  const int64_t end = min(t[k].numel, off + MT_CHUNK);
+  const float* g = reinterpret_cast<const float*>(t[k].grad);
+  double a = 0;
+  for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
+    double v = g[i];
+    a += v * v;
+  }
+  a = warp_sum_d(a);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) part[chunk] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+// total norm and clip coefficient: coef = min(1, max_norm / (norm + 1e-6))
+__global__ void mt_norm_final(const double* part, int64_t nchunks, float max_norm, float* norm_out,
+                              float* coef_out) {
+  __shared__ double sh[4];
+  double a = 0;
+  for (int64_t i = threadIdx.x; i < nchunks; i += 256) a += part[i];
+  a = warp_sum_d(a);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const float norm = (float)sqrt((sh[0] + sh[1]) + (sh[2] + sh[3]));
+  if (norm_out) *norm_out = norm;
+  if (coef_out) {
+    float c = max_norm / (norm + 1e-6f);
+    *coef_out = c < 1.f ? c : 1.f;
+  }
+}
+
+__global__ void mt_scale_kernel(const VuMtEntry* t, int n, const float* coef) {
+  const int64_t chunk = blockIdx.x;
+  const int k = find_tensor(t, n, chunk);
+  const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
+  const int64_t end = min(t[k].numel, off + MT_CHUNK);
+  float* g = reinterpret_cast<float*>(t[k].grad);
+  const float c = *coef;
+  for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) g[i] *= c;
+}
+
+// AdamW, the element order of torch's _multi_tensor_adamw:
+//   p *= 1 - lr*wd; m = lerp(m, g, 1-b1); v = v*b2 + (1-b2) g^2;
+//   p += -step_size * m / (sqrt(v) / bc2_sqrt + eps)
+// with the per-tensor step_size = lr / (1 - b1^step), bc2_sqrt = sqrt(1 - b2^step)
+// taken from the table (tensors may be at different step counts).  The
+// scalar factors (1 - lr*wd, 1 - b1, 1 - b2) arrive precomputed in double and
+// rounded once, as torch's foreach path passes them.
+__global__ void mt_adamw_kernel(const VuMtEntry* t, int n, float decay, float w1, float beta2, float w2,
+                                float eps, const float* gscale) {
+  const int64_t chunk = blockIdx.x;
+  const int k = find_tensor(t, n, chunk);
+  const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
+  const int64_t end = min(t[k].numel, off + MT_CHUNK);
+  float* p = reinterpret_cast<float*>(t[k].param);
+  const float* g = reinterpret_cast<const float*>(t[k].grad);
+  float* m = reinterpret_cast<float*>(t[k].exp_avg);
+  float* v = reinterpret_cast<float*>(t[k].exp_avg_sq);
+  const float step_size = t[k].step_size, bc2s = t[k].bc2_sqrt;
+  const float gs = gscale ? *gscale : 1.f;
+  for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
+    float gi = g[i];
+    if (gscale) gi *= gs;
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = mi + w1 * (gi - mi);                       // lerp, weight < 0.5 branch
+    float vi = v[i] * beta2;
+    vi = vi + w2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    pi = pi + (-step_size) * (mi / denom);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t vu_mt_chunk_elems() { return MT_CHUNK; }
+
+extern "C" int vu_mt_grad_norm(const VuMtEntry* table, int ntensors, int64_t nchunks, float max_norm,
+                               float* total_norm, float* clip_coef, double* workspace, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (ntensors <= 0 || nchunks <= 0) return 0;
+  hipLaunchKernelGGL(mt_sumsq_kernel, dim3((unsigned)nchunks), dim3(MT_THREADS), 0, st, table, ntensors,
+                     workspace);
+  hipLaunchKernelGGL(mt_norm_final, dim3(1), dim3(256), 0, st, workspace, nchunks, max_norm, total_norm,
+                     clip_coef);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_mt_scale_grads(const VuMtEntry* table, int ntensors, int64_t nchunks, const float* coef,
+                                 void* stream) {
+  if (ntensors <= 0 || nchunks <= 0) return 0;
+  hipLaunchKernelGGL(mt_scale_kernel, dim3((unsigned)nchunks), dim3(MT_THREADS), 0, (hipStream_t)stream, table,
+                     ntensors, coef);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_mt_adamw(const VuMtEntry* table, int ntensors, int64_t nchunks, float decay,
+                           float one_minus_beta1, float beta2, float one_minus_beta2, float eps,
+                           const float* grad_scale, void* stream) {
+  if (ntensors <= 0 || nchunks <= 0) return 0;
+  hipLaunchKernelGGL(mt_adamw_kernel, dim3((unsigned)nchunks), dim3(MT_THREADS), 0, (hipStream_t)stream, table,
+                     ntensors, decay, one_minus_beta1, beta2, one_minus_beta2, eps, grad_scale);
+  return (int)hipGetLastError();
+}
