@@ -19,6 +19,7 @@ Each is one table upload plus one to three launches for ALL parameters
 import ctypes as C
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 
@@ -117,6 +118,7 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=Fals
     _lib.call("vu_mt_grad_norm", tab.ptr(), tab.n, tab.nchunks, float(max_norm), _lib.ptr(out[0:1]),
               _lib.ptr(out[1:2]), _lib.ptr(ws), s)
     _lib.call("vu_mt_scale_grads", tab.ptr(), tab.n, tab.nchunks, _lib.ptr(out[1:2]), s)
+    increment_version(grads)  # written in place behind autograd's back
     total = out[0]
     if error_if_nonfinite and not torch.isfinite(total):
         raise RuntimeError(f"The total norm of order {norm_type} for gradients from `parameters` "
@@ -186,4 +188,8 @@ class FusedAdamW(torch.optim.Optimizer):
             _lib.call("vu_mt_adamw", tab.ptr(), tab.n, tab.nchunks,
                       1.0 - lr * float(group["weight_decay"]), 1.0 - beta1, float(beta2),
                       1.0 - beta2, float(group["eps"]), None, _lib.stream())
+            # the kernel updated params and moments in place: bump their
+            # version counters like torch's in-place ops do (derived caches,
+            # e.g. the engine's bf16 weight layouts, key on them)
+            increment_version([r[k] for r in rows for k in (0, 2, 3)])
         return loss
