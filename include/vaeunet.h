@@ -96,6 +96,12 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
                    int cvalid, int64_t s_i, int64_t s_tap, int64_t s_c,
                    float* out, int accumulate, void* stream);
 
+/* Dispatcher tuning (tests / experiments).  VU_TUNE_V4_MIN_BLOCKS: smallest
+ * grid for which the ping-pong 3x3 kernel (gemm_fwd4.hip) is used (default
+ * 256 = one block per CU); 0 forces it wherever its tiles fit. */
+#define VU_TUNE_V4_MIN_BLOCKS 0
+int vu_gemm_set_tuning(int key, int value);
+
 /* ---- weights ----------------------------------------------------------- */
 /* out[i0][i1][i2][i3] (contiguous) = in[base + i0*s0 + i1*s1 + i2*s2 + i3*s3]
  * for i3 < d3v, 0 for d3v <= i3 < d3 (channel padding of the 3-channel input

@@ -107,6 +107,81 @@ def test_conv3x3_fwd_dgrad_wgrad(mode, case):
         _close(gw, wref, mode, what=f"wgrad {fmt}")
 
 
+V4_CASES = [
+    # (N, [cin per source], H, W, cout): ping-pong halo kernel (gemm_fwd4.hip)
+    (1, [64], 8, 32, 256),           # 256x256 block tile, 2 chunks
+    (2, [96, 64], 16, 64, 256),      # two sources, chunk crosses no source edge, 5 chunks
+    (1, [32, 32, 64], 16, 32, 128),  # three sources, 512x128 block tile
+    (2, [128], 32, 32, 128),
+    (1, [64], 32, 64, 64),           # 1024x64 block tile (32x32 pixels)
+    (1, [96, 32], 32, 32, 64),
+]
+
+
+@pytest.mark.parametrize("case", V4_CASES)
+def test_conv3x3_pingpong_kernel(case):
+    """bf16 ping-pong halo kernel forced onto small problems (the production
+    dispatcher only picks it for >= 256 blocks): forward with BN statistics,
+    bias, accumulate into a channel slice, and the flipped-weight input grad."""
+    from vaeunet_amd import _lib
+    K, E = _k()
+    N, cins, H, W, co = case
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(N, c, H, W, generator=g).to(torch.bfloat16).float() for c in cins]
+    cin = sum(cins)
+    w = torch.randn(co, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    wq = w.to(torch.bfloat16).float()
+    b = torch.randn(co, generator=g)
+    d = _code("bf16")
+    _lib.call("vu_gemm_set_tuning", 0, 0)
+    try:
+        srcs = [_act(x, "bf16") for x in xs]
+        out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
+        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, srcs, E.w3x3_fwd(w.to(DEV), d), co, out)) in (256, 512, 1024)
+        st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, out, d, stats=True)
+        ref = F.conv2d(torch.cat(xs, 1), wq, padding=1)
+        _close(out, ref, "bf16", what="fwd")
+        stored = out.float().cpu()
+        n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                         dtype=torch.float64)
+        s = st.psum.double().cpu()
+        mean = s.sum(0) / n.sum()
+        m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+        torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close((m2.sum(0) / n.sum()).float(), stored.var((0, 2, 3), unbiased=False),
+                                   rtol=1e-4, atol=1e-5)
+        # bias + accumulate into the upper channel slice of a wider tensor
+        base = torch.randn(N, co + 64, H, W, generator=g).to(torch.bfloat16).float()
+        wide = _act(base, "bf16")
+        K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, wide, d, out_coff=64,
+                   bias=b.to(DEV), accumulate=True)
+        exp = base.clone()
+        exp[:, 64:] += ref + b[None, :, None, None]
+        _close(wide, exp, "bf16", what="bias+accumulate")
+        # input gradient (flipped weights) when cin is a tile width
+        if cin in (64, 128, 256) and co % 32 == 0:
+            dy = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
+            dx = K.empty_act(N, cin, H, W, torch.bfloat16, DEV)
+            K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), cin, dx, d)
+            _close(dx, torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1), "bf16", what="dgrad")
+    finally:
+        _lib.call("vu_gemm_set_tuning", 0, 256)
+
+
+def _row_tile_args(K, srcs, wmat, ncol, out):
+    import ctypes as C
+    from vaeunet_amd import _lib
+    a = _lib.VuGemmFwd()
+    a.a = K.gather3x3(srcs)
+    a.b = wmat.data_ptr()
+    a.ldb = wmat.shape[-1]
+    a.ncol = ncol
+    a.out = out.data_ptr()
+    a.out_stride = K.pstride(out)
+    a.out_mode = 0
+    return (C.byref(a), 1)
+
+
 @pytest.mark.parametrize("mode", ["f32", "bf16"])
 @pytest.mark.parametrize("case", [(4, 64, 32, 32, 32), (4, 128, 32, 32, 64), (2, 256, 32, 32, 128),
                                   (1, 48, 16, 16, 24),

@@ -325,6 +325,8 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v3_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st);
 
 static bool use_v2(int dtype) {
   static int mode = -1;
@@ -344,7 +346,20 @@ static bool use_v3(int dtype) {
   return mode == 1 && use_v2(dtype);
 }
 
+static bool use_v4(int dtype) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VU_GEMM_V4");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode == 1 && use_v3(dtype);
+}
+
 extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
+  if (use_v4(dtype)) {
+    int bm = gemm_fwd_v4_bm(*args, dtype);
+    if (bm) return bm;
+  }
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 256;
   if (use_v2(dtype)) {
     int bm = gemm_fwd_v2_bm(*args, dtype);
@@ -361,6 +376,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
     if (g.cend[t] % epc != 0 || g.stride[t] % epc != 0) return (int)hipErrorInvalidValue;
   if ((args->ldb % epc) != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);

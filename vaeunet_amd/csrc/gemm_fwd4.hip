@@ -1,0 +1,447 @@
+// 3x3 / stride-1 / pad-1 convolution as a halo-tiled implicit GEMM with a
+// PING-PONG wave schedule ("v4", bf16).  Serves the DoubleConv forward convs
+// (unet_parts.py:40,43) and their stride-1 input-gradient convs (flipped
+// weights) when the output-channel count is a multiple of 64/128/256.
+//
+// Why another kernel: v3 (gemm_fwd3.hip) runs all eight waves of a block in
+// lockstep -- every wave reads its fragments, then every wave issues MFMAs --
+// so each SIMD's matrix pipe idles while both of its waves wait on LDS, and
+// rocprof shows ~35 % of wave time parked at barriers.  Here the two halves
+// of the block (waves 0-3 and 4-7, one of each per SIMD) run the same
+// program one barrier apart: while one half streams its fragments out of LDS
+// the other half issues MFMAs, so the pipe sees back-to-back 16-MFMA
+// segments from alternating waves (cdna_hip_programming.md "256^2 8-phase
+// template"; MI355X_MICROARCH.md "Two waves per SIMD").
+//
+//   * every wave owns a 128-pixel x 64-channel output tile (8 x 4 fragments
+//     of v_mfma_f32_16x16x32_bf16, 128 accumulator registers); the block is
+//     256 x 256 (8x32 pixels), 512 x 128 (16x32) or 1024 x 64 (32x32);
+//   * K is walked in steps of one tap x 32 input channels; per 32-channel
+//     chunk the (TH+2) x (TW+2) halo lands ONCE in LDS (64-byte pixel rows,
+//     contiguous 1 KiB fragment reads -- no swizzle needed) and the nine taps
+//     read it in place at a shifted row;
+//   * weights stream per step into a 3-slot ring (prefetch distance 2), the
+//     next chunk's halo streams in during the first steps of the current
+//     chunk, both by LDS-DMA (global_load_lds_dwordx4) with counted vmcnt
+//     waits and raw s_barrier so DMA stays in flight across barriers;
+//   * MFMA operands are (weights, pixels): each lane's accumulator holds 4
+//     consecutive output channels of one pixel, which makes the BatchNorm
+//     partial statistics a register + 16-lane reduction and the bf16 output
+//     staging 8-byte LDS writes;
+//   * epilogue: bias, storage rounding, per-tile (sum, centered M2) of the
+//     rounded values (same contract as v1-v3), 16-byte NHWC stores.
+#include "common.h"
+#include "../../include/vaeunet.h"
+#include <stdlib.h>
+
+static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page4[16];
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int BN> struct PP;
+template <> struct PP<256> { static constexpr int WM = 2, WN = 4, TH = 8, TW = 32; };
+template <> struct PP<128> { static constexpr int WM = 4, WN = 2, TH = 16, TW = 32; };
+template <> struct PP<64> { static constexpr int WM = 8, WN = 1, TH = 32, TW = 32; };
+
+VU_DEV void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+  }
+}
+
+// A workgroup barrier nothing is scheduled across (the ping-pong relies on
+// the exact placement of reads, DMA issues and MFMAs between barriers).
+VU_DEV void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// XM (experiment mode, timing studies only; 0 in production): 1 = no DMA in
+// the main loop, 2 = no DMA and no barriers in the main loop, 3 = no MFMA.
+template <int BN, int XM>
+__global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
+  constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
+  constexpr int NT = 512;
+  constexpr int BM = TH * TW;
+  static_assert(BM == WM * 128 && BN == WN * 64 && WM * WN == 8, "wave grid");
+  constexpr int HW = TW + 2, HP = (TH + 2) * HW;
+  constexpr int HPIECES = HP * 4;                 // 16-byte pieces per chunk halo
+  constexpr int NHP1 = (HPIECES + 255) / 256;     // halo DMA slots per half-1 thread
+  constexpr int HALO = HP * 64;
+  constexpr int WPIECES = BN * 4;
+  constexpr int LB0 = WPIECES / 256;              // weight DMA slots per half-0 thread
+  constexpr int LB0A = (LB0 + 1) / 2;             // ... issued in phase 1 (rest in phase 2)
+  constexpr int WSLOT = BN * 64;
+  constexpr int NBW = 3;                          // weight ring (prefetch distance 2)
+  constexpr int PPS1 = (NHP1 + 7) / 8;            // halo slots issued per step (steps 0..7)
+  constexpr int MAIN = 2 * HALO + NBW * WSLOT;
+  constexpr int ROWB = BN * 2 + 16;               // bf16 staging row (padded)
+  constexpr int EPI = BM * ROWB;
+  constexpr int RED = 2 * WM * BN * 4;
+  constexpr int LDS_BYTES = MAIN > EPI + RED ? MAIN : EPI + RED;
+  static_assert(LDS_BYTES <= 163840, "LDS");
+  static_assert(NHP1 <= 8 * PPS1 && LB0 >= 1, "DMA schedule");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const VuGather& g = p.a;
+  const int H = g.H, W = g.W;
+  const int tx_n = W / TW, ty_n = H / TH;
+  const int mtiles = g.N * ty_n * tx_n;
+  const int ntiles = p.ncol / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int img = mt / (ty_n * tx_n);
+  const int trem = mt - img * (ty_n * tx_n);
+  const int y0 = (trem / tx_n) * TH, x0 = (trem - (trem / tx_n) * tx_n) * TW;
+  const int n0 = nt * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int grp = wid >> 2;  // ping-pong half (one wave of each half per SIMD)
+  const int nchunk = g.C / 32;
+  const int nk = nchunk * 9;
+
+  // ---- DMA roles ------------------------------------------------------------
+  // vmcnt counts a wave's loads in issue order, so a wave that mixes slow
+  // (HBM) halo loads with fast (L2) weight loads would have every weight wait
+  // also drain the halo.  The halves therefore split the streams: waves 0-3
+  // stream the weights (and wait for them every step), waves 4-7 stream the
+  // next chunk's halo (and wait for it once per chunk).
+  const int gt = tid & 255;        // thread index inside the half
+  const int gw = wid & 3;          // wave index inside the half
+  int hpix[NHP1];  // (half 1) halo pixel of each halo slot (-1 = zero pad)
+#pragma unroll
+  for (int i = 0; i < NHP1; ++i) {
+    const int P = i * 256 + gt;
+    const int px = P >> 2;
+    const int hy = px / HW, hx = px - (px / HW) * HW;
+    const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+    const bool ok = P < HPIECES && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+    hpix[i] = ok ? (img * H + y) * W + x : -1;
+  }
+  const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
+  const void* zp = (const void*)vu_zero_page4;
+  char* const hbuf = smem;
+  char* const wbuf = smem + 2 * HALO;
+
+  // channel sources (concat inputs) held in registers: no per-chunk kernarg loads
+  const bf16_t* const src0 = reinterpret_cast<const bf16_t*>(g.src[0]);
+  const bf16_t* const src1 = reinterpret_cast<const bf16_t*>(g.src[1]);
+  const bf16_t* const src2 = reinterpret_cast<const bf16_t*>(g.src[2]);
+  const int64_t st0 = g.stride[0], st1 = g.stride[1], st2 = g.stride[2];
+  const int ce0 = g.cend[0], ce1 = g.nsrc > 2 ? g.cend[1] : (1 << 30);
+  // chunk c's source pointer (channel offset applied) and pixel stride
+  auto chunk_src = [&](int c, const bf16_t*& src, int64_t& st) {
+    const int cb = c * 32;
+    if (cb < ce0) {
+      src = src0 + cb;
+      st = st0;
+    } else if (cb < ce1) {
+      src = src1 + (cb - ce0);
+      st = st1;
+    } else {
+      src = src2 + (cb - ce1);
+      st = st2;
+    }
+  };
+  // (half 1) halo slot i of chunk c; the last slot may cover a partial wave
+  auto halo_slot = [&](const bf16_t* src, int64_t st, int c, int i) {
+    if (i * 256 + gw * 64 >= HPIECES) return;  // wave-uniform
+    const int P = i * 256 + gt;
+    if (P < HPIECES) {
+      const void* gp = hpix[i] >= 0 ? (const void*)(src + (int64_t)hpix[i] * st + (P & 3) * 8) : zp;
+      char* dst = hbuf + (c & 1) * HALO + (i * 256 + gw * 64) * 16;
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)dst, 16, 0, 0);
+    }
+  };
+  // (half 0) weight slots [i0, i1) of step s
+  auto wstage = [&](int s, int i0, int i1) {
+    const int c = s / 9, t = s - (s / 9) * 9;
+    const int k0 = t * g.C + c * 32;
+    char* B = wbuf + (s % NBW) * WSLOT;
+#pragma unroll
+    for (int i = 0; i < LB0; ++i) {
+      if (i < i0 || i >= i1) continue;
+      const int P = i * 256 + gt;
+      const int row = P >> 2;
+      const void* gp = XM == 4 ? (const void*)(bmat + ((int64_t)s * p.ncol + n0) * 32 + P * 8)
+                               : (const void*)(bmat + (int64_t)(n0 + row) * p.ldb + k0 + (P & 3) * 8);
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * 256 + gw * 64) * 16), 16, 0, 0);
+    }
+  };
+  auto halo_chunk = [&](int c, int t) {  // (half 1) slots of chunk c issued at chunk step t
+    const bf16_t* src;
+    int64_t st;
+    chunk_src(c, src, st);
+#pragma unroll
+    for (int i = 0; i < NHP1; ++i)
+      if (t < 0 || i / PPS1 == t) halo_slot(src, st, c, i);
+  };
+
+  // ---- fragment addressing -------------------------------------------------
+  int arow[8];  // halo byte offset of this lane's pixel in each A fragment (tap (0,0))
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = wm * 128 + i * 16 + (lane & 15);
+    const int ty = m / TW, tx = m - (m / TW) * TW;
+    arow[i] = (ty * HW + tx) * 64 + (lane >> 4) * 16;
+  }
+  const int brow = (wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  // ---- prologue: halo of chunk 0, weights of steps 0 and 1 -----------------
+  if (grp) {
+    halo_chunk(0, -1);
+  } else {
+    wstage(0, 0, LB0);
+    if (nk > 1) wstage(1, 0, LB0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (grp) pp_barrier();  // the stagger: half 1 runs one barrier behind
+
+  for (int s = 0; s < nk; ++s) {
+    const int c = s / 9, t = s - (s / 9) * 9;
+    const char* A = hbuf + (c & 1) * HALO + ((t / 3) * HW + (t - (t / 3) * 3)) * 64;
+    const char* Bw = wbuf + (s % NBW) * WSLOT;
+    u32x4 bf[4], af[4];
+    // -- phase 1: weights + pixel fragments 0..3; half 0 prefetches weights(s+2)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(Bw + brow + j * 16 * 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[i]);
+    if (!grp && s + 2 < nk) wstage(s + 2, 0, LB0A);
+    pp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+                                                            __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+    // -- phase 2: pixel fragments 4..7; half 0 finishes weights(s+2) and waits
+    //    for weights(s+1); half 1 streams the next chunk's halo and waits for
+    //    it at the chunk's last step
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[4 + i]);
+    if (!grp) {
+      if (s + 2 < nk) {
+        wstage(s + 2, LB0A, LB0);
+        wait_vm(LB0);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else if (c + 1 < nchunk) {
+      if (t * PPS1 < NHP1) halo_chunk(c + 1, t);
+      if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+                                                                __builtin_bit_cast(bf16x8, af[i]), acc[4 + i][j], 0, 0,
+                                                                0);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+  }
+  if (!grp) pp_barrier();  // re-align the halves
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ---- epilogue ---------------------------------------------------------------
+  // acc[i][j][r]: pixel wm*128 + i*16 + (lane&15), channel wn*64 + j*16 + 4*(lane>>4) + r
+  const int cbase = wn * 64 + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float bv = p.bias ? p.bias[n0 + cbase + j * 16 + r] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
+    }
+  }
+  float* red_s = reinterpret_cast<float*>(smem + EPI);
+  float* red_q = red_s + WM * BN;
+  if (p.stat_sum) {
+    // column sums over this wave's 128 pixels: registers, then the 16 lanes
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += acc[i][j][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+        if ((lane & 15) == 0) red_s[wm * BN + cbase + j * 16 + r] = s;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = cbase + j * 16 + r;
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) tot += red_s[w * BN + col];
+        const float mean = tot * (1.f / BM);
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = acc[i][j][r] - mean;
+          q += d * d;
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+        if ((lane & 15) == 0) red_q[wm * BN + col] = q;
+      }
+    __syncthreads();
+    if (tid < BN) {
+      float ts = 0.f, tq = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        ts += red_s[w * BN + tid];
+        tq += red_q[w * BN + tid];
+      }
+      p.stat_sum[(int64_t)mt * p.ncol + n0 + tid] = ts;
+      p.stat_m2[(int64_t)mt * p.ncol + n0 + tid] = tq;
+    }
+  }
+  // bf16 staging: 8-byte writes of 4 consecutive channels of one pixel
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = wm * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u32x2 v;
+      v[0] = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+      v[1] = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+      *reinterpret_cast<u32x2*>(smem + m * ROWB + (cbase + j * 16) * 2) = v;
+    }
+  }
+  __syncthreads();
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  constexpr int CPR = BN / 8;
+#pragma unroll 4
+  for (int e = tid; e < BM * CPR; e += NT) {
+    const int row = e / CPR, cc = e - (e / CPR) * CPR;
+    const int ty = row / TW, tx = row - (row / TW) * TW;
+    const int64_t m = ((int64_t)img * H + y0 + ty) * W + x0 + tx;
+    bf16_t* dst = out + m * p.out_stride + p.out_coff + n0 + cc * 8;
+    Vec8<bf16_t> v;
+    v.v = *reinterpret_cast<const u32x4*>(smem + row * ROWB + cc * 16);
+    if (p.accumulate) {
+      Vec8<bf16_t> o;
+      o.load(dst);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v.set(q, o.get(q) + v.get(q));
+    }
+    v.store(dst);
+  }
+}
+
+int xmode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("VU_V4_XM");
+    m = e ? atoi(e) : 0;
+  }
+  return m;
+}
+
+template <int BN>
+int launch(const VuGemmFwd& p, hipStream_t st) {
+  const VuGather& g = p.a;
+  const int64_t mt = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW);
+  const int64_t nblk = mt * (p.ncol / BN);
+  switch (xmode()) {
+    case 1: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 2>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 3>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    case 4: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 4>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    case 5: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 5>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  }
+  return (int)hipGetLastError();
+}
+
+template <int BN>
+bool tiles_ok(const VuGemmFwd& p) {
+  const VuGather& g = p.a;
+  return p.ncol % BN == 0 && g.H % PP<BN>::TH == 0 && g.W % PP<BN>::TW == 0;
+}
+
+int g_min_blocks = 256;  // vu_gemm_set_tuning(VU_TUNE_V4_MIN_BLOCKS, ...)
+
+// Output-column tile the ping-pong kernel uses for this problem (0 = not served).
+int pick_bn(const VuGemmFwd& p) {
+  const VuGather& g = p.a;
+  const int64_t pix = (int64_t)g.N * g.H * g.W;
+  const int mb = g_min_blocks;
+  // at least ~one block per CU, else the v3 tiles (more, smaller blocks) win
+  if (tiles_ok<256>(p) && (pix / 256) * (p.ncol / 256) >= mb) return 256;
+  if (p.ncol % 256 != 0 && tiles_ok<128>(p) && (pix / 512) * (p.ncol / 128) >= mb) return 128;
+  // 64 x 64 problems (18 K steps) are prologue/epilogue bound at 1 block/CU: v3 wins
+  if (p.ncol == 64 && (g.C > 64 || mb < 256) && tiles_ok<64>(p) && pix / 1024 >= mb) return 64;
+  return 0;
+}
+
+}  // namespace
+
+// Row tile (BM) when the ping-pong kernel serves this problem, else 0: bf16,
+// 3x3 stride-1 pad-1 gather over same-size sources, 32-channel aligned source
+// groups, plain NHWC output with 8-element aligned strides.
+int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype) {
+  const VuGather& g = p.a;
+  if (dtype != VU_BF16 || p.out_mode != 0) return 0;
+  if (g.R != 3 || g.S != 3 || g.sy != 1 || g.sx != 1 || g.dy != 1 || g.dx != 1 || g.oy != -1 ||
+      g.ox != -1 || g.Hs != g.H || g.Ws != g.W)
+    return 0;
+  if (g.C % 32 != 0) return 0;
+  for (int t = 0; t < g.nsrc; ++t)
+    if (g.cend[t] % 32 != 0 || g.stride[t] % 8 != 0) return 0;
+  if (p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0) return 0;
+  if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
+  const int bn = pick_bn(p);
+  return bn == 256 ? 256 : bn == 128 ? 512 : bn == 64 ? 1024 : 0;
+}
+
+int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st) {
+  switch (pick_bn(p)) {
+    case 256: return launch<256>(p, st);
+    case 128: return launch<128>(p, st);
+    case 64: return launch<64>(p, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+extern "C" int vu_gemm_set_tuning(int key, int value) {
+  if (key == VU_TUNE_V4_MIN_BLOCKS) {
+    g_min_blocks = value;
+    return 0;
+  }
+  return (int)hipErrorInvalidValue;
+}
