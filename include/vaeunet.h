@@ -111,6 +111,24 @@ int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1,
                 int64_t s2, int64_t s3, int d0, int d1, int d2, int d3,
                 int d3v, void* out, int dtype, void* stream);
 
+/* Batched vu_permute4 (one launch for all derived weight images of a step).
+ * jobs: device array.  q = the input-fastest dim when it is not dim 3 (the
+ * job is then a batched 2-D transpose in 32x32 tiles: one block per tile,
+ * prod(other dims) * ceil(d_q/32) * ceil(d3/32) blocks), or 3 (streamed,
+ * ceil(numel / vu_permute4_chunk()) blocks).  chunk0 = prefix block count,
+ * nchunks = total blocks. */
+typedef struct VuPermJob {
+  const float* in;
+  int64_t base, s0, s1, s2, s3;
+  int32_t d0, d1, d2, d3, d3v, dtype;
+  void* out;
+  int64_t chunk0;
+  int32_t q, pad_;
+} VuPermJob;
+int64_t vu_permute4_chunk(void);
+int vu_permute4_batch(const VuPermJob* jobs, int njobs, int64_t nchunks,
+                      void* stream);
+
 /* ---- BatchNorm (nn.BatchNorm2d train mode, unet_parts.py:41,44) -------- */
 /* combine per-tile (sum, M2) partials; counts: tile t has
  * min(tile_rows, rows - t*tile_rows) rows.  Writes scale/shift (y*scale+shift

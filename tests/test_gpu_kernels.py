@@ -374,3 +374,24 @@ def test_loss_kernels_vs_oracle():
         assert abs(out.item() - ref.item()) < 1e-5 * max(1.0, abs(ref.item()))
         torch.testing.assert_close(md.grad.cpu(), 2 * m.grad, rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(vd.grad.cpu(), 2 * v.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_permute_batch_matches_single_launches():
+    """engine.refresh_weights: all stale derived weight images rebuilt in one
+    vu_permute4_batch launch equal the one-launch-per-image builds."""
+    K, E = _k()
+    g = torch.Generator().manual_seed(9)
+    ws = [torch.randn(64, 32, 3, 3, generator=g).to(DEV), torch.randn(16, 8, 1, 1, generator=g).to(DEV),
+          torch.randn(32, 16, 2, 2, generator=g).to(DEV),
+          torch.randn(64, 3, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL)]
+    for d in (0, 1):
+        single = [E.w3x3_fwd(ws[0], d), E.w3x3_dgrad(ws[0], d), E.w1x1_fwd(ws[1], d), E.w1x1_dgrad(ws[1], d),
+                  E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8)]
+        single = [t.clone() for t in single]
+        for w in ws:
+            w.mul_(1.0)  # bump the version: every image is stale
+        E.refresh_weights(ws)
+        batched = [E.w3x3_fwd(ws[0], d), E.w3x3_dgrad(ws[0], d), E.w1x1_fwd(ws[1], d), E.w1x1_dgrad(ws[1], d),
+                   E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8)]
+        for a, b in zip(single, batched):
+            assert torch.equal(a, b)

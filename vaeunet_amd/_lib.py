@@ -42,6 +42,13 @@ class VuGemmWgrad(C.Structure):
                 ("splits", C.c_int32), ("m_per_split", _l), ("out", _p)]
 
 
+class VuPermJob(C.Structure):
+    _fields_ = [("inp", _p), ("base", _l), ("s0", _l), ("s1", _l), ("s2", _l), ("s3", _l),
+                ("d0", C.c_int32), ("d1", C.c_int32), ("d2", C.c_int32), ("d3", C.c_int32),
+                ("d3v", C.c_int32), ("dtype", C.c_int32), ("out", _p), ("chunk0", _l),
+                ("q", C.c_int32), ("pad_", C.c_int32)]
+
+
 class VuMtEntry(C.Structure):
     _fields_ = [("param", _p), ("grad", _p), ("exp_avg", _p), ("exp_avg_sq", _p),
                 ("numel", _l), ("chunk0", _l), ("step_size", _f), ("bc2_sqrt", _f)]
@@ -55,6 +62,8 @@ _SIGS = {
     "vu_gemm_wgrad_tile": (_i, [C.POINTER(VuGemmWgrad), _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vu_gemm_set_tuning": (_i, [_i, _i]),
     "vu_slab_reduce": (_i, [_p, _i, _i, _i, _i, _i, _l, _l, _l, _p, _i, _p]),
+    "vu_permute4_chunk": (_l, []),
+    "vu_permute4_batch": (_i, [_p, _i, _l, _p]),
     "vu_permute4": (_i, [_p, _l, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),
     "vu_bn_finalize": (_i, [_p, _p, _i, _l, _l, _i, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p,
                             _p, _p, _p]),

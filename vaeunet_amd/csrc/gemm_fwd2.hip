@@ -22,6 +22,7 @@
 //     pixel shuffle, out_mode 2 a stride-2 parity lattice.
 #include "common.h"
 #include "../../include/vaeunet.h"
+#include <stdlib.h>
 
 static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page[16];  // 16 B of zeros: padding lanes DMA from here
 
@@ -268,6 +269,19 @@ int launch_ns(const VuGemmFwd& p, hipStream_t st) {
   return launch<BM, BN, WM, WN, 3>(p, st);
 }
 
+// Tile configuration for short-K problems (<= 2 K steps of 64), where a
+// block's life is dominated by its load latency and epilogue: 0 = 256-row
+// tiles, 1 = 128-row tiles (8 waves), 2 = 128-row tiles (4 waves).
+int v2_cfg(const VuGemmFwd& p) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VU_V2_CFG");
+    mode = e ? atoi(e) : 0;
+  }
+  const int nk = (p.a.R * p.a.S * p.a.C + 63) / 64;
+  return nk <= 2 ? mode : 0;
+}
+
 }  // namespace
 
 // Row tile of the v2 kernel for this problem, or 0 when v2 does not apply
@@ -293,10 +307,19 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
   int bn = p.ncol <= 64 ? 64 : 128;
   int64_t tiles = ((M + 255) / 256) * ((p.ncol + bn - 1) / bn);
   if (tiles < 256) return 0;
-  return 256;
+  return v2_cfg(p) ? 128 : 256;
 }
 
 int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st) {
-  if (p.ncol <= 64) return launch_ns<256, 64, 8, 1>(p, st);
-  return launch_ns<256, 128, 4, 2>(p, st);
+  switch (v2_cfg(p)) {
+    case 1:
+      if (p.ncol <= 64) return launch_ns<128, 64, 4, 2>(p, st);
+      return launch_ns<128, 128, 2, 4>(p, st);
+    case 2:
+      if (p.ncol <= 64) return launch_ns<128, 64, 2, 2>(p, st);
+      return launch_ns<128, 128, 2, 2>(p, st);
+    default:
+      if (p.ncol <= 64) return launch_ns<256, 64, 8, 1>(p, st);
+      return launch_ns<256, 128, 4, 2>(p, st);
+  }
 }

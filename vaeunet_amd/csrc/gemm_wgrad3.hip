@@ -23,6 +23,7 @@
 //     a fixed order: deterministic).
 #include "common.h"
 #include "../../include/vaeunet.h"
+#include <stdlib.h>
 
 static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page_w3[16];
 
@@ -53,7 +54,9 @@ VU_DEV u32x4 tr_frag(const char* base, int off_lo, int off_hi) {
   return u32x4{l2[0], l2[1], h2[0], h2[1]};
 }
 
-template <int BI>
+// XM: experiment mode for timing studies (0 in production): 1 = no DMA after
+// the first tile, 2 = no MFMA.
+template <int BI, int XM>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   constexpr int NT = 512;
   constexpr int RBP = BI * 2, CPI = BI / 8;
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
+    if (XM != 1 && st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
     const char* Pb = smem + (st & 1) * STAGE;
     const char* Qb = Pb + PB;
 #pragma unroll
@@ -189,9 +192,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
           for (int a = 0; a < TI; ++a)
 #pragma unroll
             for (int b = 0; b < TJ; ++b)
-              acc[a][b][r * 3 + s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              if (XM != 2) acc[a][b][r * 3 + s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b][r * 3 + s], 0, 0, 0);
           __builtin_amdgcn_s_setprio(0);
+          if (XM == 2) asm volatile("" ::"v"(bf[0]), "v"(af[0]));
         }
     }
   }
@@ -212,11 +216,24 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       }
 }
 
+int xmode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("VU_W3_XM");
+    m = e ? atoi(e) : 0;
+  }
+  return m;
+}
+
 template <int BI>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int64_t nblk = (int64_t)((p.ni + BI - 1) / BI) * (p.q.C / 64) * p.splits;
   if (nblk <= 0) return 0;
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  switch (xmode()) {
+    case 1: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 2>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
+    default: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 0>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  }
   return (int)hipGetLastError();
 }
 

@@ -386,6 +386,87 @@ extern "C" int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1
   return (int)hipGetLastError();
 }
 
+// Batched vu_permute4: every derived weight layout of a training step in one
+// launch (the per-step rebuild of the bf16 GEMM weight images after the
+// optimizer step, engine.py weight caches).  A job whose output-fastest dim
+// (3) is not the input-fastest one (e.g. the flipped [ci][tap][co] input-
+// gradient images: co is the slowest input dim) is a batched 2-D transpose:
+// 32x32 tiles through LDS, coalesced reads along the input-fast dim q and
+// coalesced writes along dim 3.  Other jobs are streamed PERM_CHUNK elements
+// per block.  chunk0 is the prefix block count (binary search per block).
+namespace {
+constexpr int PERM_CHUNK = 4096;
+__global__ void permute4_batch_kernel(const VuPermJob* jobs, int n) {
+  __shared__ float tile[32][33];
+  const int64_t chunk = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].chunk0 <= chunk) lo = mid; else hi = mid - 1;
+  }
+  const VuPermJob& j = jobs[lo];
+  // 32-bit index math (every weight image has < 2^31 elements)
+  const int d[4] = {j.d0, j.d1, j.d2, j.d3};
+  const int st[4] = {(int)j.s0, (int)j.s1, (int)j.s2, (int)j.s3};
+  const float* in = j.in + j.base;
+  const uint32_t blk = (uint32_t)(chunk - j.chunk0);
+  auto put = [&](uint32_t e, float v) {
+    if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
+    else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
+  };
+  if (j.q >= 3) {
+    const uint32_t d1 = d[1], d2 = d[2], d3 = d[3];
+    const uint32_t tot = (uint32_t)d[0] * d1 * d2 * d3;
+    const uint32_t e0 = blk * PERM_CHUNK;
+    const uint32_t e1 = e0 + PERM_CHUNK < tot ? e0 + PERM_CHUNK : tot;
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
+      const uint32_t r = e / d3, i3 = e - r * d3;
+      const uint32_t r2 = r / d2, i2 = r - r2 * d2;
+      const uint32_t i0 = r2 / d1, i1 = r2 - i0 * d1;
+      put(e, (int)i3 < j.d3v ? in[(int)i0 * st[0] + (int)i1 * st[1] + (int)i2 * st[2] + (int)i3 * st[3]] : 0.f);
+    }
+    return;
+  }
+  // tiled transpose between dim q (input-fast) and dim 3 (output-fast)
+  const int q = j.q;
+  const int a = q == 0 ? 1 : 0, c = q == 2 ? 1 : 2;  // the two batch dims, in order
+  const uint32_t tq = (d[q] + 31) / 32, t3 = (d[3] + 31) / 32;
+  const uint32_t b = blk / (tq * t3), rem = blk - b * (tq * t3);
+  const int iq0 = (int)(rem / t3) * 32, i30 = (int)(rem - (rem / t3) * t3) * 32;
+  const int ia = (int)(b / d[c]), ic = (int)(b - (b / d[c]) * d[c]);
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* ib = in + ia * st[a] + ic * st[c];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int iq = iq0 + tx, i3 = i30 + ty + 8 * k;
+    float v = 0.f;
+    if (iq < d[q] && i3 < d[3] && i3 < j.d3v) v = ib[iq * st[q] + i3 * st[3]];
+    tile[ty + 8 * k][tx] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i3 = i30 + tx, iq = iq0 + ty + 8 * k;
+    if (iq >= d[q] || i3 >= d[3]) continue;
+    int idx[4];
+    idx[a] = ia;
+    idx[c] = ic;
+    idx[q] = iq;
+    idx[3] = i3;
+    const uint32_t e = (((uint32_t)idx[0] * d[1] + idx[1]) * d[2] + idx[2]) * d[3] + i3;
+    put(e, tile[tx][ty + 8 * k]);
+  }
+}
+}  // namespace
+
+extern "C" int64_t vu_permute4_chunk(void) { return PERM_CHUNK; }
+
+extern "C" int vu_permute4_batch(const VuPermJob* jobs, int njobs, int64_t nchunks, void* stream) {
+  if (njobs <= 0 || nchunks <= 0) return 0;
+  hipLaunchKernelGGL(permute4_batch_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, jobs, njobs);
+  return (int)hipGetLastError();
+}
+
 extern "C" int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys, int ydtype, int64_t P, int C,
                        int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;

@@ -55,12 +55,34 @@ def current_mode(device, grad_ready=None):
 # ----------------------------------------------------------------------------
 def _cached(p, key, build):
     cache = p.__dict__.setdefault("_vu_cache", {})
+    p.__dict__.setdefault("_vu_build", {})[key] = build
     ent = cache.get(key)
     ver = (p._version, p.data_ptr())
     if ent is None or ent[0] != ver:
         ent = (ver, build())
         cache[key] = ent
     return ent[1]
+
+
+def refresh_weights(params):
+    """Rebuild every stale derived weight image of ``params`` (those built in
+    earlier steps, i.e. after an optimizer step bumped the version) in ONE
+    batched launch, instead of one permute launch per image mid-step."""
+    stale = []
+    for p in params:
+        builders = p.__dict__.get("_vu_build")
+        if not builders:
+            continue
+        cache = p.__dict__["_vu_cache"]
+        ver = (p._version, p.data_ptr())
+        for key, build in builders.items():
+            ent = cache.get(key)
+            if ent is None or ent[0] != ver:
+                stale.append((cache, key, build, ver))
+    if stale:
+        with K.permute_batch():
+            for cache, key, build, ver in stale:
+                cache[key] = (ver, build())
 
 
 def w3x3_fwd(w, d, cin_pad=None):

@@ -218,11 +218,68 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
     return slab
 
 
+_PBATCH = None  # job list while a permute_batch() context is open
+
+
 def permute4(src, base, strides, dims, d3v, dtype):
+    """out[i0][i1][i2][i3] = src[base + sum i*s] (0 for i3 >= d3v), in the
+    storage dtype.  Inside permute_batch() the launch is deferred and merged."""
     out = torch.empty(dims, dtype=torch.bfloat16 if dtype == _lib.BF16 else torch.float32,
                       device=src.device)
+    if _PBATCH is not None:
+        _PBATCH.append((src, base, strides, dims, d3v, out, dtype))
+        return out
     call("vu_permute4", ptr(src), base, *strides, *dims, d3v, ptr(out), dtype, stream())
     return out
+
+
+class permute_batch:
+    """Context: every permute4 issued inside becomes one vu_permute4_batch
+    launch at exit (the outputs are filled before any later launch on the
+    stream reads them)."""
+
+    def __enter__(self):
+        global _PBATCH
+        self.outer = _PBATCH is not None
+        if not self.outer:
+            _PBATCH = []
+        return self
+
+    def __exit__(self, *exc):
+        global _PBATCH
+        if self.outer:
+            return False
+        jobs, _PBATCH = _PBATCH, None
+        if not jobs or exc[0] is not None:
+            return False
+        chunk = query("vu_permute4_chunk")
+        arr = (_lib.VuPermJob * len(jobs))()
+        c0 = 0
+        for i, (src, base, strides, dims, d3v, out, dtype) in enumerate(jobs):
+            e = arr[i]
+            e.inp = src.data_ptr()
+            e.base = base
+            e.s0, e.s1, e.s2, e.s3 = strides
+            e.d0, e.d1, e.d2, e.d3 = dims
+            e.d3v, e.dtype = d3v, dtype
+            e.out = out.data_ptr()
+            e.chunk0 = c0
+            # input-fastest dim (among those of extent > 1); a transpose if not dim 3
+            cand = [k for k in range(4) if dims[k] > 1] or [3]
+            q = min(cand, key=lambda k: (abs(strides[k]), k != cand[-1]))
+            if q == cand[-1] or dims[3] == 1:
+                q = 3  # output-fast == input-fast: stream
+            e.q = q
+            if q == 3:
+                c0 += -(-out.numel() // chunk)
+            else:
+                a, cc = [k for k in range(3) if k != q]
+                c0 += dims[a] * dims[cc] * (-(-dims[q] // 32)) * (-(-dims[3] // 32))
+        dev = jobs[0][5].device
+        host = torch.frombuffer(bytearray(arr), dtype=torch.uint8).pin_memory()
+        table = host.to(dev, non_blocking=True)
+        call("vu_permute4_batch", ptr(table), len(jobs), c0, stream())
+        return False
 
 
 def bn_finalize(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps):

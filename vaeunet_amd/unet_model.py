@@ -66,6 +66,7 @@ class UNet(nn.Module):
 
     def forward(self, x):
         M = E.current_mode(x.device, self.grad_ready)
+        E.refresh_weights(self.parameters())
         params = [p for p in self.parameters() if p.requires_grad]
         if not (torch.is_grad_enabled() and (params or x.requires_grad)):
             return self._fwd(M, x)[0]

@@ -212,6 +212,7 @@ class UNetResNet(nn.Module):
 
     def forward(self, x):
         M = E.current_mode(x.device, self.grad_ready)
+        E.refresh_weights(self.parameters())
         eps = self._eps(x.shape[0], x.device)
         params = [p for p in self.parameters() if p.requires_grad]
         if not (torch.is_grad_enabled() and (params or x.requires_grad)):
