@@ -96,11 +96,60 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
                    int cvalid, int64_t s_i, int64_t s_tap, int64_t s_c,
                    float* out, int accumulate, void* stream);
 
-/* Dispatcher tuning (tests / experiments).  VU_TUNE_V4_MIN_BLOCKS: smallest
- * grid for which the ping-pong 3x3 kernel (gemm_fwd4.hip) is used (default
- * 256 = one block per CU); 0 forces it wherever its tiles fit. */
+/* Dispatcher tuning (tests / experiments):
+ *   VU_TUNE_V4_MIN_BLOCKS: smallest grid for which the ping-pong 3x3 kernel
+ *     (gemm_fwd4.hip) is used (default 256 = one block per CU; 0 forces it);
+ *   VU_TUNE_V5_MAX_C: widest input (channels) the persistent 3x3 kernel
+ *     (gemm_fwd5.hip) serves (default 0 = disabled: no net gain measured);
+ *   VU_TUNE_V5_MIN_TILES: fewest tiles for which it is used (default -1 =
+ *     2 x CU count; 0 forces it);
+ *   VU_TUNE_V5_GRID / VU_TUNE_FP8_GRID: cap on the grid of the persistent
+ *     bf16 / fp8 kernels (default 0 = CU count; tests use small caps so that
+ *     every block walks several tiles). */
 #define VU_TUNE_V4_MIN_BLOCKS 0
+#define VU_TUNE_V5_MAX_C 1
+#define VU_TUNE_V5_MIN_TILES 2
+#define VU_TUNE_V5_GRID 3
+#define VU_TUNE_FP8_GRID 4
 int vu_gemm_set_tuning(int key, int value);
+
+/* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */
+/* *amax (= or max=) max |x| over P pixels x C channels (C % 8 == 0); exact
+ * and order-independent (integer max of the float bits) */
+int vu_amax(const void* x, int64_t xs, int64_t P, int C, float* amax,
+            int accumulate, int dtype, void* stream);
+/* y = e4m3(clamp(x * s, +-448)) round-to-nearest-even, s = 448 / *amax (1 if
+ * *amax == 0); *dq = 1/s, the dequantisation scale (dq may be NULL) */
+int vu_quant_fp8(const void* x, int64_t xs, int64_t P, int C,
+                 const float* amax, uint8_t* y, int64_t ys, float* dq,
+                 int dtype, void* stream);
+/* per-row version for weights: fp32 [rows][cols] -> e4m3 [rows][ldy] (zero
+ * padded), dq[r] = 1/s_r with s_r = 448 / max_k |x[r][k]| */
+int vu_quant_rows_fp8(const float* x, int rows, int64_t cols, uint8_t* y,
+                      int64_t ldy, float* dq, void* stream);
+/* out[m][co] = x_scale[0] * w_scale[co] * sum_k xq[m][k] wq[co][k]
+ *              (+ bias[co]), bf16 NHWC at out[m*out_stride + out_coff + co].
+ * a: 3x3 stride-1 pad-1 gather over 1-3 e4m3 NHWC sources (64-channel
+ * aligned, pixel strides multiple of 16); wq: e4m3 [ncol][ldw], k = tap*C +
+ * c (conv weights [Cout][Cin][r][s] in (r, s, c) order).  stat_sum/stat_m2
+ * (optional) as in VuGemmFwd with the row tile vu_conv3x3_fp8_row_tile. */
+typedef struct VuConvFp8 {
+  VuGather a;
+  const void* w;
+  int64_t ldw;
+  int32_t ncol;
+  int32_t out_coff;
+  const float* x_scale;
+  const float* w_scale;
+  const float* bias;
+  void* out;
+  int64_t out_stride;
+  float* stat_sum;
+  float* stat_m2;
+} VuConvFp8;
+/* 128 when the kernel serves this problem, else 0 */
+int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args);
+int vu_conv3x3_fp8(const VuConvFp8* args, void* stream);
 
 /* ---- weights ----------------------------------------------------------- */
 /* out[i0][i1][i2][i3] (contiguous) = in[base + i0*s0 + i1*s1 + i2*s2 + i3*s3]

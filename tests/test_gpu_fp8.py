@@ -1,0 +1,139 @@
+"""fp8 (OCP e4m3fn) 3x3 conv path (BASELINE.json configs[4], csrc/conv_fp8.hip).
+
+* the quantisers are bit-exact against torch.float8_e4m3fn (same fp32 scale,
+  same clamp, round-to-nearest-even);
+* the conv equals fp32 convolution of the DEQUANTISED operands (e4m3 products
+  are exact in fp32; only the summation order and the bf16 output rounding
+  differ), with BN partial statistics, bias, channel-slice output, 1-3
+  concat sources and blocks that walk several tiles (grid cap);
+* the error against the unquantised fp32 conv is only reported (the
+  reference has no fp8 path) and loosely bounded here.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+CL = torch.channels_last
+TUNE_FP8_GRID = 4
+
+
+def _act(t, dtype=torch.bfloat16):
+    return t.to(DEV, dtype).contiguous(memory_format=CL)
+
+
+def _bytes(q):
+    return q.cpu().contiguous().view(torch.uint8)
+
+
+def test_quantize_bit_exact():
+    from vaeunet_amd import fp8
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 64, 8, 16, generator=g) * 3
+    x[0, :4, 0, 0] = torch.tensor([0.0, -0.0, 1e-3, -7.5])   # zeros, an e4m3-subnormal value
+    for dtype in (torch.bfloat16, torch.float32):
+        xd = _act(x, dtype)
+        am = fp8.amax([xd])
+        assert am.item() == xd.float().abs().max().item()
+        q, dq = fp8.quantize(xd, am)
+        s = torch.tensor(448.0, dtype=torch.float32) / am.cpu()
+        qr = (xd.float().cpu() * s).clamp(-448, 448).to(torch.float8_e4m3fn)
+        assert torch.equal(_bytes(q), _bytes(qr))
+        assert dq.item() == (1.0 / s).item()
+
+
+def test_quantize_rows_bit_exact():
+    from vaeunet_amd import fp8
+    g = torch.Generator().manual_seed(1)
+    m = torch.randn(48, 576, generator=g)
+    m[3] = 0.0                                                 # all-zero row: scale 1
+    q, dq = fp8.quantize_rows(m.to(DEV))
+    s = torch.tensor(448.0) / m.abs().amax(1)
+    s[3] = 1.0
+    qr = (m * s[:, None]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(_bytes(q), _bytes(qr))
+    assert torch.equal(dq.cpu(), 1.0 / s)
+
+
+FP8_CASES = [
+    # (N, [cin per source], H, W, cout, grid cap)
+    (1, [64], 8, 32, 256, 0),           # 256x256 tiles, one tile
+    (2, [64], 16, 64, 256, 3),          # 8 tiles over 3 blocks
+    (1, [64, 64], 16, 32, 384, 2),      # two sources, 512x128 tiles, 3 column tiles
+    (2, [128], 32, 32, 128, 3),
+    (2, [64], 32, 64, 64, 3),           # 1024x64 tiles
+    (3, [64, 64, 64], 32, 32, 64, 2),   # three sources, odd chunk count
+]
+
+
+@pytest.mark.parametrize("case", FP8_CASES)
+def test_conv3x3_fp8(case):
+    from vaeunet_amd import _lib, fp8
+    N, cins, H, W, co, cap = case
+    g = torch.Generator().manual_seed(7)
+    xs = [torch.randn(N, c, H, W, generator=g) for c in cins]
+    cin = sum(cins)
+    w = torch.randn(co, cin, 3, 3, generator=g) / (3 * cin ** 0.5)
+    b = torch.randn(co, generator=g)
+    _lib.call("vu_gemm_set_tuning", TUNE_FP8_GRID, cap)
+    try:
+        srcs = [_act(x) for x in xs]
+        am = fp8.amax(srcs)
+        qs, dq = [], None
+        for t in srcs:
+            q, dq = fp8.quantize(t, am)
+            qs.append(q)
+        wq, ws = fp8.quantize_weight(w.to(DEV))
+        out, st = fp8.conv3x3(qs, dq, wq, ws, co, bias=b.to(DEV), stats=True)
+        # fp32 conv of the dequantised operands
+        xd = torch.cat([q.cpu().float() for q in qs], 1) * dq.item()
+        wd = (wq.cpu().float() * ws.cpu()[:, None]).view(co, 3, 3, cin).permute(0, 3, 1, 2)
+        ref = F.conv2d(xd, wd, b, padding=1)
+        got = out.float().cpu()
+        err = (got - ref).abs()
+        bound = 2.0 ** -8 * ref.abs() + 1e-5 * ref.abs().max()
+        assert (err <= bound).all(), (f"max err {err.max().item():.3e}, "
+                                      f"{int((err > bound).sum())} elements off")
+        # BN partials of the stored bf16 values
+        n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                         dtype=torch.float64)
+        s = st.psum.double().cpu()
+        mean = s.sum(0) / n.sum()
+        m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+        torch.testing.assert_close(mean.float(), got.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close((m2.sum(0) / n.sum()).float(), got.var((0, 2, 3), unbiased=False),
+                                   rtol=1e-4, atol=1e-5)
+        # channel-slice output of a wider tensor
+        wide = torch.zeros(N, co + 64, H, W, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=CL)
+        fp8.conv3x3(qs, dq, wq, ws, co, out=wide, out_coff=64, bias=b.to(DEV))
+        assert torch.equal(wide[:, 64:].float().cpu(), got)
+        assert not wide[:, :64].any()
+        # reported: error vs the unquantised conv (loose bound only)
+        full = F.conv2d(torch.cat([x.bfloat16().float() for x in xs], 1), w, b, padding=1)
+        rel = ((got - full).abs().max() / full.abs().max()).item()
+        assert rel < 0.1, rel
+    finally:
+        _lib.call("vu_gemm_set_tuning", TUNE_FP8_GRID, 0)
+
+
+def test_fp8_rejects_unserved_shapes():
+    from vaeunet_amd import fp8
+    x = _act(torch.randn(1, 32, 8, 32))          # 32 channels: not a whole 64-channel chunk
+    w = torch.randn(64, 32, 3, 3, device=DEV)
+    with pytest.raises(ValueError):
+        fp8.conv3x3_q([x], w)
+
+
+def test_double_conv_fp8_close_to_bf16_path():
+    """DoubleConv forward with fp8 convs vs the bf16 path (train-mode BN)."""
+    from vaeunet_amd import DoubleConv, fp8
+    torch.manual_seed(3)
+    mod = DoubleConv(64, 64).to(DEV)
+    x = _act(torch.randn(2, 64, 32, 64))
+    y8 = fp8.double_conv_forward(mod, x).float()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = mod(x).float()
+    rel = ((y8 - yb).abs().max() / yb.abs().max()).item()
+    assert rel < 0.15, rel

@@ -118,14 +118,31 @@ V4_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", V4_CASES)
-def test_conv3x3_pingpong_kernel(case):
-    """bf16 ping-pong halo kernel forced onto small problems (the production
-    dispatcher only picks it for >= 256 blocks): forward with BN statistics,
-    bias, accumulate into a channel slice, and the flipped-weight input grad."""
+V5_CASES = [
+    # (N, [cin per source], H, W, cout, grid cap): persistent kernel (gemm_fwd5.hip)
+    # with the grid capped so that blocks walk several tiles
+    (2, [64], 32, 64, 64, 3),           # 1024x64 tiles: 4 tiles over 3 blocks
+    (1, [64], 16, 64, 256, 3),          # 256x256 tiles: 4 tiles
+    (1, [64], 16, 32, 384, 2),          # 512x128 tiles, 3 column tiles: n0 changes along a walk
+    (2, [32, 32, 64], 16, 32, 128, 1),  # three sources, one block walks both tiles
+    (3, [96], 32, 32, 64, 2),           # odd chunk count: the halo buffer parity flips per tile
+]
+
+TUNE_V4_MIN_BLOCKS, TUNE_V5_MAX_C, TUNE_V5_MIN_TILES, TUNE_V5_GRID = 0, 1, 2, 3
+TUNE_DEFAULTS = ((TUNE_V4_MIN_BLOCKS, 256), (TUNE_V5_MAX_C, 0), (TUNE_V5_MIN_TILES, -1), (TUNE_V5_GRID, 0))
+
+
+def _tune(*kv):
     from vaeunet_amd import _lib
+    for k, v in kv:
+        _lib.call("vu_gemm_set_tuning", k, v)
+
+
+def _check_halo_conv(case, row_tiles):
+    """forward with BN statistics, bias, accumulate into a channel slice, and
+    the flipped-weight input grad, on whatever halo kernel the tuning forces."""
     K, E = _k()
-    N, cins, H, W, co = case
+    N, cins, H, W, co = case[:5]
     g = torch.Generator().manual_seed(5)
     xs = [torch.randn(N, c, H, W, generator=g).to(torch.bfloat16).float() for c in cins]
     cin = sum(cins)
@@ -133,39 +150,58 @@ def test_conv3x3_pingpong_kernel(case):
     wq = w.to(torch.bfloat16).float()
     b = torch.randn(co, generator=g)
     d = _code("bf16")
-    _lib.call("vu_gemm_set_tuning", 0, 0)
+    srcs = [_act(x, "bf16") for x in xs]
+    out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
+    assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, srcs, E.w3x3_fwd(w.to(DEV), d), co, out)) in row_tiles
+    st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, out, d, stats=True)
+    ref = F.conv2d(torch.cat(xs, 1), wq, padding=1)
+    _close(out, ref, "bf16", what="fwd")
+    stored = out.float().cpu()
+    n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                     dtype=torch.float64)
+    s = st.psum.double().cpu()
+    mean = s.sum(0) / n.sum()
+    m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+    torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close((m2.sum(0) / n.sum()).float(), stored.var((0, 2, 3), unbiased=False),
+                               rtol=1e-4, atol=1e-5)
+    # bias + accumulate into the upper channel slice of a wider tensor
+    base = torch.randn(N, co + 64, H, W, generator=g).to(torch.bfloat16).float()
+    wide = _act(base, "bf16")
+    K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, wide, d, out_coff=64,
+               bias=b.to(DEV), accumulate=True)
+    exp = base.clone()
+    exp[:, 64:] += ref + b[None, :, None, None]
+    _close(wide, exp, "bf16", what="bias+accumulate")
+    # input gradient (flipped weights) when cin is a tile width
+    if cin in (64, 128, 256) and co % 32 == 0:
+        dy = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
+        dx = K.empty_act(N, cin, H, W, torch.bfloat16, DEV)
+        K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), cin, dx, d)
+        _close(dx, torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1), "bf16", what="dgrad")
+
+
+@pytest.mark.parametrize("case", V4_CASES)
+def test_conv3x3_pingpong_kernel(case):
+    """bf16 ping-pong halo kernel (gemm_fwd4.hip) forced onto small problems
+    (the production dispatcher only picks it for >= 256 blocks)."""
+    _tune((TUNE_V5_MAX_C, 0), (TUNE_V4_MIN_BLOCKS, 0))
     try:
-        srcs = [_act(x, "bf16") for x in xs]
-        out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
-        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, srcs, E.w3x3_fwd(w.to(DEV), d), co, out)) in (256, 512, 1024)
-        st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, out, d, stats=True)
-        ref = F.conv2d(torch.cat(xs, 1), wq, padding=1)
-        _close(out, ref, "bf16", what="fwd")
-        stored = out.float().cpu()
-        n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
-                         dtype=torch.float64)
-        s = st.psum.double().cpu()
-        mean = s.sum(0) / n.sum()
-        m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
-        torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
-        torch.testing.assert_close((m2.sum(0) / n.sum()).float(), stored.var((0, 2, 3), unbiased=False),
-                                   rtol=1e-4, atol=1e-5)
-        # bias + accumulate into the upper channel slice of a wider tensor
-        base = torch.randn(N, co + 64, H, W, generator=g).to(torch.bfloat16).float()
-        wide = _act(base, "bf16")
-        K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, wide, d, out_coff=64,
-                   bias=b.to(DEV), accumulate=True)
-        exp = base.clone()
-        exp[:, 64:] += ref + b[None, :, None, None]
-        _close(wide, exp, "bf16", what="bias+accumulate")
-        # input gradient (flipped weights) when cin is a tile width
-        if cin in (64, 128, 256) and co % 32 == 0:
-            dy = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
-            dx = K.empty_act(N, cin, H, W, torch.bfloat16, DEV)
-            K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), cin, dx, d)
-            _close(dx, torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1), "bf16", what="dgrad")
+        _check_halo_conv(case, (128,))
     finally:
-        _lib.call("vu_gemm_set_tuning", 0, 256)
+        _tune(*TUNE_DEFAULTS)
+
+
+@pytest.mark.parametrize("case", V5_CASES)
+def test_conv3x3_persistent_kernel(case):
+    """persistent ping-pong kernel (gemm_fwd5.hip): blocks walk several tiles,
+    halos and weights prefetched across tile boundaries, register epilogue
+    (bias, accumulate, BN partials per 128-pixel wave tile)."""
+    _tune((TUNE_V5_MAX_C, 1 << 20), (TUNE_V5_MIN_TILES, 0), (TUNE_V5_GRID, case[5]))
+    try:
+        _check_halo_conv(case, (128,))
+    finally:
+        _tune(*TUNE_DEFAULTS)
 
 
 def _row_tile_args(K, srcs, wmat, ncol, out):

@@ -50,7 +50,11 @@ def main():
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tune", default="", help="KEY=VAL,... for vu_gemm_set_tuning (include/vaeunet.h)")
     args = ap.parse_args()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(k), int(v))
     kinds = args.only.split(",")
     dev = torch.device("cuda")
     torch.manual_seed(0)

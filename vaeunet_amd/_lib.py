@@ -42,6 +42,12 @@ class VuGemmWgrad(C.Structure):
                 ("splits", C.c_int32), ("m_per_split", _l), ("out", _p)]
 
 
+class VuConvFp8(C.Structure):
+    _fields_ = [("a", VuGather), ("w", _p), ("ldw", _l), ("ncol", C.c_int32), ("out_coff", C.c_int32),
+                ("x_scale", _p), ("w_scale", _p), ("bias", _p), ("out", _p), ("out_stride", _l),
+                ("stat_sum", _p), ("stat_m2", _p)]
+
+
 class VuPermJob(C.Structure):
     _fields_ = [("inp", _p), ("base", _l), ("s0", _l), ("s1", _l), ("s2", _l), ("s3", _l),
                 ("d0", C.c_int32), ("d1", C.c_int32), ("d2", C.c_int32), ("d3", C.c_int32),
@@ -62,6 +68,11 @@ _SIGS = {
     "vu_gemm_wgrad_tile": (_i, [C.POINTER(VuGemmWgrad), _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vu_gemm_set_tuning": (_i, [_i, _i]),
     "vu_slab_reduce": (_i, [_p, _i, _i, _i, _i, _i, _l, _l, _l, _p, _i, _p]),
+    "vu_amax": (_i, [_p, _l, _l, _i, _p, _i, _i, _p]),
+    "vu_quant_fp8": (_i, [_p, _l, _l, _i, _p, _p, _l, _p, _i, _p]),
+    "vu_quant_rows_fp8": (_i, [_p, _i, _l, _p, _l, _p, _p]),
+    "vu_conv3x3_fp8_row_tile": (_l, [C.POINTER(VuConvFp8)]),
+    "vu_conv3x3_fp8": (_i, [C.POINTER(VuConvFp8), _p]),
     "vu_permute4_chunk": (_l, []),
     "vu_permute4_batch": (_i, [_p, _i, _l, _p]),
     "vu_permute4": (_i, [_p, _l, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),

@@ -327,6 +327,8 @@ int gemm_fwd_v3_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st);
 
 static bool use_v2(int dtype) {
   static int mode = -1;
@@ -357,7 +359,9 @@ static bool use_v4(int dtype) {
 
 extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
   if (use_v4(dtype)) {
-    int bm = gemm_fwd_v4_bm(*args, dtype);
+    int bm = gemm_fwd_v5_bm(*args, dtype);
+    if (bm) return bm;
+    bm = gemm_fwd_v4_bm(*args, dtype);
     if (bm) return bm;
   }
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 256;
@@ -376,6 +380,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
     if (g.cend[t] % epc != 0 || g.stride[t] % epc != 0) return (int)hipErrorInvalidValue;
   if ((args->ldb % epc) != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (use_v4(dtype) && gemm_fwd_v5_bm(*args, dtype)) return gemm_fwd_v5_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);

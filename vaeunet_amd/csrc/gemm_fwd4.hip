@@ -28,7 +28,7 @@
 //     consecutive output channels of one pixel, which makes the BatchNorm
 //     partial statistics a register + 16-lane reduction and the bf16 output
 //     staging 8-byte LDS writes;
-//   * epilogue: bias, storage rounding, per-tile (sum, centered M2) of the
+//   * epilogue: bias, storage rounding, per-wave (sum, centered M2) of the
 //     rounded values (same contract as v1-v3), 16-byte NHWC stores.
 #include "common.h"
 #include "../../include/vaeunet.h"
@@ -68,6 +68,13 @@ VU_DEV void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// sum over the 16 lanes of a DPP row (every lane receives the total)
+template <int R>
+VU_DEV float ror_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xf, 0xf, false));
+}
+VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
+
 // XM (experiment mode, timing studies only; 0 in production): 1 = no DMA in
 // the main loop, 2 = no DMA and no barriers in the main loop, 3 = no MFMA.
 template <int BN, int XM>
@@ -89,8 +96,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int MAIN = 2 * HALO + NBW * WSLOT;
   constexpr int ROWB = BN * 2 + 16;               // bf16 staging row (padded)
   constexpr int EPI = BM * ROWB;
-  constexpr int RED = 2 * WM * BN * 4;
-  constexpr int LDS_BYTES = MAIN > EPI + RED ? MAIN : EPI + RED;
+  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
   static_assert(LDS_BYTES <= 163840, "LDS");
   static_assert(NHP1 <= 8 * PPS1 && LB0 >= 1, "DMA schedule");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -283,52 +289,31 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
     }
   }
-  float* red_s = reinterpret_cast<float*>(smem + EPI);
-  float* red_q = red_s + WM * BN;
   if (p.stat_sum) {
-    // column sums over this wave's 128 pixels: registers, then the 16 lanes
+    // per-wave statistics tile: its 128 pixels (8 fragments x one 16-lane DPP
+    // row), two-pass (sum, centered M2); no block barrier, no LDS
+    const int64_t so = (int64_t)(mt * WM + wm) * p.ncol + n0 + cbase;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = 0.f;
+        float sv = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s += acc[i][j][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
-        if ((lane & 15) == 0) red_s[wm * BN + cbase + j * 16 + r] = s;
-      }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = cbase + j * 16 + r;
-        float tot = 0.f;
-#pragma unroll
-        for (int w = 0; w < WM; ++w) tot += red_s[w * BN + col];
-        const float mean = tot * (1.f / BM);
+        for (int i = 0; i < 8; ++i) sv += acc[i][j][r];
+        sv = row16_sum(sv);
+        const float mean = sv * (1.f / 128);
         float q = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float d = acc[i][j][r] - mean;
           q += d * d;
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
-        if ((lane & 15) == 0) red_q[wm * BN + col] = q;
+        q = row16_sum(q);
+        if ((lane & 15) == 0) {
+          p.stat_sum[so + j * 16 + r] = sv;
+          p.stat_m2[so + j * 16 + r] = q;
+        }
       }
-    __syncthreads();
-    if (tid < BN) {
-      float ts = 0.f, tq = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        ts += red_s[w * BN + tid];
-        tq += red_q[w * BN + tid];
-      }
-      p.stat_sum[(int64_t)mt * p.ncol + n0 + tid] = ts;
-      p.stat_m2[(int64_t)mt * p.ncol + n0 + tid] = tq;
-    }
   }
   // bf16 staging: 8-byte writes of 4 consecutive channels of one pixel
 #pragma unroll
@@ -425,8 +410,8 @@ int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype) {
     if (g.cend[t] % 32 != 0 || g.stride[t] % 8 != 0) return 0;
   if (p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0) return 0;
   if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
-  const int bn = pick_bn(p);
-  return bn == 256 ? 256 : bn == 128 ? 512 : bn == 64 ? 1024 : 0;
+  // BatchNorm statistics come per wave: 128-pixel tiles
+  return pick_bn(p) ? 128 : 0;
 }
 
 int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st) {
@@ -438,10 +423,14 @@ int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st) {
   }
 }
 
+int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
+int conv_fp8_tune(int key, int value);     // conv_fp8.hip
+
 extern "C" int vu_gemm_set_tuning(int key, int value) {
   if (key == VU_TUNE_V4_MIN_BLOCKS) {
     g_min_blocks = value;
     return 0;
   }
+  if (gemm_fwd_v5_tune(key, value) == 0 || conv_fp8_tune(key, value) == 0) return 0;
   return (int)hipErrorInvalidValue;
 }

@@ -1,0 +1,133 @@
+"""fp8 (OCP e4m3fn) 3x3 convolution forward path -- BASELINE.json configs[4]
+("fp8 NHWC implicit-GEMM 3x3 conv path on CDNA4 fp8 MFMA, 3x1024x1024").
+
+The reference has no fp8 path.  This is the
+DoubleConv convolution (unet_parts.py:40,43) with
+
+* activations quantised to e4m3 with ONE scale per tensor (448 / amax; the
+  concat sources of an Up block share it),
+* weights quantised to e4m3 with one scale per output channel,
+* fp32 accumulation on the gfx950 f8f6f4 MFMA (csrc/conv_fp8.hip), the two
+  dequantisation scales and the bias applied in the epilogue, bf16 output
+  and the BatchNorm partial statistics of that output.
+
+Parity: the kernel equals fp32 convolution of the DEQUANTISED operands up to
+fp32 summation order and the bf16 output rounding, and the quantisers are
+bit-exact against ``torch.float8_e4m3fn`` (tests/test_gpu_fp8.py); the error
+against the unquantised fp32 convolution is reported by tools/fp8_bench.py.
+There is no fallback: shapes the kernel does not serve raise.
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib
+from . import engine as E
+from . import kernels as K
+from ._lib import VuConvFp8, call, query, stream
+
+E4M3 = torch.float8_e4m3fn
+
+
+def amax(srcs):
+    """max |x| over all sources (device fp32 [1])."""
+    out = torch.empty(1, dtype=torch.float32, device=srcs[0].device)
+    for i, t in enumerate(srcs):
+        N, Cc, H, W = t.shape
+        call("vu_amax", C.c_void_p(t.data_ptr()), K.pstride(t), N * H * W, Cc, C.c_void_p(out.data_ptr()),
+             1 if i else 0, K.dcode(t.dtype), stream())
+    return out
+
+
+def quantize(x, am):
+    """x (bf16/fp32 NHWC) -> (e4m3 NHWC, dequant scale [1]) with s = 448/amax."""
+    N, Cc, H, W = x.shape
+    q = torch.empty((N, Cc, H, W), dtype=E4M3, device=x.device, memory_format=K.CL)
+    dq = torch.empty(1, dtype=torch.float32, device=x.device)
+    call("vu_quant_fp8", C.c_void_p(x.data_ptr()), K.pstride(x), N * H * W, Cc, C.c_void_p(am.data_ptr()),
+         C.c_void_p(q.data_ptr()), K.pstride(q), C.c_void_p(dq.data_ptr()), K.dcode(x.dtype), stream())
+    return q, dq
+
+
+def quantize_rows(m):
+    """fp32 [rows][cols] -> (e4m3 [rows][cols], per-row dequant scale [rows])."""
+    rows, cols = m.shape
+    q = torch.empty((rows, cols), dtype=E4M3, device=m.device)
+    dq = torch.empty(rows, dtype=torch.float32, device=m.device)
+    call("vu_quant_rows_fp8", C.c_void_p(m.data_ptr()), rows, cols, C.c_void_p(q.data_ptr()), cols,
+         C.c_void_p(dq.data_ptr()), stream())
+    return q, dq
+
+
+def quantize_weight(w):
+    """Conv weight [Cout, Cin, 3, 3] -> (e4m3 [Cout][9*Cin] with k = tap*Cin + c,
+    dequant scale per output channel), cached per parameter version."""
+    ver = (w._version, w.data_ptr())
+    ent = w.__dict__.get("_vu_fp8")
+    if ent is None or ent[0] != ver:
+        wf = E.w3x3_fwd(w, _lib.F32)       # fp32 [Cout][9*Cin], the bf16 kernels' k order
+        ent = (ver, quantize_rows(wf.contiguous()))
+        w.__dict__["_vu_fp8"] = ent
+    return ent[1]
+
+
+def conv3x3(xqs, x_dq, wq, w_dq, ncol, out=None, out_coff=0, bias=None, stats=False):
+    """out[m][co] = x_dq * w_dq[co] * sum_k xq[m][k] wq[co][k] (+bias), bf16 NHWC.
+    xqs: 1-3 e4m3 NHWC sources (channel concat, 64-channel aligned)."""
+    N, _, H, W = xqs[0].shape
+    if out is None:
+        out = K.empty_act(N, ncol, H, W, torch.bfloat16, xqs[0].device)
+    a = VuConvFp8()
+    a.a = K.gather3x3(xqs)
+    a.w = wq.data_ptr()
+    a.ldw = wq.shape[1]
+    a.ncol = ncol
+    a.out_coff = out_coff
+    a.x_scale = x_dq.data_ptr()
+    a.w_scale = w_dq.data_ptr()
+    a.bias = bias.data_ptr() if bias is not None else None
+    a.out = out.data_ptr()
+    a.out_stride = K.pstride(out)
+    a.stat_sum = a.stat_m2 = None
+    rows = N * H * W
+    bm = query("vu_conv3x3_fp8_row_tile", C.byref(a))
+    if bm <= 0:
+        raise ValueError(f"fp8 3x3 conv: shape not served (C={a.a.C}, ncol={ncol}, H={H}, W={W})")
+    st = None
+    if stats:
+        tiles = (rows + bm - 1) // bm
+        psum = torch.empty((tiles, ncol), dtype=torch.float32, device=out.device)
+        pm2 = torch.empty_like(psum)
+        a.stat_sum, a.stat_m2 = psum.data_ptr(), pm2.data_ptr()
+        st = K.Stats(psum, pm2, tiles, bm, rows)
+    K._timed("conv3x3_fp8_fwd", 2 * rows * ncol * 9 * a.a.C,
+             lambda: call("vu_conv3x3_fp8", C.byref(a), stream()))
+    return out, st
+
+
+def conv3x3_q(srcs, weight, bias=None, stats=False):
+    """Quantise the (bf16) sources with one shared scale and the weights, then
+    run the fp8 conv.  Returns (bf16 output, Stats or None)."""
+    am = amax(srcs)
+    qs, dq = [], None
+    for t in srcs:
+        q, dq = quantize(t, am)
+        qs.append(q)
+    wq, ws = quantize_weight(weight)
+    return conv3x3(qs, dq, wq, ws, weight.shape[0], bias=bias, stats=stats)
+
+
+@torch.no_grad()
+def double_conv_forward(mod, x):
+    """DoubleConv.forward (unet_parts.py:32-49) with both 3x3 convs in fp8:
+    conv -> BatchNorm (batch statistics from the fp8 conv epilogue in train
+    mode, running statistics in eval mode) -> ReLU, twice; bf16 NHWC out."""
+    conv1, bn1, _, conv2, bn2, _ = mod.double_conv
+    a = x
+    for conv, bn in ((conv1, bn1), (conv2, bn2)):
+        y, st = conv3x3_q([a], conv.weight, stats=bn.training)
+        coef = E.bn_coef(bn, st, conv.out_channels)
+        out = torch.empty_like(y)
+        K.bn_apply(y, out, coef, True, _lib.BF16)
+        a = out
+    return a
