@@ -28,6 +28,19 @@ PEAK_HBM_GBS = 8000.0
 # algorithmic FLOPs of the 3x3 convolutions per 512x512 image:
 # fwd 368.13 + dgrad 367.22 + wgrad 368.13 GFLOP (inc.0 included)
 CONV3_GFLOP_PER_IMG = 1103.5
+METRIC = "images/sec (whole node) at 3x512x512 bs=8/GPU; Dice parity vs CPU ref"   # BASELINE.json
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the 3x3 conv kernels from the committed rocprofv3
+    PMC passes (tools/gpu_pmc.sh -> tools/pmc_traffic.py), or None."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            v = json.load(f).get("conv3x3_hbm_bytes_per_launch")
+        return None if v is None else round(float(v))
+    except (OSError, ValueError):
+        return None
 
 
 def parse():
@@ -55,10 +68,14 @@ def synthetic(B, S, C, rank, dev):
             t.to(dev).contiguous(memory_format=torch.channels_last))
 
 
-def cpu_baseline(args, n_steps):
+def cpu_baseline(args, n_steps, dev):
     """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py)
     timed on this host on a bounded sample: batch 1 at the same 3x512x512 /
-    2-class config, fp32, full train step (fwd, CombinedLoss, bwd, clip, AdamW)."""
+    2-class config, fp32, full train step (fwd, CombinedLoss, bwd, clip, AdamW).
+
+    Its first (untimed) step also yields the oracle's logits and loss at the
+    initial weights; the GPU model (fp32 parity mode, same weights, same image)
+    is compared with them: the "Dice parity vs CPU ref" of the metric name."""
     from oracle import cpu_ref as R
     from vaeunet_amd import UNet
     from vaeunet_amd.init import seeded_init_
@@ -69,7 +86,8 @@ def cpu_baseline(args, n_steps):
     opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
     x, t = synthetic(1, args.size, args.classes, 0, "cpu")
     x, t = x.contiguous(), t.contiguous()
-    R.train_step(model, opt, x, t)  # warmup
+    ref_logits, ref_loss, _ = R.train_step(model, opt, x, t)  # warmup; pre-update outputs
+    parity = gpu_parity(args, x, t, ref_logits, ref_loss, dev)
     t0 = time.perf_counter()
     for _ in range(n_steps):
         R.train_step(model, opt, x, t)
@@ -77,7 +95,30 @@ def cpu_baseline(args, n_steps):
     return {"value": round(n_steps / dt, 4), "unit": "images/sec", "cores": threads,
             "kind": "port",
             "sample": f"{n_steps} fp32 train steps of UNet(3,{args.classes}) on 1x3x{args.size}x"
-                      f"{args.size} (oracle/cpu_ref.py, torch CPU, {threads} threads)"}
+                      f"{args.size} (oracle/cpu_ref.py, torch CPU, {threads} threads)"}, parity
+
+
+def gpu_parity(args, x, t, ref_logits, ref_loss, dev):
+    """GPU UNet (fp32 parity mode: no autocast) vs the CPU oracle on one image."""
+    from vaeunet_amd import UNet
+    from vaeunet_amd.init import seeded_init_
+    from vaeunet_amd.loss import CombinedLoss
+    model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
+    model.train()
+    xg = x.to(dev).contiguous(memory_format=torch.channels_last)
+    tg = t.to(dev).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        lg = model(xg)
+        loss = CombinedLoss()(lg, tg)
+    lg = lg.float().cpu()
+    ref = ref_logits.float()
+    cg, cr = lg.argmax(1), ref.argmax(1)
+    fg, fr = (cg == 1), (cr == 1)
+    den = int(fg.sum() + fr.sum())
+    dice = 1.0 if den == 0 else 2.0 * int((fg & fr).sum()) / den
+    return {"dice_class_map": round(dice, 6), "argmax_agree": round(float((cg == cr).float().mean()), 8),
+            "max_abs_logit_diff": float((lg - ref).abs().max()), "loss_abs_diff": abs(float(loss) - float(ref_loss)),
+            "sample": f"1x3x{args.size}x{args.size}, fp32 GPU vs oracle/cpu_ref.py, same weights/input"}
 
 
 def main():
@@ -158,18 +199,19 @@ def main():
         n = sum(v[2] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
         achieved = fl / (tm * 1e-3) / 1e12 if tm > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
+                "traffic_unit": "HBM bytes per launch (profiles/pmc_traffic.json)",
                 "kernel": "gemm_fwd_kernel+gemm_wgrad_kernel (3x3 conv fwd/dgrad/wgrad, inc.0 excluded)",
                 "launches_per_step": n // 2,
                 "per_kind": {k: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1),
                                  "ms_per_step": round(v[1] / 2, 3)} for k, v in sorted(summ.items())}}
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.cpu_sample_steps)
+        cpu, parity = cpu_baseline(args, args.cpu_sample_steps, dev)
 
     if rank == 0:
-        line = {"metric": "images/sec (whole node) at 3x512x512 bs=8/GPU", "value": round(imgs, 2),
+        line = {"metric": METRIC, "value": round(imgs, 2),
                 "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
@@ -178,7 +220,7 @@ def main():
                            "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
                            "global_batch": args.batch * world, "parallelism": f"dp{world}"},
                 "loss": round(float(loss.item()), 6),
-                "roofline": roof, "cpu_baseline": cpu}
+                "roofline": roof, "cpu_baseline": cpu, "parity": parity}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

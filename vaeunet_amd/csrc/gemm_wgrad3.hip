@@ -56,7 +56,7 @@ VU_DEV u32x4 tr_frag(const char* base, int off_lo, int off_hi) {
 
 // XM: experiment mode for timing studies (0 in production): 1 = no DMA after
 // the first tile, 2 = no MFMA.
-template <int BI, int XM>
+template <int BI, int XM, int TJ>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   constexpr int NT = 512;
   constexpr int RBP = BI * 2, CPI = BI / 8;
@@ -64,9 +64,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   constexpr int NH = (HROWS * HWP * 8 + NT - 1) / NT;     // halo DMA instrs per thread per tile
   constexpr int PB = TP * RBP, QB = NH * NT * 16;
   constexpr int STAGE = PB + QB;
-  constexpr int TI = 2;                                   // co tiles per wave
-  constexpr int TJ = BI == 64 ? 1 : 2;                    // ci tiles per wave
-  constexpr int WCI = 4 / TJ;                             // waves along ci
+  // TJ = 1: a wave owns 4 (BI=128) or 2 (BI=64) co tiles x one 16-channel ci tile,
+  // the fewest transposed LDS reads per MFMA (A fragments reused over 9 taps)
+  constexpr int WCI = 4 / TJ;                             // waves along ci (TJ ci tiles per wave)
+  constexpr int TI = BI / 16 / (8 / WCI);                 // co tiles per wave
   static_assert(LP >= 1, "tile too small");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
@@ -229,10 +230,11 @@ template <int BI>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int64_t nblk = (int64_t)((p.ni + BI - 1) / BI) * (p.q.C / 64) * p.splits;
   if (nblk <= 0) return 0;
+  const dim3 grid((unsigned)nblk), blk(512);
   switch (xmode()) {
-    case 1: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 2>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    default: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 0>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+    case 1: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, 1>), grid, blk, 0, st, p); break;
+    case 2: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 2, 1>), grid, blk, 0, st, p); break;
+    default: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 0, 1>), grid, blk, 0, st, p);
   }
   return (int)hipGetLastError();
 }
