@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--classes", type=int, default=2)
+    ap.add_argument("--model", choices=("unet", "vae"), default="unet",
+                    help="unet = BASELINE configs[1] (the metric); vae = configs[2], UNetResNet + KL")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=2)
@@ -103,7 +105,17 @@ def gpu_parity(args, x, t, ref_logits, ref_loss, dev):
     from vaeunet_amd import UNet
     from vaeunet_amd.init import seeded_init_
     from vaeunet_amd.loss import CombinedLoss
-    model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
+    vae = args.model == "vae"
+    if vae:
+        # BASELINE configs[2]: VAE-U-Net (ResNet34 encoder, latent 32, attention, latent
+        # injection "all"), 1 class as train.py's resnet path (train.py:683,693)
+        from vaeunet_amd import UNetResNet
+        from vaeunet_amd.loss import kl_with_free_bits
+        args.classes = 1
+        args.no_cpu_baseline = True
+        model = seeded_init_(UNetResNet(3, 1, pretrained=False), 0).to(dev).to(memory_format=torch.channels_last)
+    else:
+        model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
     model.train()
     xg = x.to(dev).contiguous(memory_format=torch.channels_last)
     tg = t.to(dev).contiguous(memory_format=torch.channels_last)
@@ -136,7 +148,17 @@ def main():
     from vaeunet_amd.loss import CombinedLoss
     from vaeunet_amd import parallel
 
-    model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
+    vae = args.model == "vae"
+    if vae:
+        # BASELINE configs[2]: VAE-U-Net (ResNet34 encoder, latent 32, attention, latent
+        # injection "all"), 1 class as train.py's resnet path (train.py:683,693)
+        from vaeunet_amd import UNetResNet
+        from vaeunet_amd.loss import kl_with_free_bits
+        args.classes = 1
+        args.no_cpu_baseline = True
+        model = seeded_init_(UNetResNet(3, 1, pretrained=False), 0).to(dev).to(memory_format=torch.channels_last)
+    else:
+        model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
     model.train()
     reducer = parallel.attach(model) if world > 1 else None
     if args.torch_optim:
@@ -154,8 +176,12 @@ def main():
         if reducer is not None:
             reducer.prepare()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            logits = model(x)
-            loss = crit(logits, t)
+            if vae:
+                logits, mu, lv = model(x)
+                loss = crit(logits, t) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+            else:
+                logits = model(x)
+                loss = crit(logits, t)
         loss.backward()
         if reducer is not None:
             reducer.finish()
@@ -215,8 +241,10 @@ def main():
                 "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-                "config": {"workload": f"UNet(3,{args.classes}) train step (fwd+CombinedLoss+bwd"
-                                       "+clip+AdamW), random-init weights",
+                "config": {"workload": (f"UNetResNet(3,1) VAE train step (fwd+CombinedLoss+1e-3*KL+bwd"
+                                        "+clip+AdamW), random-init weights" if vae else
+                                        f"UNet(3,{args.classes}) train step (fwd+CombinedLoss+bwd"
+                                        "+clip+AdamW), random-init weights"),
                            "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
                            "global_batch": args.batch * world, "parallelism": f"dp{world}"},
                 "loss": round(float(loss.item()), 6),
