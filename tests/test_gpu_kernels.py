@@ -204,6 +204,45 @@ def test_conv3x3_persistent_kernel(case):
         _tune(*TUNE_DEFAULTS)
 
 
+IMAGE_CASES = [
+    # (N, H, W, cout): the 8-channel (packed 3-channel image) conv kernel (conv_image.hip)
+    (2, 16, 64, 64),
+    (1, 12, 32, 128),    # two 64-column tiles, image borders on every side
+    (3, 8, 48, 64),
+]
+
+
+@pytest.mark.parametrize("case", IMAGE_CASES)
+def test_conv3x3_image_kernel(case):
+    """inc.0 conv over the channel-padded image: forward with bias and BN
+    statistics vs torch fp32 (the padded channels are zero)."""
+    K, E = _k()
+    N, H, W, co = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.zeros(N, 8, H, W)
+    x[:, :3] = torch.rand(N, 3, H, W, generator=g)
+    x = x.to(torch.bfloat16).float()
+    w = torch.randn(co, 3, 3, 3, generator=g) / 3
+    b = torch.randn(co, generator=g)
+    d = _code("bf16")
+    xs = _act(x, "bf16")
+    wm = E.w3x3_fwd(w.to(DEV), d, 8)
+    out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
+    assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out)) == 64
+    st = K.gemm_fwd(K.gather3x3([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
+    ref = F.conv2d(x[:, :3], w.to(torch.bfloat16).float(), b, padding=1)
+    _close(out, ref, "bf16", what="image conv")
+    stored = out.float().cpu()
+    n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                     dtype=torch.float64)
+    s = st.psum.double().cpu()
+    mean = s.sum(0) / n.sum()
+    m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+    torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close((m2.sum(0) / n.sum()).float(), stored.var((0, 2, 3), unbiased=False),
+                               rtol=1e-4, atol=1e-5)
+
+
 def _row_tile_args(K, srcs, wmat, ncol, out):
     import ctypes as C
     from vaeunet_amd import _lib
