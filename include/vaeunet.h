@@ -105,12 +105,15 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     2 x CU count; 0 forces it);
  *   VU_TUNE_V5_GRID / VU_TUNE_FP8_GRID: cap on the grid of the persistent
  *     bf16 / fp8 kernels (default 0 = CU count; tests use small caps so that
- *     every block walks several tiles). */
+ *     every block walks several tiles);
+ *   VU_TUNE_STREAM: 1 (default) lets the short-K 1x1 stream kernel
+ *     (gemm_stream.hip) serve the problems it takes, 0 routes them to v2. */
 #define VU_TUNE_V4_MIN_BLOCKS 0
 #define VU_TUNE_V5_MAX_C 1
 #define VU_TUNE_V5_MIN_TILES 2
 #define VU_TUNE_V5_GRID 3
 #define VU_TUNE_FP8_GRID 4
+#define VU_TUNE_STREAM 5
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */

@@ -243,11 +243,57 @@ def test_conv3x3_image_kernel(case):
                                rtol=1e-4, atol=1e-5)
 
 
-def _row_tile_args(K, srcs, wmat, ncol, out):
+STREAM_CASES = [
+    # (K = Cin, N = Cout, accumulate into a channel slice): 1x1 stream kernel (gemm_stream.hip)
+    (64, 32, False),
+    (128, 64, False),
+    (32, 64, True),
+]
+
+
+@pytest.mark.parametrize("case", STREAM_CASES)
+def test_gemm_stream_kernel(case):
+    """short-K 1x1 GEMM streams (attention W_g/W_x and their input grads at
+    256^2/512^2): bias + BN partials, or accumulate into a channel slice."""
+    K, E = _k()
+    cin, co, acc = case
+    N, H, W = 2, 256, 256
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, cin, H, W, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(co, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(co, generator=g)
+    d = _code("bf16")
+    xs = _act(x, "bf16")
+    wm = E.w1x1_fwd(w.to(DEV), d)
+    ref = F.conv2d(x, w.to(torch.bfloat16).float(), b)
+    if not acc:
+        out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
+        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out, K.gather1x1)) in (32, 64)
+        st = K.gemm_fwd(K.gather1x1([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
+        _close(out, ref, "bf16", what="stream fwd")
+        stored = out.float().cpu()
+        n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                         dtype=torch.float64)
+        s_ = st.psum.double().cpu()
+        mean = s_.sum(0) / n.sum()
+        m2 = st.pm2.double().cpu() + n[:, None] * (s_ / n[:, None] - mean) ** 2
+        torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close((m2.sum(0) / n.sum()).float(), stored.var((0, 2, 3), unbiased=False),
+                                   rtol=1e-4, atol=1e-4)
+    else:
+        base = torch.randn(N, co + 32, H, W, generator=g).to(torch.bfloat16).float()
+        wide = _act(base, "bf16")
+        K.gemm_fwd(K.gather1x1([xs]), wm, co, wide, d, out_coff=32, bias=b.to(DEV), accumulate=True)
+        exp = base.clone()
+        exp[:, 32:] += ref
+        _close(wide, exp, "bf16", what="stream accumulate")
+
+
+def _row_tile_args(K, srcs, wmat, ncol, out, gather=None):
     import ctypes as C
     from vaeunet_amd import _lib
     a = _lib.VuGemmFwd()
-    a.a = K.gather3x3(srcs)
+    a.a = (gather or K.gather3x3)(srcs)
     a.b = wmat.data_ptr()
     a.ldb = wmat.shape[-1]
     a.ncol = ncol

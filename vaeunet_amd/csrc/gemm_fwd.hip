@@ -331,6 +331,8 @@ int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st);
 int conv_image_bm(const VuGemmFwd& p, int dtype);      // conv_image.hip (3-channel image conv)
 int conv_image_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_stream_bm(const VuGemmFwd& p, int dtype);     // gemm_stream.hip (short-K 1x1 streams)
+int gemm_stream_launch(const VuGemmFwd& p, hipStream_t st);
 
 static bool use_v2(int dtype) {
   static int mode = -1;
@@ -363,6 +365,8 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype)) {
     int bm = conv_image_bm(*args, dtype);
     if (bm) return bm;
+    bm = gemm_stream_bm(*args, dtype);
+    if (bm) return bm;
   }
   if (use_v4(dtype)) {
     int bm = gemm_fwd_v5_bm(*args, dtype);
@@ -387,6 +391,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if ((args->ldb % epc) != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return conv_image_launch(*args, st);
+  if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v5_bm(*args, dtype)) return gemm_fwd_v5_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);

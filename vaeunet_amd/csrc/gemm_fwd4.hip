@@ -425,12 +425,14 @@ int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st) {
 
 int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
 int conv_fp8_tune(int key, int value);     // conv_fp8.hip
+int gemm_stream_tune(int key, int value);  // gemm_stream.hip
 
 extern "C" int vu_gemm_set_tuning(int key, int value) {
   if (key == VU_TUNE_V4_MIN_BLOCKS) {
     g_min_blocks = value;
     return 0;
   }
-  if (gemm_fwd_v5_tune(key, value) == 0 || conv_fp8_tune(key, value) == 0) return 0;
+  if (gemm_fwd_v5_tune(key, value) == 0 || conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0)
+    return 0;
   return (int)hipErrorInvalidValue;
 }

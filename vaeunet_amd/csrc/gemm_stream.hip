@@ -1,0 +1,258 @@
+// Short-K, narrow-N 1x1 GEMMs as HBM streams ("stream" kernel, bf16):
+// out[m][j] = sum_k A[m][k] B[j][k] (+bias) with K = 32, 64 or 128 and
+// N <= 64 -- the AttentionGate W_g / W_x convolutions of the 256^2 / 512^2
+// levels (unet_parts.py:11,15) and the 512^2 level's input gradients
+// (accumulated into the skip / gate gradients); the ConvTranspose2d
+// pixel-shuffle store (unet_parts.py:76) is supported for N <= 64.  These move 2-3 bytes per flop: at 256-row LDS tiles
+// (gemm_fwd2.hip) a block's life is its load latency and epilogue, so they
+// ran at 2.5-4 TB/s.  Here:
+//
+//   * the weight matrix (<= 16 KB) is copied into LDS ONCE per block and the
+//     blocks are persistent (one pass over the pixel tiles);
+//   * each wave streams its own 16*NF-pixel tiles straight from global: all
+//     K of a tile (16 bytes = 8 channels per lane and k-step) is in flight
+//     before the first MFMA;
+//   * MFMA(weights, pixels), weight rows read in a permuted order so a lane
+//     owns 4*GS consecutive output columns of one pixel (16/32-byte stores,
+//     the ConvT pixel shuffle keeps them contiguous), BN partials per wave
+//     tile by DPP row sums, optional accumulate (input gradients).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int R>
+VU_DEV float ror_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xf, 0xf, false));
+}
+VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
+
+VU_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+constexpr int NT = 256;  // 4 waves
+
+// KS: k-steps of 32 (K = 32*KS); NJ: 16-column fragments (N = 16*NJ);
+// NF: 16-pixel fragments per wave tile.
+template <int KS, int NJ, int NF>
+__global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
+  constexpr int K = 32 * KS, N = 16 * NJ, PX = 16 * NF;
+  constexpr int GS = NJ < 4 ? NJ : 4;   // fragments per column group (4*GS consecutive columns per lane)
+  constexpr int RB = K * 2;             // LDS bytes per weight row
+  __shared__ __attribute__((aligned(16))) char wsm[N * RB];
+
+  const VuGather& g = p.a;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  const int ntiles = (int)(M / PX);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gq = lane >> 4, r16 = lane & 15;
+
+  // weights -> LDS (row j = output column j, K contiguous bf16), plain 16-byte copies
+  {
+    const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
+    constexpr int PIECES = N * K / 8;
+    for (int e = threadIdx.x; e < PIECES; e += NT) {
+      const int row = e / (K / 8), c8 = e - row * (K / 8);
+      *reinterpret_cast<u32x4*>(wsm + row * RB + c8 * 16) =
+          *reinterpret_cast<const u32x4*>(bmat + (int64_t)row * p.ldb + c8 * 8);
+    }
+    __syncthreads();
+  }
+  // A-row r16 of fragment j -> weight row (column) of the permuted order
+  auto wrow = [&](int j) { return (j / GS) * 16 * GS + 4 * GS * (r16 >> 2) + 4 * (j % GS) + (r16 & 3); };
+
+  const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[0]);
+  const int64_t st = g.stride[0];
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  const int HW = g.H * g.W;
+
+  for (int tile = blockIdx.x * (NT / 64) + wid; tile < ntiles; tile += gridDim.x * (NT / 64)) {
+    const int64_t pb = (int64_t)tile * PX;
+    u32x4 pf[NF][KS];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        pf[f][ks] = *reinterpret_cast<const u32x4*>(src + (pb + 16 * f + r16) * st + 32 * ks + 8 * gq);
+    f32x4 acc[NF][NJ];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[f][j] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const u32x4 wf = *reinterpret_cast<const u32x4*>(wsm + wrow(j) * RB + (32 * ks + 8 * gq) * 2);
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+          acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf),
+                                                              __builtin_bit_cast(bf16x8, pf[f][ks]), acc[f][j], 0, 0, 0);
+      }
+    // acc[f][j][r]: pixel pb + 16f + r16, column (j/GS)*16*GS + 4*GS*gq + 4*(j%GS) + r
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = (j / GS) * 16 * GS + 4 * GS * gq + 4 * (j % GS) + r;
+        const float bv = p.bias ? p.bias[p.out_mode == 1 ? col % p.cout : col] : 0.f;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(acc[f][j][r] + bv);
+      }
+    if (p.stat_sum) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        f32x4 sm, m2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sv = 0.f;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) sv += acc[f][j][r];
+          sv = row16_sum(sv);
+          const float mean = sv * (1.f / PX);
+          float v = 0.f;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) {
+            const float d = acc[f][j][r] - mean;
+            v += d * d;
+          }
+          sm[r] = sv;
+          m2[r] = row16_sum(v);
+        }
+        if (r16 == 0) {
+          const int col = (j / GS) * 16 * GS + 4 * GS * gq + 4 * (j % GS);
+          *reinterpret_cast<f32x4*>(p.stat_sum + (int64_t)tile * p.ncol + col) = sm;
+          *reinterpret_cast<f32x4*>(p.stat_m2 + (int64_t)tile * p.ncol + col) = m2;
+        }
+      }
+    }
+    // stores: per column group, 4*GS consecutive bf16 of one pixel
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int64_t m = pb + 16 * f + r16;
+#pragma unroll
+      for (int grp = 0; grp < NJ / GS; ++grp) {
+        const int col0 = grp * 16 * GS + 4 * GS * gq;
+        bf16_t* dst;
+        if (p.out_mode == 1) {
+          const int n = (int)(m / HW);
+          const int rem = (int)(m - (int64_t)n * HW);
+          const int h = rem / g.W, w = rem - (rem / g.W) * g.W;
+          const int ab = col0 / p.cout, co = col0 - ab * p.cout;
+          const int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
+          dst = out + ((int64_t)(n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
+        } else {
+          dst = out + m * p.out_stride + p.out_coff + col0;
+        }
+#pragma unroll
+        for (int h2 = 0; h2 < GS / 2; ++h2) {
+          f32x4 a = acc[f][grp * GS + 2 * h2], b = acc[f][grp * GS + 2 * h2 + 1];
+          if (p.accumulate) {
+            const u32x4 o = *reinterpret_cast<const u32x4*>(dst + 8 * h2);
+            a[0] += __uint_as_float(o[0] << 16);
+            a[1] += __uint_as_float(o[0] & 0xffff0000u);
+            a[2] += __uint_as_float(o[1] << 16);
+            a[3] += __uint_as_float(o[1] & 0xffff0000u);
+            b[0] += __uint_as_float(o[2] << 16);
+            b[1] += __uint_as_float(o[2] & 0xffff0000u);
+            b[2] += __uint_as_float(o[3] << 16);
+            b[3] += __uint_as_float(o[3] & 0xffff0000u);
+          }
+          u32x4 pk;
+          pk[0] = pack2(a[0], a[1]);
+          pk[1] = pack2(a[2], a[3]);
+          pk[2] = pack2(b[0], b[1]);
+          pk[3] = pack2(b[2], b[3]);
+          *reinterpret_cast<u32x4*>(dst + 8 * h2) = pk;
+        }
+      }
+    }
+  }
+}
+
+int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// pixel fragments per wave tile: NF*NJ <= 16 accumulator fragments, NF*KS <= 8 operand registers sets
+constexpr int nf_of(int ks, int nj) {
+  return (16 / nj < 4 ? 16 / nj : 4) < (8 / ks) ? (16 / nj < 4 ? 16 / nj : 4) : 8 / ks;
+}
+
+template <int KS, int NJ>
+int launch_nj(const VuGemmFwd& p, hipStream_t st) {
+  constexpr int NF = nf_of(KS, NJ);
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  const int64_t tiles = M / (16 * NF);
+  int64_t nblk = (tiles + 3) / 4;
+  const int64_t cap = 2 * (int64_t)cu_count();
+  if (nblk > cap) nblk = cap;
+  hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+template <int KS>
+int launch_ks(const VuGemmFwd& p, hipStream_t st) {
+  switch (p.ncol / 16) {
+    case 2: return launch_nj<KS, 2>(p, st);
+    case 4: return launch_nj<KS, 4>(p, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+bool g_enabled = true;  // VU_TUNE_STREAM
+
+}  // namespace
+
+// Row tile (16*NF pixels) when the stream kernel serves this problem, else 0:
+// bf16 1x1 gather of ONE NHWC source with K = C in {32, 64, 128}, N in {32,
+// 64}, plain (mode 0, optional accumulate) or ConvT pixel-shuffle
+// (mode 1, no statistics) output, whole tiles, enough tiles to fill the chip.
+int gemm_stream_bm(const VuGemmFwd& p, int dtype) {
+  const VuGather& g = p.a;
+  if (!g_enabled || dtype != VU_BF16) return 0;
+  if (g.R != 1 || g.S != 1 || g.sy != 1 || g.sx != 1 || g.oy != 0 || g.ox != 0 || g.Hs != g.H ||
+      g.Ws != g.W || g.nsrc != 1)
+    return 0;
+  if (g.C != 32 && g.C != 64 && g.C != 128) return 0;
+  const int nj = p.ncol / 16;
+  // N <= 64: wider tiles spill (the epilogue's per-column state outgrows the register file)
+  if (p.ncol % 16 != 0 || (nj != 2 && nj != 4)) return 0;
+  if (g.stride[0] % 8 != 0 || p.ldb % 8 != 0 || p.ldb < g.C || p.out_stride % 8 != 0 || p.out_coff % 8 != 0)
+    return 0;
+  if (p.out_mode == 1) {
+    if (p.stat_sum || p.cout % 16 != 0 || p.ncol != 4 * p.cout) return 0;
+  } else if (p.out_mode != 0) {
+    return 0;
+  }
+  const int ks = g.C / 32;
+  const int px = 16 * nf_of(ks, nj);
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  if (M % px != 0 || M >= ((int64_t)1 << 31) || M / px < 4 * 2 * (int64_t)cu_count()) return 0;
+  return px;
+}
+
+int gemm_stream_launch(const VuGemmFwd& p, hipStream_t st) {
+  switch (p.a.C) {
+    case 32: return launch_ks<1>(p, st);
+    case 64: return launch_ks<2>(p, st);
+    case 128: return launch_ks<4>(p, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+int gemm_stream_tune(int key, int value) {
+  if (key == VU_TUNE_STREAM) {
+    g_enabled = value != 0;
+    return 0;
+  }
+  return -1;
+}
