@@ -47,6 +47,20 @@ template <> struct PP<64> { static constexpr int WM = 8, WN = 1, TH = 32, TW = 3
 
 VU_DEV void wait_vm(int n) {
   switch (n) {
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
@@ -54,7 +68,7 @@ VU_DEV void wait_vm(int n) {
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
@@ -76,8 +90,11 @@ VU_DEV float ror_add(float v) {
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
 // XM (experiment mode, timing studies only; 0 in production): 1 = no DMA in
-// the main loop, 2 = no DMA and no barriers in the main loop, 3 = no MFMA.
-template <int BN, int XM>
+// the main loop, 2 = no DMA and no barriers in the main loop, 3 = no MFMA,
+// 6/9 = next-chunk halo issued over steps 0-2 / 0-7 (production: step 0),
+// 7 = no weight DMA in the main loop, 8 = no halo DMA in the main loop.
+// NBW: weight ring slots (prefetch distance NBW-1 steps).
+template <int BN, int XM, int NBW>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
   constexpr int NT = 512;
@@ -91,8 +108,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int LB0 = WPIECES / 256;              // weight DMA slots per half-0 thread
   constexpr int LB0A = (LB0 + 1) / 2;             // ... issued in phase 1 (rest in phase 2)
   constexpr int WSLOT = BN * 64;
-  constexpr int NBW = 3;                          // weight ring (prefetch distance 2)
-  constexpr int PPS1 = (NHP1 + 7) / 8;            // halo slots issued per step (steps 0..7)
+  constexpr int PD = NBW - 1;                     // weight prefetch distance (steps)
+  // halo slots issued per step: the whole next-chunk halo goes out at step 0
+  // of the current chunk (measured 5 % faster than spreading it over steps
+  // 0..7: the HBM/MALL latency gets 8 steps of cover); XM 6 = steps 0-2,
+  // XM 9 = steps 0-7
+  constexpr int PPS1 = XM == 6 ? (NHP1 + 2) / 3 : XM == 9 ? (NHP1 + 7) / 8 : NHP1;
   constexpr int MAIN = 2 * HALO + NBW * WSLOT;
   constexpr int ROWB = BN * 2 + 16;               // bf16 staging row (padded)
   constexpr int EPI = BM * ROWB;
@@ -217,8 +238,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   if (grp) {
     halo_chunk(0, -1);
   } else {
-    wstage(0, 0, LB0);
-    if (nk > 1) wstage(1, 0, LB0);
+#pragma unroll
+    for (int q = 0; q < PD; ++q)
+      if (q < nk) wstage(q, 0, LB0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
@@ -234,44 +256,49 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(Bw + brow + j * 16 * 64);
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[i]);
-    if (!grp && s + 2 < nk) wstage(s + 2, 0, LB0A);
-    pp_barrier();
+    if (XM != 1 && XM != 2 && XM != 7 && !grp && s + PD < nk) wstage(s + PD, 0, LB0A);
+    if (XM != 2) pp_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+        if (XM != 3) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
                                                             __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
+    if (XM != 2) pp_barrier();
     // -- phase 2: pixel fragments 4..7; half 0 finishes weights(s+2) and waits
     //    for weights(s+1); half 1 streams the next chunk's halo and waits for
     //    it at the chunk's last step
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[4 + i]);
-    if (!grp) {
-      if (s + 2 < nk) {
-        wstage(s + 2, LB0A, LB0);
-        wait_vm(LB0);
+    if (XM == 1 || XM == 2 || (XM == 7 && !grp)) {
+    } else if (XM == 8 && grp) {
+    } else if (!grp) {
+      // outstanding weight steps after this issue: s+1 .. min(nk-1, s+PD);
+      // step s+1 must have landed
+      if (s + PD < nk) {
+        wstage(s + PD, LB0A, LB0);
+        wait_vm((PD - 1) * LB0);
       } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int out = nk - 2 - s;
+        wait_vm(out > 0 ? out * LB0 : 0);
       }
     } else if (c + 1 < nchunk) {
       if (t * PPS1 < NHP1) halo_chunk(c + 1, t);
       if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    pp_barrier();
+    if (XM != 2) pp_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+        if (XM != 3) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
                                                                 __builtin_bit_cast(bf16x8, af[i]), acc[4 + i][j], 0, 0,
                                                                 0);
     __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
+    if (XM != 2) pp_barrier();
   }
   if (!grp) pp_barrier();  // re-align the halves
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -357,18 +384,46 @@ int xmode() {
   return m;
 }
 
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// weight-ring depth: 3 slots (prefetch distance 2).  Deeper rings (up to the
+// LDS budget, max(2 halo + ring, bf16 staging) <= 160 KiB) measured within
+// 1 % on the 17 layer shapes, so they stay an experiment (VU_V4_NBW).
+template <int BN> constexpr int kNbwMax = BN == 64 ? 3 : 6;
+template <int BN> int nbw_for() {
+  static int v = -1;
+  if (v < 0) {
+    v = env_int("VU_V4_NBW", 3);
+    if (v < 3) v = 3;
+    if (v > kNbwMax<BN>) v = kNbwMax<BN>;
+  }
+  return v;
+}
+
 template <int BN>
 int launch(const VuGemmFwd& p, hipStream_t st) {
   const VuGather& g = p.a;
   const int64_t mt = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW);
-  const int64_t nblk = mt * (p.ncol / BN);
+  const dim3 grid((unsigned)(mt * (p.ncol / BN)));
+  constexpr int NM = kNbwMax<BN>;
   switch (xmode()) {
-    case 1: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 2>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 3>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    case 4: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 4>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    case 5: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 5>), dim3((unsigned)nblk), dim3(512), 0, st, p); break;
-    default: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+    case 1: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 1, 3>), grid, dim3(512), 0, st, p); break;
+    case 2: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 2, 3>), grid, dim3(512), 0, st, p); break;
+    case 3: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 3, 3>), grid, dim3(512), 0, st, p); break;
+    case 9: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 9, 3>), grid, dim3(512), 0, st, p); break;
+    case 6: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 6, 3>), grid, dim3(512), 0, st, p); break;
+    case 7: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 7, 3>), grid, dim3(512), 0, st, p); break;
+    case 8: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 8, 3>), grid, dim3(512), 0, st, p); break;
+    default:
+      switch (nbw_for<BN>()) {
+        case 3: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, 3>), grid, dim3(512), 0, st, p); break;
+        case 4: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, (NM < 4 ? NM : 4)>), grid, dim3(512), 0, st, p); break;
+        case 5: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, (NM < 5 ? NM : 5)>), grid, dim3(512), 0, st, p); break;
+        default: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, NM>), grid, dim3(512), 0, st, p);
+      }
   }
   return (int)hipGetLastError();
 }
@@ -387,8 +442,9 @@ int pick_bn(const VuGemmFwd& p) {
   const int64_t pix = (int64_t)g.N * g.H * g.W;
   const int mb = g_min_blocks;
   // at least ~one block per CU, else the v3 tiles (more, smaller blocks) win
-  if (tiles_ok<256>(p) && (pix / 256) * (p.ncol / 256) >= mb) return 256;
-  if (p.ncol % 256 != 0 && tiles_ok<128>(p) && (pix / 512) * (p.ncol / 128) >= mb) return 128;
+  static const int pref = env_int("VU_V4_PREF_BN", 256);
+  if (pref == 256 && tiles_ok<256>(p) && (pix / 256) * (p.ncol / 256) >= mb) return 256;
+  if ((pref != 256 || p.ncol % 256 != 0) && tiles_ok<128>(p) && (pix / 512) * (p.ncol / 128) >= mb) return 128;
   // 64 x 64 problems (18 K steps) are prologue/epilogue bound at 1 block/CU: v3 wins
   if (p.ncol == 64 && (g.C > 64 || mb < 256) && tiles_ok<64>(p) && pix / 1024 >= mb) return 64;
   return 0;
