@@ -169,9 +169,8 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     const int cur = st % NSTAGE;
     const char* Pb = smem + cur * STAGE;
     const char* Qb = Pb + BMR * RBP;
-#pragma unroll
-    for (int ks = 0; ks < BMR / 32; ++ks) {
-      u32x4 af[TI], bf[TJ];
+    // fragments of k-step ks+1 are read while k-step ks's MFMAs issue
+    auto load = [&](int ks, u32x4* af, u32x4* bf) {
       const int m = ks * 32 + 8 * g4 + qd;
 #pragma unroll
       for (int a = 0; a < TI; ++a) {
@@ -189,13 +188,19 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
         u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
         bf[b] = u32x4{l2[0], l2[1], h2[0], h2[1]};
       }
+    };
+    u32x4 af[2][TI], bf[2][TJ];
+    load(0, af[0], bf[0]);
+#pragma unroll
+    for (int ks = 0; ks < BMR / 32; ++ks) {
+      if (ks + 1 < BMR / 32) load(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TI; ++a)
 #pragma unroll
         for (int b = 0; b < TJ; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b], 0, 0, 0);
+              __builtin_bit_cast(bf16x8, af[ks & 1][a]), __builtin_bit_cast(bf16x8, bf[ks & 1][b]), acc[a][b], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   }

@@ -55,7 +55,8 @@ VU_DEV u32x4 tr_frag(const char* base, int off_lo, int off_hi) {
 }
 
 // XM: experiment mode for timing studies (0 in production): 1 = no DMA after
-// the first tile, 2 = no MFMA.
+// the first tile, 2 = no MFMA, 3 = the old full-pitch halo DMA (padding
+// pixels loaded from a zero page).
 template <int BI, int XM, int TJ>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   constexpr int NT = 512;
@@ -129,13 +130,18 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       }
       __builtin_amdgcn_global_load_lds(s, (lds_void*)(Pb + (k * NT + wid * 64) * 16), 16, 0, 0);
     }
+    // halo: only the 34 used pixels of each 48-pixel row are loaded (lanes on
+    // the pitch padding or past the last row issue nothing; a wave whose
+    // lanes are all padding skips the instruction)
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
-      const int y = y0 - 1 + q_hy[k], x = x0 - 1 + q_hx[k];
-      const void* s = zp;
-      if (q_hy[k] < HROWS && q_hx[k] < TW + 2 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
-        s = xsrc + (((int64_t)img * H + y) * W + x) * xst + q_col[k];
-      __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
+      if (XM == 3 || (q_hy[k] < HROWS && q_hx[k] < TW + 2)) {
+        const int y = y0 - 1 + q_hy[k], x = x0 - 1 + q_hx[k];
+        const void* s = zp;
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && q_hy[k] < HROWS && q_hx[k] < TW + 2)
+          s = xsrc + (((int64_t)img * H + y) * W + x) * xst + q_col[k];
+        __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
+      }
     }
   };
 
@@ -174,30 +180,40 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     if (XM != 1 && st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
     const char* Pb = smem + (st & 1) * STAGE;
     const char* Qb = Pb + PB;
+    // software-pipelined fragment reads over the 36 (k-step, tap) MFMA groups
+    // of a tile: group g's B fragments are read two groups ahead (and a
+    // k-step's A fragments two groups before its first tap), so an MFMA group
+    // never waits on a just-issued transposed LDS read
+    constexpr int NG = TP / 32 * 9;
+    u32x4 aq[2][TI], bq[3][TJ];
+    auto load_b = [&](int g, u32x4* dst) {
+      const int ks = g / 9, q = g - (g / 9) * 9, r = q / 3, s = q - (q / 3) * 3;
 #pragma unroll
-    for (int ks = 0; ks < TP / 32; ++ks) {
-      u32x4 af[TI];
+      for (int b = 0; b < TJ; ++b) dst[b] = tr_frag(Qb + (ks + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
+    };
+    auto load_a = [&](int ks, u32x4* dst) {
+#pragma unroll
+      for (int a = 0; a < TI; ++a) dst[a] = tr_frag(Pb + ks * 32 * RBP, offA[a][0], offA[a][1]);
+    };
+    load_a(0, aq[0]);
+    load_b(0, bq[0]);
+    load_b(1, bq[1]);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int ks = g / 9, t = g - (g / 9) * 9;
+      if (g + 2 < NG) {
+        if ((g + 2) % 9 == 0) load_a((g + 2) / 9, aq[((g + 2) / 9) & 1]);
+        load_b(g + 2, bq[(g + 2) % 3]);
+      }
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TI; ++a)
-        af[a] = tr_frag(Pb + ks * 32 * RBP, offA[a][0], offA[a][1]);
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          u32x4 bf[TJ];
-#pragma unroll
-          for (int b = 0; b < TJ; ++b)
-            bf[b] = tr_frag(Qb + (ks + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int a = 0; a < TI; ++a)
-#pragma unroll
-            for (int b = 0; b < TJ; ++b)
-              if (XM != 2) acc[a][b][r * 3 + s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b][r * 3 + s], 0, 0, 0);
-          __builtin_amdgcn_s_setprio(0);
-          if (XM == 2) asm volatile("" ::"v"(bf[0]), "v"(af[0]));
-        }
+        for (int b = 0; b < TJ; ++b)
+          if (XM != 2) acc[a][b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              __builtin_bit_cast(bf16x8, aq[ks & 1][a]), __builtin_bit_cast(bf16x8, bq[g % 3][b]), acc[a][b][t], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (XM == 2) asm volatile("" ::"v"(bq[g % 3][0]), "v"(aq[ks & 1][0]));
     }
   }
 
@@ -234,6 +250,7 @@ int launch(const VuGemmWgrad& p, hipStream_t st) {
   switch (xmode()) {
     case 1: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, 1>), grid, blk, 0, st, p); break;
     case 2: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 2, 1>), grid, blk, 0, st, p); break;
+    case 3: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 3, 1>), grid, blk, 0, st, p); break;
     default: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 0, 1>), grid, blk, 0, st, p);
   }
   return (int)hipGetLastError();
