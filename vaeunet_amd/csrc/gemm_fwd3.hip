@@ -186,22 +186,27 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(VuGemmFwd p) {
     const char* A = hbuf + (c % NHB) * HALO;
     const char* B = bbuf + (s % NBS) * BSTG;
     const int toff = (t / 3) * HW + (t - (t / 3) * 3);
+    // both k-halves' fragments are read up front: the second half's reads
+    // complete under the first half's MFMAs
+    u32x4 af[2][TM], bf[2][TN];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      u32x4 af[TM], bf[TN];
       const int ch = kk * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + swz(hrow[i] + toff, ch));
+      for (int i = 0; i < TM; ++i) af[kk][i] = *reinterpret_cast<const u32x4*>(A + swz(hrow[i] + toff, ch));
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        bf[j] = *reinterpret_cast<const u32x4*>(B + swz(wn * (BN / WN) + j * 16 + (lane & 15), ch));
+        bf[kk][j] = *reinterpret_cast<const u32x4*>(B + swz(wn * (BN / WN) + j * 16 + (lane & 15), ch));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                              __builtin_bit_cast(bf16x8, bf[j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[kk][i]),
+                                                              __builtin_bit_cast(bf16x8, bf[kk][j]), acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
   }
