@@ -7,6 +7,7 @@ channel concat of unet_parts.py:94 is addressed without a copy).  Every
 function launches on the current HIP stream and never synchronises.
 """
 import ctypes as C
+import os
 
 import torch
 
@@ -179,6 +180,10 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     return st
 
 
+SPLIT_PIX = int(os.environ.get("VU_WGRAD_SPLIT_PIX", "4096"))
+SPLIT_MAX = 1024
+
+
 def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
     """grad[i*s_i + (j//Cq)*s_tap + (j%Cq)*s_c] (+)= sum_m P[m][i] Q[m][j]."""
     M = gp.N * gp.H * gp.W
@@ -204,6 +209,12 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
         if eff > best[0] + 1e-9:
             best = (eff, s)
     splits = best[1]
+    # v2 (1x1 / ConvT): very long pixel ranges per block (> SPLIT_PIX) expose
+    # the ring's DMA latency on every step, so a second wave of blocks measured
+    # faster (512^2 attention W_x gradient: 256 splits 158 us, 512 splits
+    # 112 us); the halo kernel (v3) measured slower with more splits
+    while kind == 2 and M // splits > SPLIT_PIX and tiles * splits * 2 <= 8 * slots and splits * 2 <= SPLIT_MAX:
+        splits *= 2
     mps = ((-(-M // splits)) + gran - 1) // gran * gran
     splits = -(-M // mps)
     slab = torch.empty((splits, ni, nj), dtype=torch.float32, device=grad.device)
