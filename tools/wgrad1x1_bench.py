@@ -43,8 +43,27 @@ def run(gp, gq, ni, nj, splits, slab):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--splits", default="64,128,256,512,1024")
+    ap.add_argument("--convt", action="store_true", help="the ConvTranspose(2,2) weight gradients instead")
     args = ap.parse_args()
     dev = torch.device("cuda")
+    if args.convt:
+        # up1..up4: ConvT(cin -> cin/2) on an h x h input, dW[ci][(a,b,co)] = sum x1 * dU
+        for name, cin, h in [("up1", 1024, 32), ("up2", 512, 64), ("up3", 256, 128), ("up4", 128, 256)]:
+            cu = cin // 2
+            x1 = torch.randn(B, cin, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=K.CL)
+            du = torch.randn(B, cu, 2 * h, 2 * h, device=dev).to(torch.bfloat16).contiguous(memory_format=K.CL)
+            g = torch.empty(cin, cu, 2, 2, device=dev)
+            fl = 2.0 * B * h * h * cin * 4 * cu
+            from vaeunet_amd.engine import convT_layout
+            ms = timeit(lambda: K.gemm_wgrad(K.gather1x1([x1]), K.gather_convT(du, B, h, h, 0, 0), cin, 4 * cu, g,
+                                             convT_layout(g), _lib.BF16, False))
+            line = f"{name} {cin:4d}x{4 * cu:4d} M={B * h * h:7d} | dispatch {ms * 1e3:7.1f}us {fl / ms / 1e9:5.0f}TF"
+            slab = torch.empty(max(int(v) for v in args.splits.split(",")), cin, 4 * cu, device=dev)
+            for s in [int(v) for v in args.splits.split(",")]:
+                ms = timeit(lambda: run(K.gather1x1([x1]), K.gather_convT(du, B, h, h, 0, 0), cin, 4 * cu, s, slab))
+                line += f" | s{s} {ms * 1e3:6.1f}us"
+            print(line, flush=True)
+        return
     for name, c, h in LEVELS:
         fi = c // 2
         dy = torch.randn(B, fi, h, h, device=dev).to(torch.bfloat16).contiguous(memory_format=K.CL)
