@@ -55,7 +55,11 @@ def parse():
                     help="unet = BASELINE configs[1] (the metric); vae = configs[2], UNetResNet + KL")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--cpu-sample-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=8, help="CPU baseline batch (BASELINE.md §4: 8)")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps per leg after 1 warmup")
+    ap.add_argument("--cpu-budget-s", type=float, default=90.0,
+                    help="cap on the timed CPU work per leg (fewer steps on a slow host)")
+    ap.add_argument("--cpu-no-bf16", action="store_true", help="skip the CPU autocast-bf16 leg")
     ap.add_argument("--torch-optim", action="store_true",
                     help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
     return ap.parse_args()
@@ -70,67 +74,118 @@ def synthetic(B, S, C, rank, dev):
             t.to(dev).contiguous(memory_format=torch.channels_last))
 
 
-def cpu_baseline(args, n_steps, dev):
-    """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py)
-    timed on this host on a bounded sample: batch 1 at the same 3x512x512 /
-    2-class config, fp32, full train step (fwd, CombinedLoss, bwd, clip, AdamW).
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
-    Its first (untimed) step also yields the oracle's logits and loss at the
-    initial weights; the GPU model (fp32 parity mode, same weights, same image)
-    is compared with them: the "Dice parity vs CPU ref" of the metric name."""
+
+def _cpu_threads():
+    """All cores this process may run on, capped by the box's OMP_NUM_THREADS
+    share when the launcher set one (the GPU box sets its per-GPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
+
+
+def cpu_baseline(args, dev):
+    """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py;
+    kind "port") timed on this host: the same synthetic batch
+    (B x 3 x S x S, rank-0 seed), 1 warmup + K timed full train steps (fwd,
+    CombinedLoss, bwd, clip, AdamW), fp32 (the reference semantics) and CPU
+    autocast bf16 (train.py's amp default on CPU).
+
+    The fp32 warmup step's pre-update logits are also the parity reference:
+    the GPU model (fp32 parity mode, same weights, same batch) is compared
+    with them (the "Dice parity vs CPU ref" of the metric name)."""
     from oracle import cpu_ref as R
     from vaeunet_amd import UNet
     from vaeunet_amd.init import seeded_init_
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(threads, 16))
+    threads, affinity = _cpu_threads()
     torch.set_num_threads(threads)
-    model = R.UNetRef(seeded_init_(UNet(3, args.classes), 0).state_dict())
-    opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
-    x, t = synthetic(1, args.size, args.classes, 0, "cpu")
-    x, t = x.contiguous(), t.contiguous()
-    ref_logits, ref_loss, _ = R.train_step(model, opt, x, t)  # warmup; pre-update outputs
-    parity = gpu_parity(args, x, t, ref_logits, ref_loss, dev)
-    t0 = time.perf_counter()
-    for _ in range(n_steps):
-        R.train_step(model, opt, x, t)
-    dt = time.perf_counter() - t0
-    return {"value": round(n_steps / dt, 4), "unit": "images/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"{n_steps} fp32 train steps of UNet(3,{args.classes}) on 1x3x{args.size}x"
-                      f"{args.size} (oracle/cpu_ref.py, torch CPU, {threads} threads)"}, parity
+    B = args.cpu_batch
+    x, t = synthetic(B, args.size, args.classes, 0, "cpu")
+    legs, parity = {}, None
+    for leg in ("fp32", "bf16"):
+        if leg == "bf16" and args.cpu_no_bf16:
+            continue
+        model = R.UNetRef(seeded_init_(UNet(3, args.classes), 0).state_dict())
+        opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
+        ctx = torch.autocast("cpu", dtype=torch.bfloat16) if leg == "bf16" else _Null()
+        t0 = time.perf_counter()
+        with ctx:
+            ref_logits, ref_loss, _ = R.train_step(model, opt, x, t)  # warmup; pre-update outputs
+        warm = time.perf_counter() - t0
+        if leg == "fp32":
+            parity = gpu_parity(args, x, t, ref_logits, ref_loss, dev)
+        # bounded sample: a slow host gets fewer timed steps (stated in "sample")
+        n = args.cpu_steps if warm * args.cpu_steps <= args.cpu_budget_s else max(1, int(args.cpu_budget_s // warm))
+        t0 = time.perf_counter()
+        with ctx:
+            for _ in range(n):
+                R.train_step(model, opt, x, t)
+        dt = time.perf_counter() - t0
+        legs[leg] = {"value": round(B * n / dt, 4), "steps": n, "s_per_step": round(dt / n, 3)}
+    f = legs["fp32"]
+    out = {"value": f["value"], "unit": "images/sec", "cores": threads, "kind": "port",
+           "cpu_model": _cpu_model(), "affinity_cores": affinity,
+           "sample": (f"1 warmup + {f['steps']} timed fp32 train steps (fwd+CombinedLoss+bwd+clip+AdamW) of "
+                      f"UNet(3,{args.classes}) on {B}x3x{args.size}x{args.size} (oracle/cpu_ref.py, torch CPU, "
+                      f"{threads} threads)"),
+           "legs": legs}
+    return out, parity
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def gpu_parity(args, x, t, ref_logits, ref_loss, dev):
-    """GPU UNet (fp32 parity mode: no autocast) vs the CPU oracle on one image."""
+    """GPU UNet (fp32 parity mode: no autocast) vs the CPU oracle, same weights,
+    same batch: Dice of the argmax class maps, the reference's own dice_score
+    semantics (utils/metrics.py:8-35: both tensors thresholded at 0.5), argmax
+    agreement with the reference margin of EVERY flipped pixel, max |dlogit|
+    and |dloss|."""
     from vaeunet_amd import UNet
     from vaeunet_amd.init import seeded_init_
     from vaeunet_amd.loss import CombinedLoss
-    vae = args.model == "vae"
-    if vae:
-        # BASELINE configs[2]: VAE-U-Net (ResNet34 encoder, latent 32, attention, latent
-        # injection "all"), 1 class as train.py's resnet path (train.py:683,693)
-        from vaeunet_amd import UNetResNet
-        from vaeunet_amd.loss import kl_with_free_bits
-        args.classes = 1
-        args.no_cpu_baseline = True
-        model = seeded_init_(UNetResNet(3, 1, pretrained=False), 0).to(dev).to(memory_format=torch.channels_last)
-    else:
-        model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
+    from vaeunet_amd.metrics import dice_score
+    from oracle import cpu_ref as R
+    model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
     model.train()
     xg = x.to(dev).contiguous(memory_format=torch.channels_last)
     tg = t.to(dev).contiguous(memory_format=torch.channels_last)
     with torch.no_grad():
         lg = model(xg)
         loss = CombinedLoss()(lg, tg)
+        ds_gpu = float(dice_score(lg, ref_logits.float().to(dev).contiguous(memory_format=torch.channels_last)))
     lg = lg.float().cpu()
     ref = ref_logits.float()
+    ds_ref = float(R.dice_score(lg.contiguous(), ref.contiguous()))
     cg, cr = lg.argmax(1), ref.argmax(1)
     fg, fr = (cg == 1), (cr == 1)
     den = int(fg.sum() + fr.sum())
     dice = 1.0 if den == 0 else 2.0 * int((fg & fr).sum()) / den
-    return {"dice_class_map": round(dice, 6), "argmax_agree": round(float((cg == cr).float().mean()), 8),
-            "max_abs_logit_diff": float((lg - ref).abs().max()), "loss_abs_diff": abs(float(loss) - float(ref_loss)),
-            "sample": f"1x3x{args.size}x{args.size}, fp32 GPU vs oracle/cpu_ref.py, same weights/input"}
+    flips = cg != cr
+    margins = (ref[:, 0] - ref[:, 1]).abs()[flips]
+    return {"dice_class_map": round(dice, 6), "dice_score_ref_semantics": round(ds_gpu, 7),
+            "dice_score_ref_semantics_cpu": round(ds_ref, 7),
+            "argmax_agree": round(float((~flips).float().mean()), 8), "argmax_flips": int(flips.sum()),
+            "flipped_ref_margins": [float(f"{v:.3e}") for v in margins.tolist()[:32]],
+            "max_flipped_ref_margin": float(margins.max()) if margins.numel() else 0.0,
+            "max_abs_logit_diff": float((lg - ref).abs().max()),
+            "logit_scale": float(ref.abs().max()),
+            "loss_abs_diff": abs(float(loss) - float(ref_loss)),
+            "sample": f"{x.shape[0]}x3x{args.size}x{args.size}, fp32 GPU vs oracle/cpu_ref.py fp32, same weights/input"}
 
 
 def main():
@@ -234,7 +289,7 @@ def main():
 
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline(args, args.cpu_sample_steps, dev)
+        cpu, parity = cpu_baseline(args, dev)
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(imgs, 2),

@@ -193,22 +193,26 @@ int vu_bn_finalize(const float* psum, const float* pm2, int tiles,
                    float eps, float* scale, float* shift, float* save_mean,
                    float* save_invstd, int64_t* num_batches_tracked,
                    float* workspace, void* stream);
-/* eval mode: scale/shift from running statistics */
+/* eval mode: scale/shift from running statistics; save_mean/save_invstd
+ * (optional) receive running_mean and 1/sqrt(running_var + eps) */
 int vu_bn_eval_coeffs(const float* gamma, const float* beta,
                       const float* running_mean, const float* running_var,
-                      float eps, int C, float* scale, float* shift, void* stream);
+                      float eps, int C, float* scale, float* shift,
+                      float* save_mean, float* save_invstd, void* stream);
 /* y = max(0, x*scale[c] + shift[c]) (relu=1) or x*scale+shift (relu=0) */
 int vu_bn_apply(const void* x, int64_t x_stride, void* y, int64_t y_stride,
                 int64_t P, int C, const float* scale, const float* shift,
                 int relu, int dtype, void* stream);
 /* Backward of y = relu(x*scale+shift): per-channel sums of dz and dz*xhat,
  * dz = dy * (z > 0).  Writes dgamma, dbeta (accumulate flag) and the
- * coefficients (k1, k2, k3) with dx = k1*dz + k2*(x - mean) + k3. */
+ * coefficients (k1, k2, k3) with dx = k1*dz + k2*(x - mean) + k3.
+ * train = 1: mean/invstd are the batch statistics (differentiated through);
+ * train = 0: eval mode, they are constants (k2 = k3 = 0). */
 int vu_bn_bwd_reduce(const void* dy, int64_t dy_stride, const void* x,
                      int64_t x_stride, int64_t P, int C, const float* scale,
                      const float* shift, const float* mean,
                      const float* invstd, const float* gamma, int relu,
-                     float* dgamma, float* dbeta, int accumulate,
+                     int train, float* dgamma, float* dbeta, int accumulate,
                      float* coef, float* workspace, int dtype, void* stream);
 /* dx = k1*dz + k2*(x-mean) + k3 (+ add) */
 int vu_bn_bwd_apply(const void* dy, int64_t dy_stride, const void* x,
@@ -317,6 +321,15 @@ int vu_kl_free_bits2(const float* mu, const float* logvar, int B, int L,
 int vu_kl_free_bits(const float* mu, const float* logvar, int B, int L,
                     float free_bits, float* value, float* gmu, float* glogvar,
                     void* stream);
+
+/* dice_score (utils/metrics.py:8-35): a = x > 0.5, b = t > 0.5 over n
+ * elements; *score = 1 if sum a + sum b == 0 else (2*sum(a*b) + epsilon) /
+ * (sum a + sum b + epsilon), computed on the device (no host sync; the
+ * reference's denominator.item() branch is a device select).  counts
+ * (optional) = {sum a, sum b, sum a*b}.  workspace: vu_loss_workspace_bytes */
+int vu_dice_score(const float* x, const float* t, int64_t n, float epsilon,
+                  float* score, double* counts, double* workspace,
+                  void* stream);
 
 /* ---- optimizer (train.py:334,406-411) ---------------------------------- */
 /* sum of squares of n fp32 values into out (fp64, deterministic) */

@@ -165,6 +165,12 @@ def resnet34_features(x, p, pre, bufs, train):
 
 def unet_resnet_forward(x, p, bufs, eps=None, train=True, latent_injection="all"):
     feats = resnet34_features(x, p, "encoder.", bufs, train)
+    return unet_resnet_tail(feats, x.shape[2:], p, bufs, eps, train, latent_injection)
+
+
+def unet_resnet_tail(feats, size, p, bufs, eps=None, train=True, latent_injection="all"):
+    """unet_resnet.py:203-240 given the encoder features (pinned by the
+    vae_*_256 goldens, generated with a fixed-feature encoder double)."""
     xe = feats[-1]
     mu = conv(xe, p, "mu_head.0.").mean(dim=(2, 3))
     logvar = conv(xe, p, "logvar_head.0.").mean(dim=(2, 3))
@@ -185,7 +191,7 @@ def unet_resnet_forward(x, p, bufs, eps=None, train=True, latent_injection="all"
         h = decoder_block(h, feats[-(i + 2)], zs, p, f"decoder_blocks.{i}.", bufs, train,
                           use_latent=bool(inj[i]))
     out = conv(h, p, "final_conv.")
-    return bilinear_ac(out, x.shape[2:]), mu, logvar
+    return bilinear_ac(out, size), mu, logvar
 
 
 # ----------------------------------------------------------------------------

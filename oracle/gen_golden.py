@@ -12,11 +12,18 @@ modules imported are
   kl_with_free_bits 148-170)
 * ``utils.metrics.dice_score`` (8-35)
 * ``unet/unet_resnet.py``: ``timm`` (requirements.txt:2, timm~=1.0.13) is
-  absent here, so the module cannot be imported.  ``DecoderBlock`` (31-101)
-  and ``AttentionGate`` (6-29) do not use timm; their class bodies are
-  compiled from the reference file's AST *without* the ``import timm`` line
-  (no timm stand-in is written).  The ResNet34 encoder and the
-  ``UNetResNet`` wiring stay parity-unpinned.
+  absent here, so the module cannot be imported.  ``DecoderBlock`` (31-101),
+  ``AttentionGate`` (6-29) and ``UNetResNet`` (103-279) are compiled from the
+  reference file's AST *without* the ``import timm`` line.  For
+  ``UNetResNet`` the name ``timm`` is bound to a TEST DOUBLE whose
+  ``create_model`` returns a module that ignores its input and returns five
+  fixed, seeded feature maps (leaf parameters, so their gradients are
+  recorded) with ``feature_info.channels() == [64, 64, 128, 256, 512]``; it
+  restates nothing of timm.  ``torch.randn_like`` is patched to return a
+  fixture ``eps`` during those runs.  This pins everything after the encoder
+  (heads 140-147, reparameterize 191-194, injection modes 157-175/210-234,
+  DecoderBlocks, final conv + interpolate 237-238); the ResNet34 encoder's
+  own arithmetic stays parity-unpinned.
 
 The train-step golden restates ``train.py:381-411`` (the reference's own
 ``train.py`` needs wandb/torchvision and cannot be imported) using the
@@ -42,6 +49,9 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, REF)
 
 from vaeunet_amd.init import seeded_init_  # noqa: E402
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from golden_util import (_rand, seed_vae_tail, vae_feature, vae_feature_shapes,  # noqa: E402
+                         vae_eps, vae_target)
 from unet.unet_parts import AttentionGate, DoubleConv, Down, Up, OutConv  # noqa: E402
 from unet.unet_model import UNet  # noqa: E402
 from utils.loss import dice_loss, CombinedLoss, KLAnnealer, kl_with_free_bits  # noqa: E402
@@ -49,14 +59,6 @@ from utils.metrics import dice_score  # noqa: E402
 
 torch.set_num_threads(8)
 torch.use_deterministic_algorithms(True)
-
-
-def _rng(seed):
-    return np.random.Generator(np.random.PCG64(seed))
-
-
-def _rand(seed, shape, lo=-1.0, hi=1.0):
-    return _rng(seed).uniform(lo, hi, size=shape).astype(np.float32)
 
 
 def _t(a, cl=False):
@@ -79,6 +81,87 @@ def _load_decoder_block():
     ns = {"torch": torch, "nn": nn, "F": F}
     exec(compile(mod, path, "exec"), ns)
     return ns["DecoderBlock"]
+
+
+class _FeatureInfo:
+    def channels(self):
+        return [64, 64, 128, 256, 512]
+
+
+class FixedFeatures(nn.Module):
+    """Test double standing in for ``timm.create_model(..., features_only=True)``:
+    returns five seeded feature maps, whatever the input."""
+
+    def __init__(self, shapes, seed):
+        super().__init__()
+        self.f = nn.ParameterList([nn.Parameter(torch.from_numpy(vae_feature(shape, seed, i)))
+                                   for i, shape in enumerate(shapes)])
+        self.feature_info = _FeatureInfo()
+
+    def forward(self, x):
+        return [f for f in self.f]
+
+
+def _load_unet_resnet(stub_factory):
+    path = os.path.join(REF, "unet", "unet_resnet.py")
+    tree = ast.parse(open(path).read())
+    keep = [n for n in tree.body if isinstance(n, ast.ClassDef)]
+    mod = ast.Module(body=keep, type_ignores=[])
+
+    class _TimmDouble:
+        @staticmethod
+        def create_model(backbone, pretrained=False, features_only=True, in_chans=3, **kw):
+            return stub_factory()
+
+    ns = {"torch": torch, "nn": nn, "F": F, "timm": _TimmDouble}
+    exec(compile(mod, path, "exec"), ns)
+    return ns["UNetResNet"]
+
+
+def gen_vae(mode, B=2, S=256, seed=300):
+    """UNetResNet train-step fixture (fp64 reference run) with a fixed-feature
+    encoder double and a fixture eps; fixtures regenerable from seeds
+    (features, target, eps, parameters) are NOT stored, only outputs."""
+    shapes = vae_feature_shapes(B, S)
+    UNetResNet = _load_unet_resnet(lambda: FixedFeatures(shapes, seed))
+    torch.manual_seed(0)
+    model = UNetResNet(3, 1, pretrained=False, latent_injection=mode)
+    seed_vae_tail(model, seed)
+    model = model.double().train()
+    eps = vae_eps(B, seed).astype(np.float64)
+    target = vae_target(B, S, seed).astype(np.float64)
+    x = torch.zeros(B, 3, S, S, dtype=torch.float64)
+    real = torch.randn_like
+    torch.randn_like = lambda t, **kw: torch.from_numpy(eps).to(t.dtype)
+    try:
+        out, mu, logvar = model(x)
+    finally:
+        torch.randn_like = real
+    crit = CombinedLoss()
+    loss = crit(out, torch.from_numpy(target)) + 1e-3 * kl_with_free_bits(mu, logvar, free_bits=1e-3)
+    loss.backward()
+    rec = {"out": _np(out).astype(np.float32), "mu": _np(mu), "logvar": _np(logvar),
+           "loss": np.float64(loss.item()), "B": np.int64(B), "S": np.int64(S), "seed": np.int64(seed)}
+    names, norms, heads = [], [], []
+    for k, p in model.named_parameters():
+        if k.startswith("encoder."):
+            continue
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        names.append(k)
+        norms.append(float(g.norm()))
+        heads.append(_np(g).reshape(-1)[:16])
+    rec["names"] = np.array(names)
+    rec["gnorm"] = np.array(norms, np.float64)
+    rec["ghead"] = np.stack([np.pad(h, (0, 16 - len(h))) for h in heads])
+    rec["fgnorm"] = np.array([float(f.grad.norm()) if f.grad is not None else 0.0
+                              for f in model.encoder.f], np.float64)
+    rec["fghead"] = np.stack([_np(f.grad).reshape(-1)[:16] if f.grad is not None else np.zeros(16)
+                              for f in model.encoder.f])
+    for k, b in model.named_buffers():
+        if "running" in k:
+            rec[f"buf.{k}"] = _np(b)
+    np.savez_compressed(os.path.join(OUT, f"vae_{mode}_{S}.npz"), **rec)
+    print(f"vae_{mode}_{S}: loss {loss.item():.6f} |mu| {float(mu.abs().mean()):.4f}")
 
 
 def record_module(name, module, inputs, seed, cl=True):
@@ -228,10 +311,27 @@ def gen_unet(n_classes, bilinear, tag, batch=2, size=64, steps=1):
     print(f"{tag}: loss {rec['loss']:.6f} total_norm {rec['total_norm']:.6f}")
 
 
+def gen_decoder_spatial():
+    """DecoderBlock with the reference's spatial z [B, L, h, w] (not constant)."""
+    DecoderBlock = _load_decoder_block()
+    record_module("decoder_zspatial_64_32_48", DecoderBlock(64, 32, 48, 8, True, True, True),
+                  [_rand(34, (2, 64, 4, 4)), _rand(35, (2, 32, 8, 8)), _rand(36, (2, 8, 3, 3))], 37)
+
+
 if __name__ == "__main__":
+    # python oracle/gen_golden.py [parts losses unet vae decoder_spatial]  (default: all)
     os.makedirs(OUT, exist_ok=True)
-    gen_parts()
-    gen_losses()
-    gen_unet(1, False, "unet_c1_64")
-    gen_unet(2, False, "unet_c2_64")
-    gen_unet(1, True, "unet_c1_bilinear_64")
+    what = set(sys.argv[1:]) or {"parts", "losses", "unet", "vae", "decoder_spatial"}
+    if "parts" in what:
+        gen_parts()
+    if "losses" in what:
+        gen_losses()
+    if "unet" in what:
+        gen_unet(1, False, "unet_c1_64")
+        gen_unet(2, False, "unet_c2_64")
+        gen_unet(1, True, "unet_c1_bilinear_64")
+    if "decoder_spatial" in what:
+        gen_decoder_spatial()
+    if "vae" in what:
+        for mode in ("all", "none", "first", "bottleneck"):
+            gen_vae(mode)

@@ -65,6 +65,7 @@ FP8_CASES = [
     (2, [128], 32, 32, 128, 3),
     (2, [64], 32, 64, 64, 3),           # 1024x64 tiles
     (3, [64, 64, 64], 32, 32, 64, 2),   # three sources, odd chunk count
+    (1, [64], 1024, 1024, 64, 0),       # config 5 layer shape: 64->64 at 1x64x1024x1024
 ]
 
 

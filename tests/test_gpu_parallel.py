@@ -1,0 +1,148 @@
+"""Data-parallel product path on the GPU (vaeunet_amd/parallel.py).
+
+* world 2, both ranks on cuda:0, ``gloo`` backend (one card on the test box;
+  RCCL refuses two ranks on one device): the REAL fused UNet engine drives
+  the buckets through ``Mode.notify`` -> ``grad_ready``; the DP gradients must
+  equal the mean over ranks of single-rank gradients, also
+  with grad accumulation x2 where the first micro-batch runs under
+  ``no_sync`` (train.py:401-411);
+* world 1 on the ``nccl`` backend (RCCL): the ReduceOp.AVG branch on the
+  engine path.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard(i):
+    g = torch.Generator().manual_seed(500 + i)
+    x = torch.rand(2, 3, 64, 64, generator=g)
+    t = (torch.rand(2, 1, 64, 64, generator=g) < 0.05).float()
+    return x, t
+
+
+def _grads(model, x, t):
+    from vaeunet_amd.loss import CombinedLoss
+    for p in model.parameters():
+        p.grad = None
+    loss = CombinedLoss()(model(x.cuda().contiguous(memory_format=torch.channels_last)), t.cuda())
+    loss.backward()
+    return [p.grad.detach().clone() for p in model.parameters()]
+
+
+def _worker(rank, world, port, backend, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        from vaeunet_amd import UNet, parallel
+        from vaeunet_amd.init import seeded_init_
+        from vaeunet_amd.loss import CombinedLoss
+        model = seeded_init_(UNet(3, 1), 0).cuda().to(memory_format=torch.channels_last).train()
+        # single-rank gradients of every shard (deterministic kernels: the
+        # same on every rank), before the reducer is attached
+        single = [_grads(model, *_shard(i)) for i in range(2 * world)]
+        red = parallel.attach(model, bucket_bytes=2 * 1024 * 1024)
+        launched = []
+        orig = red._launch
+
+        def spy(bi):
+            launched.append(bi)
+            orig(bi)
+        red._launch = spy
+        res = {}
+        # (a) one micro-batch per rank: shard `rank`
+        for p in model.parameters():
+            p.grad = None
+        red.prepare()
+        x, t = _shard(rank)
+        CombinedLoss()(model(x.cuda().contiguous(memory_format=torch.channels_last)), t.cuda()).backward()
+        n_during = len(launched)
+        red.finish()
+        res["dp"] = [p.grad.detach().cpu() for p in model.parameters()]
+        res["early"] = n_during
+        res["nbuckets"] = len(red.buckets)
+        # (b) accumulation x2: shards world + 2*rank + {0, 1}; micro-batch 0 under no_sync
+        for p in model.parameters():
+            p.grad = None
+        launched.clear()
+        for micro in range(2):
+            x, t = _shard(world + 2 * rank + micro) if world > 1 else _shard(micro)
+            if micro == 0:
+                with red.no_sync():
+                    red.prepare()
+                    loss = CombinedLoss()(model(x.cuda().contiguous(memory_format=torch.channels_last)), t.cuda())
+                    loss.backward()
+                    red.finish()
+                res["nosync_launches"] = len(launched)
+            else:
+                red.prepare()
+                CombinedLoss()(model(x.cuda().contiguous(memory_format=torch.channels_last)), t.cuda()).backward()
+                red.finish()
+        res["acc"] = [p.grad.detach().cpu() for p in model.parameters()]
+        res["single"] = [[g.cpu() for g in s] for s in single]
+        torch.cuda.synchronize()
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, backend):
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join(
+        [os.path.dirname(here), here] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _close(a, b):
+    return (a - b).abs().max().item() <= 1e-6 * max(b.abs().max().item(), 1e-12) + 1e-9
+
+
+def test_dp_world2_gloo_engine_path():
+    world = 2
+    res = _run(world, "gloo")
+    single = res[0]["single"]
+    for r in range(world):
+        rr = res[r]
+        assert rr["nbuckets"] > 1
+        assert rr["early"] > 0, "no bucket was all-reduced during the backward"
+        assert rr["nosync_launches"] == 0, "collective launched inside no_sync"
+        for i, g in enumerate(rr["dp"]):
+            want = (single[0][i] + single[1][i]) / 2
+            assert _close(g, want), ("dp", r, i)
+        for i, g in enumerate(rr["acc"]):
+            want = sum(single[world + k][i] for k in range(2 * world)) / world
+            assert _close(g, want), ("accumulate", r, i)
+
+
+def test_dp_world1_nccl_avg_branch():
+    res = _run(1, "nccl")[0]
+    for i, g in enumerate(res["dp"]):
+        assert _close(g, res["single"][0][i])
+    for i, g in enumerate(res["acc"]):
+        assert _close(g, res["single"][0][i] + res["single"][1][i])

@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import load, state_of, relerr
+from golden_util import (load, state_of, relerr, seed_vae_tail, vae_feature, vae_feature_shapes,
+                         vae_eps, vae_target)
 from oracle import cpu_ref as R
 
 torch.set_num_threads(8)
@@ -28,6 +29,7 @@ BLOCKS = {
     "decoder_64_32_48": lambda i, p, b: R.decoder_block(i[0], i[1], i[2], p, "", b, True),
     "decoder_noattn_64_32_48": lambda i, p, b: R.decoder_block(
         i[0], i[1], i[2], p, "", b, True, use_attention=False, use_latent=False),
+    "decoder_zspatial_64_32_48": lambda i, p, b: R.decoder_block(i[0], i[1], i[2], p, "", b, True),
 }
 
 
@@ -136,3 +138,49 @@ def test_unet_train_step_matches_reference(tag, nc, bil):
         ev = model.forward(x, train=False)
     # after the update (noise-sign Adam steps above), eval-mode logits: 1e-3
     assert relerr(ev, rec["eval_logits"]) < 1e-3
+
+
+def vae_tail_params(mode, seed):
+    """Seeded UNetResNet tail parameters keyed like the reference state_dict
+    (the vaeunet_amd module is used only as a CPU parameter holder)."""
+    from vaeunet_amd import UNetResNet
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        m = UNetResNet(3, 1, pretrained=False, latent_injection=mode)
+    seed_vae_tail(m, seed)
+    return {k: v for k, v in m.state_dict().items() if not k.startswith("encoder.")}
+
+
+@pytest.mark.parametrize("mode", ["all", "none", "first", "bottleneck"])
+def test_vae_tail_matches_reference(mode):
+    """UNetResNet after the encoder (unet_resnet.py:203-240; rows J/K/L/N) vs the
+    reference's own class run in fp64 with a fixed-feature encoder double."""
+    rec = load(f"vae_{mode}_256")
+    B, S, seed = int(rec["B"]), int(rec["S"]), int(rec["seed"])
+    st = vae_tail_params(mode, seed)
+    p = {k: v.double().requires_grad_(True) for k, v in st.items()
+         if "running" not in k and "num_batches" not in k}
+    bufs = {k: (v.double() if v.is_floating_point() else v.clone()) for k, v in st.items()
+            if "running" in k or "num_batches" in k}
+    feats = [torch.from_numpy(vae_feature(sh, seed, i)).double().requires_grad_(True)
+             for i, sh in enumerate(vae_feature_shapes(B, S))]
+    eps = torch.from_numpy(vae_eps(B, seed)).double()
+    t = torch.from_numpy(vae_target(B, S, seed)).double()
+    out, mu, lv = R.unet_resnet_tail(feats, (S, S), p, bufs, eps=eps, latent_injection=mode)
+    loss = R.combined_loss(out, t) + 1e-3 * R.kl_with_free_bits(mu, lv, 1e-3)
+    loss.backward()
+    assert relerr(out.detach(), rec["out"]) < 1e-5
+    assert relerr(mu.detach(), rec["mu"]) < 1e-9
+    assert relerr(lv.detach(), rec["logvar"]) < 1e-9
+    assert abs(loss.item() - float(rec["loss"])) < 1e-9
+    for k, gn in zip(rec["names"], rec["gnorm"]):
+        g = p[str(k)].grad
+        mine = float(g.norm()) if g is not None else 0.0
+        assert abs(mine - gn) <= 1e-6 * max(gn, 1e-12) + 1e-12, k
+    for i, f in enumerate(feats):
+        mine = float(f.grad.norm()) if f.grad is not None else 0.0
+        assert abs(mine - rec["fgnorm"][i]) <= 1e-6 * max(rec["fgnorm"][i], 1e-12) + 1e-12, i
+    for k, v in bufs.items():
+        if f"buf.{k}" in rec:
+            assert relerr(v, rec[f"buf.{k}"]) < 1e-9, k

@@ -45,6 +45,8 @@ def _worker(rank, world, port, out_q, bucket_bytes):
         params = list(m.parameters())
         results = []
         for step in range(2):
+            for q in params:
+                q.grad = None  # zero_grad(set_to_none=True) between optimizer steps
             red.prepare()
             launched = []
             # engine order: reverse registration; "accumulate" into the bound views
@@ -96,3 +98,68 @@ def test_bucketed_allreduce_average_gloo(bucket_bytes):
                 assert torch.allclose(g, torch.full_like(g, mean)), (step, i)
             if bucket_bytes == 4096:
                 assert early, "buckets were not launched during the backward"
+
+
+def _accum_worker(rank, world, port, out_q):
+    """train.py:401-411 grad-accumulation x2 under DP: the first micro-batch runs
+    inside no_sync (no collective, local accumulation), the second reduces the
+    sum; the result must be the average over ranks of both micro-batches."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vaeunet_amd.parallel import GradBucketReducer
+        m = _model()
+        red = GradBucketReducer(m.parameters(), bucket_bytes=4096)
+        params = list(m.parameters())
+        out = []
+        for opt_step in range(2):
+            for q in params:
+                q.grad = None
+            for micro in range(2):
+                ctx = red.no_sync() if micro == 0 else _nullctx()
+                with ctx:
+                    red.prepare()
+                    for i, p in enumerate(reversed(params)):
+                        p.grad.add_(torch.full_like(p, float(10 * rank + micro + 1 + opt_step)) * (i + 1))
+                        red.grad_ready([p])
+                    if micro == 0:
+                        assert not red._handles, "collective launched inside no_sync"
+                    red.finish()
+            out.append([p.grad.detach().numpy().copy() for p in params])
+        out_q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def test_grad_accumulation_no_sync_gloo():
+    world = 2
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join(
+        [os.path.dirname(here), here] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        for opt_step, grads in enumerate(res[r]):
+            n = len(grads)
+            for i, g in enumerate(grads):
+                k = n - i
+                # sum over the two micro-batches, averaged over the two ranks
+                want = sum(float(10 * rr + mb + 1 + opt_step) for rr in range(world) for mb in range(2)) / world * k
+                assert torch.allclose(torch.from_numpy(g), torch.full_like(torch.from_numpy(g), want)), (r, opt_step, i)

@@ -79,10 +79,10 @@ _SIGS = {
     "vu_bn_finalize": (_i, [_p, _p, _i, _l, _l, _i, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p,
                             _p, _p, _p]),
     "vu_bn_finalize_workspace_bytes": (_l, [_i, _i]),
-    "vu_bn_eval_coeffs": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p]),
+    "vu_bn_eval_coeffs": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p, _p, _p]),
     "vu_bn_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _i, _i, _p]),
-    "vu_bn_bwd_reduce": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _p, _p, _i, _p,
-                              _p, _i, _p]),
+    "vu_bn_bwd_reduce": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i,
+                              _p, _p, _i, _p]),
     "vu_bn_bwd_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _i, _p, _l, _i, _p]),
     "vu_reduce_workspace_bytes": (_l, [_l, _i]),
     "vu_chan_sum": (_i, [_p, _l, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
@@ -108,6 +108,7 @@ _SIGS = {
     "vu_bce_dice_bwd": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p]),
     "vu_kl_free_bits2": (_i, [_p, _p, _i, _i, _f, _p, _p, _p, _p, _p]),
     "vu_sumsq": (_i, [_p, _l, _p, _p, _p]),
+    "vu_dice_score": (_i, [_p, _p, _l, _f, _p, _p, _p, _p]),
     "vu_mt_chunk_elems": (_l, []),
     "vu_mt_grad_norm": (_i, [_p, _i, _l, _f, _p, _p, _p, _p]),
     "vu_mt_scale_grads": (_i, [_p, _i, _l, _p, _p]),

@@ -150,13 +150,15 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
 }
 
 __global__ void bn_eval_kernel(const float* gamma, const float* beta, const float* rm, const float* rv,
-                               float eps, int C, float* scale, float* shift) {
+                               float eps, int C, float* scale, float* shift, float* smean, float* sinvstd) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float invstd = 1.f / sqrtf(rv[c] + eps);
   float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   scale[c] = g * invstd;
   shift[c] = b - rm[c] * g * invstd;
+  if (smean) smean[c] = rm[c];
+  if (sinvstd) sinvstd[c] = invstd;
 }
 
 // Fixed-channel mapping: V = C/8 vectors per pixel, V a power of two <= 256.
@@ -300,7 +302,7 @@ __global__ void chan_final_sum(const float* part, int nblk, int C, float* out, i
 
 __global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, int accumulate,
-                             float* coef) {
+                             float* coef, int train) {
   int c = blockIdx.x * 32 + (threadIdx.x & 31);
   double s[2];
   colsum32<2>(part, nblk, 2 * (int64_t)C, C, c, c < C, s);
@@ -309,8 +311,8 @@ __global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, cons
   float is = invstd[c];
   float k1 = g * is;
   coef[c] = k1;
-  coef[C + c] = (float)(-(double)k1 * is * s[1] / (double)P);
-  coef[2 * C + c] = (float)(-(double)k1 * s[0] / (double)P);
+  coef[C + c] = train ? (float)(-(double)k1 * is * s[1] / (double)P) : 0.f;
+  coef[2 * C + c] = train ? (float)(-(double)k1 * s[0] / (double)P) : 0.f;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s[1] : (float)s[1];
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s[0] : (float)s[0];
 }
@@ -447,9 +449,9 @@ extern "C" int vu_bn_finalize(const float* psum, const float* pm2, int tiles, in
 
 extern "C" int vu_bn_eval_coeffs(const float* gamma, const float* beta, const float* running_mean,
                                  const float* running_var, float eps, int C, float* scale,
-                                 float* shift, void* stream) {
+                                 float* shift, float* save_mean, float* save_invstd, void* stream) {
   hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, gamma,
-                     beta, running_mean, running_var, eps, C, scale, shift);
+                     beta, running_mean, running_var, eps, C, scale, shift, save_mean, save_invstd);
   return (int)hipGetLastError();
 }
 
@@ -479,16 +481,16 @@ extern "C" int vu_bn_apply(const void* x, int64_t xs, void* y, int64_t ys, int64
 
 extern "C" int vu_bn_bwd_reduce(const void* dy, int64_t dys, const void* x, int64_t xs, int64_t P,
                                 int C, const float* scale, const float* shift, const float* mean,
-                                const float* invstd, const float* gamma, int relu, float* dgamma,
-                                float* dbeta, int accumulate, float* coef, float* workspace,
-                                int dtype, void* stream) {
+                                const float* invstd, const float* gamma, int relu, int train,
+                                float* dgamma, float* dbeta, int accumulate, float* coef,
+                                float* workspace, int dtype, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   RedArgs r{dy, dys, x, xs, P, C, scale, shift, mean, invstd, relu, workspace, 0, 0, 0, 0, 0, 0};
   int nblk = 0, rc;
   rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk) : launch_partial<float, 1>(r, st, nblk);
   if (rc) return rc;
   hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, C, P,
-                     gamma, invstd, dgamma, dbeta, accumulate, coef);
+                     gamma, invstd, dgamma, dbeta, accumulate, coef, train);
   return (int)hipGetLastError();
 }
 

@@ -155,6 +155,44 @@ __global__ void sum_stage2(const double* ws, int nblk, double* out, int accumula
   out[0] = accumulate ? out[0] + s : s;
 }
 
+// Hard Dice (utils/metrics.py:8-35): a = (x > 0.5), b = (t > 0.5) over the
+// whole tensor (reduce_batch_first only changes the view, not the sums);
+// exact integer counts, so the result is order-independent.
+__global__ void dice_score_stage1(const float* x, const float* t, int64_t n, unsigned long long* ws) {
+  __shared__ unsigned long long sh[3][4];
+  unsigned long long a = 0, b = 0, ab = 0;
+  for (int64_t i = (int64_t)blockIdx.x * LBLK + threadIdx.x; i < n; i += (int64_t)gridDim.x * LBLK) {
+    const bool pa = x[i] > 0.5f, pb = t[i] > 0.5f;
+    a += pa;
+    b += pb;
+    ab += pa && pb;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    ab += __shfl_xor(ab, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sh[0][w] = a; sh[1][w] = b; sh[2][w] = ab; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int k = threadIdx.x;
+    ws[blockIdx.x * 3 + k] = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
+  }
+}
+
+__global__ void dice_score_stage2(const unsigned long long* ws, int nblk, float epsilon, float* score,
+                                  double* counts) {
+  if (threadIdx.x != 0) return;
+  unsigned long long a = 0, b = 0, ab = 0;
+  for (int i = 0; i < nblk; ++i) { a += ws[i * 3]; b += ws[i * 3 + 1]; ab += ws[i * 3 + 2]; }
+  // fp32 arithmetic as the reference: (2*I + eps) / (sum a + sum b + eps)
+  const float I = (float)ab, den = (float)a + (float)b;
+  score[0] = (a + b == 0) ? 1.f : (2.f * I + epsilon) / (den + epsilon);
+  if (counts) { counts[0] = (double)a; counts[1] = (double)b; counts[2] = (double)ab; }
+}
+
 int nblocks(int64_t n) {
   int64_t b = (n + LBLK * 4 - 1) / (LBLK * 4);
   if (b > LNB) b = LNB;
@@ -208,5 +246,15 @@ extern "C" int vu_sumsq(const float* x, int64_t n, double* out, double* workspac
   int nb = nblocks(n);
   hipLaunchKernelGGL(sumsq_stage1, dim3(nb), dim3(LBLK), 0, st, x, n, workspace);
   hipLaunchKernelGGL(sum_stage2, dim3(1), dim3(LBLK), 0, st, workspace, nb, out, 0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_dice_score(const float* x, const float* t, int64_t n, float epsilon, float* score,
+                             double* counts, double* workspace, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int nb = nblocks(n);
+  unsigned long long* ws = reinterpret_cast<unsigned long long*>(workspace);
+  hipLaunchKernelGGL(dice_score_stage1, dim3(nb), dim3(LBLK), 0, st, x, t, n, ws);
+  hipLaunchKernelGGL(dice_score_stage2, dim3(1), dim3(64), 0, st, ws, nb, epsilon, score, counts);
   return (int)hipGetLastError();
 }

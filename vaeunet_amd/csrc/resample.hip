@@ -219,9 +219,10 @@ __global__ void upsample_bwd_kernel(const T* dy, int64_t dys, int N, int Hi, int
     for (int yy = ylo; yy <= yhi; ++yy) {
       float wy = ac_w(yy, i, sh, Hi);
       if (wy == 0.f) continue;
+      if (yy + py < 0 || yy + py >= Hp) continue;  // cropped by a negative F.pad
       for (int xx = xlo; xx <= xhi; ++xx) {
         float wx = ac_w(xx, j, sw, Wi);
-        if (wx == 0.f) continue;
+        if (wx == 0.f || xx + px < 0 || xx + px >= Wp) continue;
         const T* src = dy + (((int64_t)n * Hp + yy + py) * Wp + xx + px) * dys + c;
         float wgt = wy * wx;
         if (VW == 8) {

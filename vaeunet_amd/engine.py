@@ -14,6 +14,8 @@ return None for parameters.  A ``grad_ready`` hook on the run mode lets the
 data-parallel reducer start all-reducing a block's gradients while the
 backward of the blocks below it is still running.
 """
+import warnings
+
 import torch
 
 from . import kernels as K
@@ -40,12 +42,26 @@ class Mode:
             self.grad_ready([p for p in params if p is not None and p.grad is not None])
 
 
+_FP16_WARNED = False
+
+
 def current_mode(device, grad_ready=None):
-    """bf16 under torch.autocast (train.py:385), fp32 otherwise (parity)."""
+    """bf16 under torch.autocast (train.py:385), fp32 otherwise (parity).
+
+    The reference's ``torch.autocast('cuda')`` defaults to float16 (with a
+    GradScaler).  The kernels have no fp16 storage path: an fp16 autocast
+    region runs in bf16 (same 16-bit storage, 8-bit exponent, no overflow
+    risk) and says so once.  GradScaler keeps working: it only scales the
+    loss and unscales fp32 gradients."""
+    global _FP16_WARNED
     if device.type != "cuda":
         raise RuntimeError("vaeunet_amd runs on MI355X (HIP) devices only; got "
                            f"a tensor on {device}")
     ac = torch.is_autocast_enabled("cuda")
+    if ac and torch.get_autocast_dtype("cuda") == torch.float16 and not _FP16_WARNED:
+        _FP16_WARNED = True
+        warnings.warn("vaeunet_amd: float16 autocast requested; the HIP kernels compute this "
+                      "region with bf16 storage (fp32 accumulation) instead")
     return Mode(BF16 if ac else F32, device, grad_ready)
 
 
@@ -215,15 +231,17 @@ def bn_coef(bn, st, C_):
 
 
 def bn_bwd(dy, x, coef, bn, relu, M, dx=None):
-    if not bn.training:
-        raise NotImplementedError("backward through eval-mode BatchNorm")
+    """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
+    batch statistics; eval mode (running statistics, constants) gives
+    dx = gamma*invstd*dz and the same dgamma/dbeta sums."""
     gw, accw = grad_sink(bn.weight)
     gb, accb = grad_sink(bn.bias)
     if gw is not None and gb is not None and accw != accb:
         raise RuntimeError("inconsistent BatchNorm grad state")
     if dx is None:
         dx = torch.empty_like(x)
-    K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, accw or accb, dx, K.dcode(x.dtype))
+    K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, accw or accb, dx, K.dcode(x.dtype),
+                  train=bn.training)
     return dx
 
 
@@ -353,7 +371,7 @@ def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
     gw, accw = grad_sink(bnp.weight)
     gb, _ = grad_sink(bnp.bias)
     dq = torch.empty_like(q)
-    K.bn_backward(dbnq, q, cq, bnp.weight, False, gw, gb, accw, dq, F32)
+    K.bn_backward(dbnq, q, cq, bnp.weight, False, gw, gb, accw, dq, F32, train=bnp.training)
     # psi conv + ReLU backward -> ds (grad of g1 + x1)
     ds = M.act(N, F, H, W)
     gwp, accp = grad_sink(wp.weight)
@@ -388,18 +406,28 @@ def up_fwd(M, mod, x1, x2):
     bilinear = isinstance(mod.up, torch.nn.Upsample)
     uh, uw = 2 * h, 2 * w
     dy_, dx_ = H - uh, W - uw
-    if dy_ < 0 or dx_ < 0:
-        raise NotImplementedError("Up with an upsampled map larger than the skip (negative pad)")
+    # F.pad(x1, [dx//2, dx - dx//2, dy//2, dy - dy//2]): the upsampled map sits
+    # at (dy//2, dx//2) of the skip-sized canvas; a negative offset crops
     py, px = dy_ // 2, dx_ // 2
+    crop = dy_ < 0 or dx_ < 0
     if bilinear:
         cu = x1.shape[1]
         u = M.act(N, cu, H, W)
         K.upsample_fwd(x1, u, uh, uw, py, px, M.d)
     else:
         cu = mod.up.out_channels
-        u = M.zeros(N, cu, H, W) if (dy_ or dx_) else M.act(N, cu, H, W)
-        K.gemm_fwd(K.gather1x1([x1]), wT_fwd(mod.up.weight, M.d), 4 * cu, u, M.d,
-                   bias=mod.up.bias, convT=(H, W, py, px, cu))
+        if crop:
+            # full ConvT map, then an exact shifted copy into the canvas (the
+            # align_corners resampler at scale 1 with the pad offsets)
+            uf = M.act(N, cu, uh, uw)
+            K.gemm_fwd(K.gather1x1([x1]), wT_fwd(mod.up.weight, M.d), 4 * cu, uf, M.d,
+                       bias=mod.up.bias, convT=(uh, uw, 0, 0, cu))
+            u = M.act(N, cu, H, W)
+            K.upsample_fwd(uf, u, uh, uw, py, px, M.d)
+        else:
+            u = M.zeros(N, cu, H, W) if (dy_ or dx_) else M.act(N, cu, H, W)
+            K.gemm_fwd(K.gather1x1([x1]), wT_fwd(mod.up.weight, M.d), 4 * cu, u, M.d,
+                       bias=mod.up.bias, convT=(H, W, py, px, cu))
     x2a, satt = attention_fwd(M, mod.attention, u, x2)
     out, sdc = double_conv_fwd(M, mod.conv.double_conv, [x2a, u])
     return out, (x1, x2, u, (py, px, uh, uw), satt, sdc)
@@ -418,6 +446,12 @@ def up_bwd(M, mod, saved, dout):
         dx1 = torch.empty_like(x1)
         K.upsample_bwd(du, dx1, uh, uw, py, px, False, M.d)
     else:
+        if py < 0 or px < 0:
+            # gradient of the crop: scatter du back onto the full ConvT map
+            duf = M.act(N, cu, uh, uw)
+            K.upsample_bwd(du, duf, uh, uw, py, px, False, M.d)
+            du, py, px = duf, 0, 0
+            H, W = uh, uw
         g, acc = grad_sink(mod.up.weight)
         if g is not None:
             K.gemm_wgrad(K.gather1x1([x1]), K.gather_convT(du, N, h, w, py, px), x1.shape[1], 4 * cu,

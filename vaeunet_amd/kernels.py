@@ -305,9 +305,10 @@ def bn_finalize(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps):
 
 
 def bn_eval(C_, gamma, beta, rmean, rvar, eps):
+    """Eval-mode coefficients; rows: scale, shift, running mean, 1/sqrt(running var + eps)."""
     coef = torch.empty((4, C_), dtype=torch.float32, device=rmean.device)
     call("vu_bn_eval_coeffs", ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), eps, C_,
-         ptr(coef[0]), ptr(coef[1]), stream())
+         ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), stream())
     return coef
 
 
@@ -318,8 +319,9 @@ def bn_apply(x, y, coef, relu, dtype):
     return y
 
 
-def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype):
-    """dx = BN(+ReLU) backward; writes/accumulates dgamma, dbeta."""
+def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
+    """dx = BN(+ReLU) backward; writes/accumulates dgamma, dbeta.  train=False:
+    the statistics are constants (eval mode)."""
     N, Cc, H, W = x.shape
     P = N * H * W
     dev = x.device
@@ -328,7 +330,8 @@ def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype):
                      device=dev)
     call("vu_bn_bwd_reduce", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
          ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
-         ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype, stream())
+         1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype,
+         stream())
     call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
          ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
          stream())

@@ -20,6 +20,8 @@ SyncBN; DDP-without-SyncBN semantics: every rank normalises with its own
 shard's batch statistics).  Parameters are broadcast from rank 0 once at
 construction.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -49,33 +51,70 @@ class GradBucketReducer:
                 self.where[id(p)] = bi
         self._pending = None
         self._handles = []
+        self._sync = True
         with torch.no_grad():
             for p in self.params:
                 dist.broadcast(p.data, src=0, group=group)
 
     def _bind(self):
-        """Point every .grad at its slot of the flat bucket buffer (zeroed)."""
+        """Point every .grad at its slot of the flat bucket buffer.
+
+        torch semantics are kept: a gradient accumulates until it is reset.
+        A parameter whose ``.grad`` is None (``zero_grad(set_to_none=True)``)
+        gets its slot zeroed; one already bound keeps its contents (gradient
+        accumulation over micro-batches, train.py:401-411); a foreign tensor
+        is copied into the slot."""
         for bi, plist in enumerate(self.buckets):
             flat = self.flats[bi]
-            flat.zero_()
+            fresh = all(p.grad is None for p in plist)
+            if fresh:
+                flat.zero_()  # one launch per bucket after zero_grad(set_to_none=True)
             off = 0
             for p in plist:
                 n = p.numel()
                 view = flat[off:off + n].view(p.shape)
-                if p.grad is None or p.grad.data_ptr() != view.data_ptr():
-                    # keep the parameter's memory layout (channels_last weights)
-                    if p.dim() == 4 and not p.is_contiguous():
-                        view = flat[off:off + n].view(p.shape[0], p.shape[2], p.shape[3],
-                                                      p.shape[1]).permute(0, 3, 1, 2)
+                # keep the parameter's memory layout (channels_last weights)
+                if p.dim() == 4 and not p.is_contiguous():
+                    view = flat[off:off + n].view(p.shape[0], p.shape[2], p.shape[3],
+                                                  p.shape[1]).permute(0, 3, 1, 2)
+                if p.grad is None:
+                    if not fresh:
+                        view.zero_()
+                    p.grad = view
+                elif p.grad.data_ptr() != view.data_ptr():
+                    view.copy_(p.grad)
                     p.grad = view
                 off += n
 
+    def zero_grad(self):
+        """Zero every bucket in place (the bound .grad views included)."""
+        for flat in self.flats:
+            flat.zero_()
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Micro-batches run inside accumulate their gradients locally (no
+        collective); the next synchronised backward all-reduces the sum --
+        DDP's ``no_sync`` for the reference's grad-accumulation x2
+        (train.py:401,406)."""
+        old = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = old
+
     def prepare(self):
-        """Call before the forward of a step whose backward should be reduced."""
+        """Call before the forward of every micro-batch (inside or outside
+        ``no_sync``): binds the gradient views; arms the bucket counters only
+        when this backward is to be reduced."""
         self._bind()
-        self._pending = [len(b) for b in self.buckets]
-        self._seen = set()
         self._handles = []
+        if self._sync:
+            self._pending = [len(b) for b in self.buckets]
+            self._seen = set()
+        else:
+            self._pending = None
 
     def grad_ready(self, params):
         """Engine callback: these parameters' gradients are final for this step."""
@@ -100,7 +139,10 @@ class GradBucketReducer:
             self._handles.append((h, flat if self.average else None))
 
     def finish(self):
-        """Launch any bucket the engine did not report, then fence on all of them."""
+        """Launch any bucket the engine did not report, then fence on all of
+        them (a no-op after a ``no_sync`` micro-batch)."""
+        if not self._sync:
+            return
         if self._pending is not None:
             for bi, left in enumerate(self._pending):
                 if left > 0:

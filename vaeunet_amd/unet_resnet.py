@@ -111,21 +111,33 @@ class DecoderBlock(nn.Module):
         self.conv2 = _cbr3x3(out_channels, out_channels)
 
     def forward(self, x, skip, z):
+        """z: [B, L], [B, L, 1, 1] or the reference's spatial z_spatial
+        [B, L, h, w] (utils/vae_utils.py:55-65, visualize_vae.py:71-77), which
+        is resampled to the skip size exactly as unet_resnet.py:93 does."""
         M = E.current_mode(x.device)
-        zv = z.reshape(z.shape[0], -1).float().contiguous()
-        if zv.shape[1] != (self.z_proj[0].in_channels if self.use_latent else zv.shape[1]):
-            raise ValueError("z must be [B, latent_dim] or [B, latent_dim, 1, 1]")
+        spatial = z.dim() == 4 and z.shape[2] * z.shape[3] > 1
+        if self.use_latent and (z.shape[1] if z.dim() > 1 else -1) != self.z_proj[0].in_channels:
+            raise ValueError("z must be [B, latent_dim] or [B, latent_dim, h, w]")
+        zv = None if spatial else z.reshape(z.shape[0], -1).float().contiguous()
         inputs = (x, skip, z) if skip is not None else (x, z)
 
         def fwd(inp):
             xa = E.to_act(M, inp[0])
             sa = E.to_act(M, inp[1]) if skip is not None else None
-            return V.decoder_fwd(M, self, xa, sa, zv)
+            za = E.to_act(M, inp[-1]) if spatial else zv
+            out, st = V.decoder_fwd(M, self, xa, sa, za)
+            return out, (st, za)
 
         def bwd(state, dout):
-            dx, dskip, dz = V.decoder_bwd(M, self, state, act_grad(M, dout))
+            st, za = state
+            dx, dskip, dz = V.decoder_bwd(M, self, st, act_grad(M, dout), za)
             gx = E.from_act(dx, x)
-            gz = dz.view(z.shape).to(z.dtype) if dz is not None else None
+            if dz is None:
+                gz = None
+            elif spatial:
+                gz = E.from_act(dz, z)
+            else:
+                gz = dz.view(z.shape).to(z.dtype)
             if skip is None:
                 return gx, gz
             gs = E.from_act(dskip, skip) if dskip is not None else None
@@ -214,6 +226,8 @@ class UNetResNet(nn.Module):
         M = E.current_mode(x.device, self.grad_ready)
         E.refresh_weights(self.parameters())
         eps = self._eps(x.shape[0], x.device)
+        if not isinstance(self.encoder, ResNet34Features):
+            return self._forward_foreign_encoder(M, x, eps)
         params = [p for p in self.parameters() if p.requires_grad]
         if not (torch.is_grad_enabled() and (params or x.requires_grad)):
             out, mu, lv, _ = V.vae_fwd(M, self, x, eps)
@@ -228,6 +242,28 @@ class UNetResNet(nn.Module):
             V.vae_bwd(M, self, state, dout, dmu, dlv)
             return (None,)
         return BlockFn.apply(Runner(fwd, bwd), 1, x, *params)
+
+    def _forward_foreign_encoder(self, M, x, eps):
+        """``self.encoder`` replaced by any module returning the five feature
+        maps (a timm ``features_only`` backbone, or a test double): it runs
+        under torch autograd, everything after it (heads, reparameterize,
+        bottleneck, decoder, final conv + resize) is the fused HIP tail."""
+        feats = list(self.encoder(x))
+        Hin, Win = x.shape[2], x.shape[3]
+        params = [p for n, p in self.named_parameters() if not n.startswith("encoder.") and p.requires_grad]
+
+        def fwd(inp):
+            fa = [E.to_act(M, f) for f in inp]
+            out, mu, lv, st = V.vae_tail_fwd(M, self, fa, Hin, Win, eps)
+            return (out, mu, lv), st
+
+        if not (torch.is_grad_enabled() and (params or any(f.requires_grad for f in feats))):
+            return fwd(feats)[0]
+
+        def bwd(state, douts):
+            dfe = V.vae_tail_bwd(M, self, state, *douts)
+            return tuple(E.from_act(d, f) if d is not None else None for d, f in zip(dfe, feats))
+        return BlockFn.apply(Runner(fwd, bwd), len(feats), *feats, *params)
 
     def encode(self, x):
         M = E.current_mode(x.device)

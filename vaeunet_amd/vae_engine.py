@@ -270,7 +270,13 @@ def decoder_fwd(M, blk, x, skip, z):
         srcs.append(sk)
     szp = None
     if blk.use_latent:
-        zb = latent_map(M, z, N, H, W)
+        if z.dim() == 2:
+            # interpolate([B, L, 1, 1] -> (H, W), align_corners) is a broadcast
+            zb = latent_map(M, z, N, H, W)
+        else:
+            # a spatial z [B, L, h, w] (the reference's z_spatial, unet_resnet.py:93)
+            zb = M.act(N, z.shape[1], H, W)
+            K.upsample_fwd(z, zb, H, W, 0, 0, M.d)
         zp, szp = cbr1x1_fwd(M, blk.z_proj, zb)
         srcs.append(zp)
     a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1])
@@ -278,8 +284,9 @@ def decoder_fwd(M, blk, x, skip, z):
     return a2, (x, skip, xu, srcs, satt, szp, a1, s1, s2)
 
 
-def decoder_bwd(M, blk, saved, dout):
-    """-> (dx, dskip or None, dz [B, L] fp32 or None)."""
+def decoder_bwd(M, blk, saved, dout, z=None):
+    """-> (dx, dskip or None, dz or None): dz is [B, L] fp32 for a vector z,
+    an NHWC map like ``z`` for a spatial one."""
     x, skip, xu, srcs, satt, szp, a1, s1, s2 = saved
     da1 = E.conv_bn_relu_bwd(M, [a1], blk.conv2[0], blk.conv2[1], s2, dout, True)
     dsrc = E.conv_bn_relu_bwd(M, srcs, blk.conv1[0], blk.conv1[1], s1, da1, True)
@@ -297,7 +304,11 @@ def decoder_bwd(M, blk, saved, dout):
     if blk.use_latent:
         dzp = dsrc[:, off:]
         dzb = cbr1x1_bwd(M, blk.z_proj, szp, dzp)
-        dz = sample_sum(M, dzb)
+        if z is not None and z.dim() == 4:
+            dz = torch.empty_like(z)
+            K.upsample_bwd(dzb, dz, dzb.shape[2], dzb.shape[3], 0, 0, False, M.d)
+        else:
+            dz = sample_sum(M, dzb)
     dx = torch.empty_like(x)
     H, W = xu.shape[2], xu.shape[3]
     K.upsample_bwd(dsrc[:, :cx], dx, H, W, 0, 0, False, M.d)
@@ -312,11 +323,26 @@ def vae_fwd(M, model, x, eps):
     cp = (cin + 7) // 8 * 8
     xa = E.to_act(M, x, cp)
     feats, senc = encoder_fwd(M, model.encoder, xa, cp)
+    out, mu, logvar, stail = vae_tail_fwd(M, model, feats, Hin, Win, eps)
+    return out, mu, logvar, (senc, stail, cin)
+
+
+def vae_bwd(M, model, state, dout, dmu, dlogvar):
+    senc, stail, cin = state
+    dfeats = vae_tail_bwd(M, model, stail, dout, dmu, dlogvar)
+    encoder_bwd(M, model.encoder, senc, dfeats, cin)
+
+
+def vae_tail_fwd(M, model, feats, Hin, Win, eps):
+    """Everything after the encoder (unet_resnet.py:203-240): heads, reparameterize,
+    bottleneck, the four DecoderBlocks, final_conv and the resize to the input size."""
     f4 = feats[-1]
+    N = f4.shape[0]
+    dev = f4.device
     H4, W4 = f4.shape[2], f4.shape[3]
     pooled = sample_sum(M, f4, 1.0 / (H4 * W4))
     L = model.latent_dim
-    mu = torch.empty((N, L), dtype=torch.float32, device=x.device)
+    mu = torch.empty((N, L), dtype=torch.float32, device=dev)
     logvar = torch.empty_like(mu)
     for head, out in ((model.mu_head[0], mu), (model.logvar_head[0], logvar)):
         K.call("vu_linear_small_fwd", K.ptr(pooled), N, f4.shape[1], K.ptr(head.weight),
@@ -337,14 +363,15 @@ def vae_fwd(M, model, x, eps):
         h, s = decoder_fwd(M, blk, h, skip, z)
         sdec.append(s)
     small, sfc = E.outconv_fwd(M, model.final_conv, h)
-    out = torch.empty((N, small.shape[1], Hin, Win), dtype=torch.float32, device=x.device,
+    out = torch.empty((N, small.shape[1], Hin, Win), dtype=torch.float32, device=dev,
                       memory_format=torch.channels_last)
     K.upsample_fwd(small, out, Hin, Win, 0, 0, F32)
-    return out, mu, logvar, (senc, feats, pooled, eps, logvar, szi, sdec, sfc, small, cin)
+    return out, mu, logvar, (feats, pooled, eps, logvar, szi, sdec, sfc, small)
 
 
-def vae_bwd(M, model, state, dout, dmu, dlogvar):
-    senc, feats, pooled, eps, logvar, szi, sdec, sfc, small, cin = state
+def vae_tail_bwd(M, model, state, dout, dmu, dlogvar):
+    """-> gradients of the five encoder features (None where none flows)."""
+    feats, pooled, eps, logvar, szi, sdec, sfc, small = state
     N = small.shape[0]
     dsmall = torch.empty_like(small)
     if dout is not None:
@@ -355,11 +382,11 @@ def vae_bwd(M, model, state, dout, dmu, dlogvar):
     dh = E.outconv_bwd(M, model.final_conv, sfc, dsmall)
     L = model.latent_dim
     dz = torch.zeros((N, L), dtype=torch.float32, device=small.device)
-    dfeats = [None] * 5
+    dfeats = [None] * len(feats)
     for i in range(len(model.decoder_blocks) - 1, -1, -1):
         dh, dskip, dzi = decoder_bwd(M, model.decoder_blocks[i], sdec[i], dh)
         if dskip is not None:
-            dfeats[3 - i] = dskip
+            dfeats[len(feats) - 2 - i] = dskip
         if dzi is not None:
             K.call("vu_sample_broadcast", K.ptr(dzi), 1, 1, N * L, 1.0, K.ptr(dz), N * L, 1, F32,
                    K.stream())
@@ -391,5 +418,5 @@ def vae_bwd(M, model, state, dout, dmu, dlogvar):
     else:
         K.call("vu_sample_broadcast", K.ptr(dpooled), N, HW4, C4, 1.0 / HW4, K.ptr(df4),
                K.pstride(df4), 1, M.d, K.stream())
-    dfeats[4] = df4
-    encoder_bwd(M, model.encoder, senc, dfeats, cin)
+    dfeats[-1] = df4
+    return dfeats
