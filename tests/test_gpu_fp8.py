@@ -94,7 +94,9 @@ def test_conv3x3_fp8(case):
         ref = F.conv2d(xd, wd, b, padding=1)
         got = out.float().cpu()
         err = (got - ref).abs()
-        bound = 2.0 ** -8 * ref.abs() + 1e-5 * ref.abs().max()
+        # bf16 output rounding (half an ulp of the stored value's binade) plus
+        # fp32 summation-order noise of the K-term dot products
+        bound = 2.0 ** -8 * torch.maximum(ref.abs(), got.abs()) + 1e-5 * ref.abs().max()
         assert (err <= bound).all(), (f"max err {err.max().item():.3e}, "
                                       f"{int((err > bound).sum())} elements off")
         # BN partials of the stored bf16 values

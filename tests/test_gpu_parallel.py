@@ -56,7 +56,7 @@ def _worker(rank, world, port, backend, out_q):
         model = seeded_init_(UNet(3, 1), 0).cuda().to(memory_format=torch.channels_last).train()
         # single-rank gradients of every shard (deterministic kernels: the
         # same on every rank), before the reducer is attached
-        single = [_grads(model, *_shard(i)) for i in range(2 * world)]
+        single = [_grads(model, *_shard(i)) for i in range(3 * world)]
         red = parallel.attach(model, bucket_bytes=2 * 1024 * 1024)
         launched = []
         orig = red._launch
@@ -74,7 +74,7 @@ def _worker(rank, world, port, backend, out_q):
         CombinedLoss()(model(x.cuda().contiguous(memory_format=torch.channels_last)), t.cuda()).backward()
         n_during = len(launched)
         red.finish()
-        res["dp"] = [p.grad.detach().cpu() for p in model.parameters()]
+        res["dp"] = [p.grad.detach().cpu().numpy() for p in model.parameters()]
         res["early"] = n_during
         res["nbuckets"] = len(red.buckets)
         # (b) accumulation x2: shards world + 2*rank + {0, 1}; micro-batch 0 under no_sync
@@ -94,8 +94,10 @@ def _worker(rank, world, port, backend, out_q):
                 red.prepare()
                 CombinedLoss()(model(x.cuda().contiguous(memory_format=torch.channels_last)), t.cuda()).backward()
                 red.finish()
-        res["acc"] = [p.grad.detach().cpu() for p in model.parameters()]
-        res["single"] = [[g.cpu() for g in s] for s in single]
+        res["acc"] = [p.grad.detach().cpu().numpy() for p in model.parameters()]
+        # numpy (pickled by value): torch tensors would be shared through file
+        # descriptors that die with this process
+        res["single"] = [[g.cpu().numpy() for g in s] for s in single]
         torch.cuda.synchronize()
         out_q.put((rank, res))
     finally:
@@ -120,6 +122,7 @@ def _run(world, backend):
 
 
 def _close(a, b):
+    a, b = torch.as_tensor(a), torch.as_tensor(b)
     return (a - b).abs().max().item() <= 1e-6 * max(b.abs().max().item(), 1e-12) + 1e-9
 
 
