@@ -71,6 +71,8 @@ typedef struct VuGemmFwd {
   float* stat_sum;
   float* stat_m2;
   int32_t accumulate;  /* out += result (gradient accumulation) */
+  int32_t ksplit;      /* set by the library (split-K ways); callers pass 0 */
+  float* workspace;    /* fp32 split-K slabs, vu_gemm_fwd_workspace_bytes() */
 } VuGemmFwd;
 
 /* Weight-gradient GEMM: out[s][i][j] = sum_{m in split s} P[m][i] * Q[m][j]
@@ -87,6 +89,9 @@ typedef struct VuGemmWgrad {
 /* ---- GEMM family ------------------------------------------------------ */
 int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream);
 int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype);  /* BM used */
+/* bytes of args->workspace the dispatcher needs for this problem (0 = none):
+ * the split-K slabs of the 3x3 kernel when its grid is under one block per CU */
+int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype);
 int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream);
 /* output tile (BI x BJ) the dispatcher picks for this problem (split-K sizing) */
 int vu_gemm_wgrad_tile(const VuGemmWgrad* args, int dtype, int* bi, int* bj);
@@ -98,22 +103,20 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 
 /* Dispatcher tuning (tests / experiments):
  *   VU_TUNE_V4_MIN_BLOCKS: smallest grid for which the ping-pong 3x3 kernel
- *     (gemm_fwd4.hip) is used (default 256 = one block per CU; 0 forces it);
- *   VU_TUNE_V5_MAX_C: widest input (channels) the persistent 3x3 kernel
- *     (gemm_fwd5.hip) serves (default 0 = disabled: no net gain measured);
- *   VU_TUNE_V5_MIN_TILES: fewest tiles for which it is used (default -1 =
- *     2 x CU count; 0 forces it);
- *   VU_TUNE_V5_GRID / VU_TUNE_FP8_GRID: cap on the grid of the persistent
- *     bf16 / fp8 kernels (default 0 = CU count; tests use small caps so that
- *     every block walks several tiles);
+ *     (gemm_fwd4.hip) is used without split-K (default 256 = one block per
+ *     CU; 0 forces it);
+ *   VU_TUNE_V4_SPLITK: 0 = no split-K, 1 = automatic (default: grids of
+ *     16..255 256x256 tiles are split to reach one block per CU), k >= 2 =
+ *     k-way split wherever the ping-pong kernel serves (tests);
+ *   VU_TUNE_FP8_GRID: cap on the grid of the persistent fp8 kernel (default
+ *     0 = CU count; tests use small caps so that every block walks several
+ *     tiles);
  *   VU_TUNE_STREAM: 1 (default) lets the short-K 1x1 stream kernel
  *     (gemm_stream.hip) serve the problems it takes, 0 routes them to v2. */
 #define VU_TUNE_V4_MIN_BLOCKS 0
-#define VU_TUNE_V5_MAX_C 1
-#define VU_TUNE_V5_MIN_TILES 2
-#define VU_TUNE_V5_GRID 3
 #define VU_TUNE_FP8_GRID 4
 #define VU_TUNE_STREAM 5
+#define VU_TUNE_V4_SPLITK 6
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */

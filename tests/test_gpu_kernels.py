@@ -118,18 +118,17 @@ V4_CASES = [
 ]
 
 
-V5_CASES = [
-    # (N, [cin per source], H, W, cout, grid cap): persistent kernel (gemm_fwd5.hip)
-    # with the grid capped so that blocks walk several tiles
-    (2, [64], 32, 64, 64, 3),           # 1024x64 tiles: 4 tiles over 3 blocks
-    (1, [64], 16, 64, 256, 3),          # 256x256 tiles: 4 tiles
-    (1, [64], 16, 32, 384, 2),          # 512x128 tiles, 3 column tiles: n0 changes along a walk
-    (2, [32, 32, 64], 16, 32, 128, 1),  # three sources, one block walks both tiles
-    (3, [96], 32, 32, 64, 2),           # odd chunk count: the halo buffer parity flips per tile
+SPLITK_CASES = [
+    # (N, [cin per source], H, W, cout, forced split): split-K ping-pong kernel +
+    # splitk_finish_kernel (bias, accumulate, BN partials from the fp32 slabs)
+    (1, [64], 8, 32, 256, 2),
+    (2, [96, 64], 16, 64, 256, 5),      # two sources, one chunk per split
+    (1, [32, 32, 64], 16, 32, 128, 3),  # three sources, uneven chunk ranges
+    (1, [128], 32, 64, 64, 2),          # 1024x64 tiles
 ]
 
-TUNE_V4_MIN_BLOCKS, TUNE_V5_MAX_C, TUNE_V5_MIN_TILES, TUNE_V5_GRID = 0, 1, 2, 3
-TUNE_DEFAULTS = ((TUNE_V4_MIN_BLOCKS, 256), (TUNE_V5_MAX_C, 0), (TUNE_V5_MIN_TILES, -1), (TUNE_V5_GRID, 0))
+TUNE_V4_MIN_BLOCKS, TUNE_V4_SPLITK = 0, 6
+TUNE_DEFAULTS = ((TUNE_V4_MIN_BLOCKS, 256), (TUNE_V4_SPLITK, 1))
 
 
 def _tune(*kv):
@@ -174,7 +173,7 @@ def _check_halo_conv(case, row_tiles):
     exp[:, 64:] += ref + b[None, :, None, None]
     _close(wide, exp, "bf16", what="bias+accumulate")
     # input gradient (flipped weights) when cin is a tile width
-    if cin in (64, 128, 256) and co % 32 == 0:
+    if cin in (64, 128, 256, 512) and co % 32 == 0:
         dy = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
         dx = K.empty_act(N, cin, H, W, torch.bfloat16, DEV)
         K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), cin, dx, d)
@@ -185,23 +184,27 @@ def _check_halo_conv(case, row_tiles):
 def test_conv3x3_pingpong_kernel(case):
     """bf16 ping-pong halo kernel (gemm_fwd4.hip) forced onto small problems
     (the production dispatcher only picks it for >= 256 blocks)."""
-    _tune((TUNE_V5_MAX_C, 0), (TUNE_V4_MIN_BLOCKS, 0))
+    _tune((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 0))
     try:
         _check_halo_conv(case, (128,))
     finally:
         _tune(*TUNE_DEFAULTS)
 
 
-@pytest.mark.parametrize("case", V5_CASES)
-def test_conv3x3_persistent_kernel(case):
-    """persistent ping-pong kernel (gemm_fwd5.hip): blocks walk several tiles,
-    halos and weights prefetched across tile boundaries, register epilogue
-    (bias, accumulate, BN partials per 128-pixel wave tile)."""
-    _tune((TUNE_V5_MAX_C, 1 << 20), (TUNE_V5_MIN_TILES, 0), (TUNE_V5_GRID, case[5]))
+@pytest.mark.parametrize("case", SPLITK_CASES)
+def test_conv3x3_pingpong_splitk(case):
+    """split-K: blocks walk chunk ranges, fp32 slabs, deterministic finish."""
+    _tune((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, case[5]))
     try:
         _check_halo_conv(case, (128,))
     finally:
         _tune(*TUNE_DEFAULTS)
+
+
+def test_conv3x3_splitk_auto_32x32_level():
+    """the production dispatch of a down4-like layer (512 -> 1024 at 32x32):
+    16..255 256x256 tiles -> automatic split-K (default tuning)."""
+    _check_halo_conv((2, [512], 32, 32, 1024), (128,))
 
 
 IMAGE_CASES = [

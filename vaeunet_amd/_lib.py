@@ -34,7 +34,8 @@ class VuGemmFwd(C.Structure):
                 ("out_mode", C.c_int32), ("out", _p), ("out_stride", _l),
                 ("out_coff", C.c_int32), ("oH", C.c_int32), ("oW", C.c_int32),
                 ("opy", C.c_int32), ("opx", C.c_int32), ("cout", C.c_int32),
-                ("bias", _p), ("stat_sum", _p), ("stat_m2", _p), ("accumulate", C.c_int32)]
+                ("bias", _p), ("stat_sum", _p), ("stat_m2", _p), ("accumulate", C.c_int32),
+                ("ksplit", C.c_int32), ("workspace", _p)]
 
 
 class VuGemmWgrad(C.Structure):
@@ -64,6 +65,7 @@ class VuMtEntry(C.Structure):
 _SIGS = {
     "vu_gemm_fwd": (_i, [C.POINTER(VuGemmFwd), _i, _p]),
     "vu_gemm_fwd_row_tile": (_l, [C.POINTER(VuGemmFwd), _i]),
+    "vu_gemm_fwd_workspace_bytes": (_l, [C.POINTER(VuGemmFwd), _i]),
     "vu_gemm_wgrad": (_i, [C.POINTER(VuGemmWgrad), _i, _p]),
     "vu_gemm_wgrad_tile": (_i, [C.POINTER(VuGemmWgrad), _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vu_gemm_set_tuning": (_i, [_i, _i]),

@@ -327,8 +327,7 @@ int gemm_fwd_v3_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st);
-int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype);
-int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st);
+int64_t gemm_fwd_v4_workspace(const VuGemmFwd& p, int dtype);
 int conv_image_bm(const VuGemmFwd& p, int dtype);      // conv_image.hip (3-channel image conv)
 int conv_image_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_stream_bm(const VuGemmFwd& p, int dtype);     // gemm_stream.hip (short-K 1x1 streams)
@@ -369,9 +368,7 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
     if (bm) return bm;
   }
   if (use_v4(dtype)) {
-    int bm = gemm_fwd_v5_bm(*args, dtype);
-    if (bm) return bm;
-    bm = gemm_fwd_v4_bm(*args, dtype);
+    int bm = gemm_fwd_v4_bm(*args, dtype);
     if (bm) return bm;
   }
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 256;
@@ -380,6 +377,11 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
     if (bm) return bm;
   }
   return pick_bm(*args);
+}
+
+extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype) {
+  if (use_v2(dtype) && (conv_image_bm(*args, dtype) || gemm_stream_bm(*args, dtype))) return 0;
+  return use_v4(dtype) ? gemm_fwd_v4_workspace(*args, dtype) : 0;
 }
 
 extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
@@ -392,7 +394,6 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return conv_image_launch(*args, st);
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
-  if (use_v4(dtype) && gemm_fwd_v5_bm(*args, dtype)) return gemm_fwd_v5_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);

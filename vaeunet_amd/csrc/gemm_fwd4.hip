@@ -29,7 +29,12 @@
 //     partial statistics a register + 16-lane reduction and the bf16 output
 //     staging 8-byte LDS writes;
 //   * epilogue: bias, storage rounding, per-wave (sum, centered M2) of the
-//     rounded values (same contract as v1-v3), 16-byte NHWC stores.
+//     rounded values (same contract as v1-v3), 16-byte NHWC stores;
+//   * split-K for grids under one block per CU (the 32x32 and 64x64 levels:
+//     down4 convs and their input gradients have 64-128 256x256 tiles for
+//     256 CUs): each block walks a contiguous range of 32-channel chunks and
+//     writes its fp32 tile to a slab; splitk_finish_kernel sums the slabs in
+//     a fixed order and applies the epilogue above (deterministic).
 #include "common.h"
 #include "../../include/vaeunet.h"
 #include <stdlib.h>
@@ -89,13 +94,9 @@ VU_DEV float ror_add(float v) {
 }
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
-// XM (experiment mode, timing studies only; 0 in production): 1 = no DMA in
-// the main loop, 2 = no DMA and no barriers in the main loop, 3 = no MFMA,
-// 6/9 = next-chunk halo issued over steps 0-2 / 0-7 (production: step 0),
-// 7 = no weight DMA in the main loop, 8 = no halo DMA in the main loop.
-// NBW: weight ring slots (prefetch distance NBW-1 steps).
-template <int BN, int XM, int NBW>
+template <int BN>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
+  constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
   constexpr int NT = 512;
   constexpr int BM = TH * TW;
@@ -109,11 +110,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int LB0A = (LB0 + 1) / 2;             // ... issued in phase 1 (rest in phase 2)
   constexpr int WSLOT = BN * 64;
   constexpr int PD = NBW - 1;                     // weight prefetch distance (steps)
-  // halo slots issued per step: the whole next-chunk halo goes out at step 0
-  // of the current chunk (measured 5 % faster than spreading it over steps
-  // 0..7: the HBM/MALL latency gets 8 steps of cover); XM 6 = steps 0-2,
-  // XM 9 = steps 0-7
-  constexpr int PPS1 = XM == 6 ? (NHP1 + 2) / 3 : XM == 9 ? (NHP1 + 7) / 8 : NHP1;
+  // the whole next-chunk halo goes out at step 0 of the current chunk
+  // (measured 5 % faster than spreading it over steps 0..7: the HBM/MALL
+  // latency gets 8 steps of cover)
+  constexpr int PPS1 = NHP1;
   constexpr int MAIN = 2 * HALO + NBW * WSLOT;
   constexpr int ROWB = BN * 2 + 16;               // bf16 staging row (padded)
   constexpr int EPI = BM * ROWB;
@@ -127,7 +127,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int tx_n = W / TW, ty_n = H / TH;
   const int mtiles = g.N * ty_n * tx_n;
   const int ntiles = p.ncol / BN;
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
+  const int btiles = mtiles * ntiles;
+  const int bid0 = xcd_remap(blockIdx.x, btiles * ksplit);
+  const int kidx = bid0 / btiles;  // K-split index (0 without split-K)
+  const int bid = bid0 - kidx * btiles;
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int img = mt / (ty_n * tx_n);
   const int trem = mt - img * (ty_n * tx_n);
@@ -138,8 +142,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int grp = wid >> 2;  // ping-pong half (one wave of each half per SIMD)
-  const int nchunk = g.C / 32;
-  const int nk = nchunk * 9;
+  // this block's contiguous range of 32-channel chunks
+  const int call = g.C / 32;
+  const int cbeg = kidx * call / ksplit, cend = (kidx + 1) * call / ksplit;
+  const int nk = (cend - cbeg) * 9;
 
   // ---- DMA roles ------------------------------------------------------------
   // vmcnt counts a wave's loads in issue order, so a wave that mixes slow
@@ -196,7 +202,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   };
   // (half 0) weight slots [i0, i1) of step s
   auto wstage = [&](int s, int i0, int i1) {
-    const int c = s / 9, t = s - (s / 9) * 9;
+    const int c = cbeg + s / 9, t = s - (s / 9) * 9;
     const int k0 = t * g.C + c * 32;
     char* B = wbuf + (s % NBW) * WSLOT;
 #pragma unroll
@@ -204,8 +210,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       if (i < i0 || i >= i1) continue;
       const int P = i * 256 + gt;
       const int row = P >> 2;
-      const void* gp = XM == 4 ? (const void*)(bmat + ((int64_t)s * p.ncol + n0) * 32 + P * 8)
-                               : (const void*)(bmat + (int64_t)(n0 + row) * p.ldb + k0 + (P & 3) * 8);
+      const void* gp = (const void*)(bmat + (int64_t)(n0 + row) * p.ldb + k0 + (P & 3) * 8);
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * 256 + gw * 64) * 16), 16, 0, 0);
     }
   };
@@ -236,7 +241,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
 
   // ---- prologue: halo of chunk 0, weights of steps 0 and 1 -----------------
   if (grp) {
-    halo_chunk(0, -1);
+    halo_chunk(cbeg, -1);
   } else {
 #pragma unroll
     for (int q = 0; q < PD; ++q)
@@ -247,7 +252,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   if (grp) pp_barrier();  // the stagger: half 1 runs one barrier behind
 
   for (int s = 0; s < nk; ++s) {
-    const int c = s / 9, t = s - (s / 9) * 9;
+    const int c = cbeg + s / 9, t = s - (s / 9) * 9;
     const char* A = hbuf + (c & 1) * HALO + ((t / 3) * HW + (t - (t / 3) * 3)) * 64;
     const char* Bw = wbuf + (s % NBW) * WSLOT;
     u32x4 bf[4], af[4];
@@ -256,25 +261,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(Bw + brow + j * 16 * 64);
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[i]);
-    if (XM != 1 && XM != 2 && XM != 7 && !grp && s + PD < nk) wstage(s + PD, 0, LB0A);
-    if (XM != 2) pp_barrier();
+    if (!grp && s + PD < nk) wstage(s + PD, 0, LB0A);
+    pp_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (XM != 3) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
                                                             __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    if (XM != 2) pp_barrier();
+    pp_barrier();
     // -- phase 2: pixel fragments 4..7; half 0 finishes weights(s+2) and waits
     //    for weights(s+1); half 1 streams the next chunk's halo and waits for
     //    it at the chunk's last step
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[4 + i]);
-    if (XM == 1 || XM == 2 || (XM == 7 && !grp)) {
-    } else if (XM == 8 && grp) {
-    } else if (!grp) {
+    if (!grp) {
       // outstanding weight steps after this issue: s+1 .. min(nk-1, s+PD);
       // step s+1 must have landed
       if (s + PD < nk) {
@@ -284,21 +287,21 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
         const int out = nk - 2 - s;
         wait_vm(out > 0 ? out * LB0 : 0);
       }
-    } else if (c + 1 < nchunk) {
+    } else if (c + 1 < cend) {
       if (t * PPS1 < NHP1) halo_chunk(c + 1, t);
       if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (XM != 2) pp_barrier();
+    pp_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (XM != 3) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
                                                                 __builtin_bit_cast(bf16x8, af[i]), acc[4 + i][j], 0, 0,
                                                                 0);
     __builtin_amdgcn_s_setprio(0);
-    if (XM != 2) pp_barrier();
+    pp_barrier();
   }
   if (!grp) pp_barrier();  // re-align the halves
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -307,6 +310,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   // ---- epilogue ---------------------------------------------------------------
   // acc[i][j][r]: pixel wm*128 + i*16 + (lane&15), channel wn*64 + j*16 + 4*(lane>>4) + r
   const int cbase = wn * 64 + 4 * (lane >> 4);
+  if (ksplit > 1) {
+    // split-K: raw fp32 partial tile -> slab kidx (16-byte stores of 4 channels)
+    float* slab = p.workspace + (int64_t)kidx * ((int64_t)g.N * H * W) * p.ncol;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = wm * 128 + i * 16 + (lane & 15);
+      const int ty = m / TW, tx = m - (m / TW) * TW;
+      const int64_t gm = ((int64_t)img * H + y0 + ty) * W + x0 + tx;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4*>(slab + gm * p.ncol + n0 + cbase + j * 16) = acc[i][j];
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -375,57 +392,85 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   }
 }
 
-int xmode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("VU_V4_XM");
-    m = e ? atoi(e) : 0;
+// split-K epilogue: out = round(sum_k slab[k] + bias) (+ out if accumulate),
+// BatchNorm (sum, centered M2) per 128-row tile of the rounded values.  Block:
+// 128 rows x 64 columns, 256 threads (8 column groups of 8 x 32 row lanes).
+__global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
+  __shared__ float red[32][65];
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  const int ctiles = p.ncol / 64;
+  const int rb = blockIdx.x / ctiles, cb = blockIdx.x - (blockIdx.x / ctiles) * ctiles;
+  const int t = threadIdx.x, cg = t & 7, rs = t >> 3;
+  const int c0 = cb * 64 + cg * 8;
+  const int64_t slab = M * p.ncol;
+  float v[4][8];
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = p.bias ? p.bias[c0 + e] : 0.f;
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t m = (int64_t)rb * 128 + rs + 32 * q;
+    f32x4 a = f32x4{0, 0, 0, 0}, b = f32x4{0, 0, 0, 0};
+    for (int k = 0; k < p.ksplit; ++k) {
+      const float* src = p.workspace + k * slab + m * p.ncol + c0;
+      a += *reinterpret_cast<const f32x4*>(src);
+      b += *reinterpret_cast<const f32x4*>(src + 4);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[q][e] = rnd<bf16_t>(a[e] + bv[e]);
+      v[q][4 + e] = rnd<bf16_t>(b[e] + bv[4 + e]);
+    }
+    bf16_t* dst = out + m * p.out_stride + p.out_coff + c0;
+    Vec8<bf16_t> o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.set(e, v[q][e]);
+    if (p.accumulate) {
+      Vec8<bf16_t> old;
+      old.load(dst);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.set(e, old.get(e) + v[q][e]);
+    }
+    o.store(dst);
   }
-  return m;
-}
-
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// weight-ring depth: 3 slots (prefetch distance 2).  Deeper rings (up to the
-// LDS budget, max(2 halo + ring, bf16 staging) <= 160 KiB) measured within
-// 1 % on the 17 layer shapes, so they stay an experiment (VU_V4_NBW).
-template <int BN> constexpr int kNbwMax = BN == 64 ? 3 : 6;
-template <int BN> int nbw_for() {
-  static int v = -1;
-  if (v < 0) {
-    v = env_int("VU_V4_NBW", 3);
-    if (v < 3) v = 3;
-    if (v > kNbwMax<BN>) v = kNbwMax<BN>;
+  if (!p.stat_sum) return;
+  // two-pass (sum, centered M2) of the 128 rows of each column
+  float mean[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rs][cg * 8 + e] = (v[0][e] + v[1][e]) + (v[2][e] + v[3][e]);
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float sm = 0.f;
+    for (int r = 0; r < 32; ++r) sm += red[r][cg * 8 + e];
+    mean[e] = sm;
   }
-  return v;
-}
-
-template <int BN>
-int launch(const VuGemmFwd& p, hipStream_t st) {
-  const VuGather& g = p.a;
-  const int64_t mt = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW);
-  const dim3 grid((unsigned)(mt * (p.ncol / BN)));
-  constexpr int NM = kNbwMax<BN>;
-  switch (xmode()) {
-    case 1: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 1, 3>), grid, dim3(512), 0, st, p); break;
-    case 2: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 2, 3>), grid, dim3(512), 0, st, p); break;
-    case 3: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 3, 3>), grid, dim3(512), 0, st, p); break;
-    case 9: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 9, 3>), grid, dim3(512), 0, st, p); break;
-    case 6: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 6, 3>), grid, dim3(512), 0, st, p); break;
-    case 7: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 7, 3>), grid, dim3(512), 0, st, p); break;
-    case 8: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 8, 3>), grid, dim3(512), 0, st, p); break;
-    default:
-      switch (nbw_for<BN>()) {
-        case 3: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, 3>), grid, dim3(512), 0, st, p); break;
-        case 4: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, (NM < 4 ? NM : 4)>), grid, dim3(512), 0, st, p); break;
-        case 5: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, (NM < 5 ? NM : 5)>), grid, dim3(512), 0, st, p); break;
-        default: hipLaunchKernelGGL((conv3x3_pp_kernel<BN, 0, NM>), grid, dim3(512), 0, st, p);
-      }
+  __syncthreads();
+  if (rs == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) p.stat_sum[(int64_t)rb * p.ncol + c0 + e] = mean[e];
   }
-  return (int)hipGetLastError();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mean[e] *= 1.f / 128;
+    float q2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float d = v[q][e] - mean[e];
+      q2 += d * d;
+    }
+    red[rs][cg * 8 + e] = q2;
+  }
+  __syncthreads();
+  if (rs == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float sm = 0.f;
+      for (int r = 0; r < 32; ++r) sm += red[r][cg * 8 + e];
+      p.stat_m2[(int64_t)rb * p.ncol + c0 + e] = sm;
+    }
+  }
 }
 
 template <int BN>
@@ -435,6 +480,7 @@ bool tiles_ok(const VuGemmFwd& p) {
 }
 
 int g_min_blocks = 256;  // vu_gemm_set_tuning(VU_TUNE_V4_MIN_BLOCKS, ...)
+int g_splitk = 1;        // vu_gemm_set_tuning(VU_TUNE_V4_SPLITK, ...): 0 off, 1 auto, k >= 2 forced
 
 // Output-column tile the ping-pong kernel uses for this problem (0 = not served).
 int pick_bn(const VuGemmFwd& p) {
@@ -442,44 +488,100 @@ int pick_bn(const VuGemmFwd& p) {
   const int64_t pix = (int64_t)g.N * g.H * g.W;
   const int mb = g_min_blocks;
   // at least ~one block per CU, else the v3 tiles (more, smaller blocks) win
-  static const int pref = env_int("VU_V4_PREF_BN", 256);
-  if (pref == 256 && tiles_ok<256>(p) && (pix / 256) * (p.ncol / 256) >= mb) return 256;
-  if ((pref != 256 || p.ncol % 256 != 0) && tiles_ok<128>(p) && (pix / 512) * (p.ncol / 128) >= mb) return 128;
+  if (tiles_ok<256>(p) && (pix / 256) * (p.ncol / 256) >= mb) return 256;
+  if (p.ncol % 256 != 0 && tiles_ok<128>(p) && (pix / 512) * (p.ncol / 128) >= mb) return 128;
   // 64 x 64 problems (18 K steps) are prologue/epilogue bound at 1 block/CU: v3 wins
   if (p.ncol == 64 && (g.C > 64 || mb < 256) && tiles_ok<64>(p) && pix / 1024 >= mb) return 64;
   return 0;
+}
+
+struct Plan {
+  int bn, ks;
+};
+
+// Tile and K-split.  A grid of 16..255 256x256 tiles gets the smallest split
+// that reaches one block per CU (down4: 128 tiles -> 2, its input gradient:
+// 64 tiles -> 4); at least 2 chunks per split.
+Plan plan(const VuGemmFwd& p) {
+  const VuGather& g = p.a;
+  const int chunks = g.C / 32;
+  Plan r{pick_bn(p), 1};
+  if (r.bn) {
+    if (g_splitk >= 2) r.ks = g_splitk < chunks ? g_splitk : chunks;
+    return r;
+  }
+  if (g_splitk == 0 || !tiles_ok<256>(p) || chunks < 4) return r;
+  const int64_t blocks = ((int64_t)g.N * g.H * g.W / 256) * (p.ncol / 256);
+  if (blocks < 16) return r;
+  int ks = (int)((g_min_blocks + blocks - 1) / blocks);
+  if (g_splitk >= 2) ks = g_splitk;
+  if (ks > chunks / 2) ks = chunks / 2;
+  if (ks < 2) return r;
+  return Plan{256, ks};
+}
+
+template <int BN>
+int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
+  const VuGather& g = p.a;
+  const int64_t mt = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW);
+  const dim3 grid((unsigned)(mt * (p.ncol / BN) * ks));
+  if (ks <= 1) {
+    VuGemmFwd q = p;
+    q.ksplit = 1;
+    hipLaunchKernelGGL((conv3x3_pp_kernel<BN>), grid, dim3(512), 0, st, q);
+    return (int)hipGetLastError();
+  }
+  if (!p.workspace) return (int)hipErrorInvalidValue;
+  VuGemmFwd q = p;
+  q.ksplit = ks;
+  hipLaunchKernelGGL((conv3x3_pp_kernel<BN>), grid, dim3(512), 0, st, q);
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  hipLaunchKernelGGL(splitk_finish_kernel, dim3((unsigned)((M / 128) * (p.ncol / 64))), dim3(256), 0, st, q);
+  return (int)hipGetLastError();
+}
+
+bool operands_ok(const VuGemmFwd& p, int dtype) {
+  const VuGather& g = p.a;
+  if (dtype != VU_BF16 || p.out_mode != 0) return false;
+  if (g.R != 3 || g.S != 3 || g.sy != 1 || g.sx != 1 || g.dy != 1 || g.dx != 1 || g.oy != -1 ||
+      g.ox != -1 || g.Hs != g.H || g.Ws != g.W)
+    return false;
+  if (g.C % 32 != 0) return false;
+  for (int t = 0; t < g.nsrc; ++t)
+    if (g.cend[t] % 32 != 0 || g.stride[t] % 8 != 0) return false;
+  if (p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0) return false;
+  if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return false;
+  return true;
 }
 
 }  // namespace
 
 // Row tile (BM) when the ping-pong kernel serves this problem, else 0: bf16,
 // 3x3 stride-1 pad-1 gather over same-size sources, 32-channel aligned source
-// groups, plain NHWC output with 8-element aligned strides.
+// groups, plain NHWC output with 8-element aligned strides.  BatchNorm
+// statistics come per 128 pixels (one wave tile, or one finish-kernel tile).
 int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype) {
-  const VuGather& g = p.a;
-  if (dtype != VU_BF16 || p.out_mode != 0) return 0;
-  if (g.R != 3 || g.S != 3 || g.sy != 1 || g.sx != 1 || g.dy != 1 || g.dx != 1 || g.oy != -1 ||
-      g.ox != -1 || g.Hs != g.H || g.Ws != g.W)
-    return 0;
-  if (g.C % 32 != 0) return 0;
-  for (int t = 0; t < g.nsrc; ++t)
-    if (g.cend[t] % 32 != 0 || g.stride[t] % 8 != 0) return 0;
-  if (p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0) return 0;
-  if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
-  // BatchNorm statistics come per wave: 128-pixel tiles
-  return pick_bn(p) ? 128 : 0;
+  return operands_ok(p, dtype) && plan(p).bn ? 128 : 0;
+}
+
+// fp32 split-K slab bytes the ping-pong kernel needs for this problem (0 = none)
+int64_t gemm_fwd_v4_workspace(const VuGemmFwd& p, int dtype) {
+  if (!operands_ok(p, dtype)) return 0;
+  const Plan r = plan(p);
+  if (!r.bn || r.ks <= 1) return 0;
+  return (int64_t)r.ks * p.a.N * p.a.H * p.a.W * p.ncol * (int64_t)sizeof(float);
 }
 
 int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st) {
-  switch (pick_bn(p)) {
-    case 256: return launch<256>(p, st);
-    case 128: return launch<128>(p, st);
-    case 64: return launch<64>(p, st);
+  const Plan r = plan(p);
+  switch (r.bn) {
+    case 256: return launch<256>(p, r.ks, st);
+    case 128: return launch<128>(p, r.ks, st);
+    case 64: return launch<64>(p, r.ks, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
 
-int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
 int conv_fp8_tune(int key, int value);     // conv_fp8.hip
 int gemm_stream_tune(int key, int value);  // gemm_stream.hip
 
@@ -488,7 +590,10 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
     g_min_blocks = value;
     return 0;
   }
-  if (gemm_fwd_v5_tune(key, value) == 0 || conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0)
+  if (key == VU_TUNE_V4_SPLITK) {
+    g_splitk = value;
     return 0;
+  }
+  if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0) return 0;
   return (int)hipErrorInvalidValue;
 }

@@ -173,6 +173,14 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
         st = Stats(psum, pm2, tiles, bm, rows)
     else:
         a.stat_sum = a.stat_m2 = None
+    a.ksplit = 0
+    a.workspace = None
+    ws = None
+    if g.R == 3 and dtype == _lib.BF16:
+        nb = query("vu_gemm_fwd_workspace_bytes", C.byref(a), dtype)
+        if nb > 0:
+            ws = torch.empty(nb // 4, dtype=torch.float32, device=out.device)
+            a.workspace = ws.data_ptr()
     M = g.N * g.H * g.W
     _timed(_gemm_tag(g, kind),
            2 * M * ncol * g.R * g.S * g.C,
