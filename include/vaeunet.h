@@ -413,6 +413,31 @@ int vu_reparam_fwd(const float* mu, const float* lv, const float* eps, int n,
 int vu_reparam_bwd(const float* lv, const float* eps, const float* dz, int n,
                    float* dmu, float* dlv, int accumulate, void* stream);
 
+/* ---- inference sampling path (utils/vae_utils.py, visualize_vae.py) --- */
+/* out[e] = (sum_{k < groups} x[k*n + e]) / groups  (stack(preds).mean(0)) */
+int vu_mean_groups(const float* x, int groups, int64_t n, float* out,
+                   void* stream);
+/* y = 1 / (1 + exp(-x)) */
+int vu_sigmoid(const float* x, int64_t n, float* y, void* stream);
+/* Feathered sliding-window accumulation of one patch prediction
+ * (visualize_vae.py:360-384): pred [B][ph][pw] (image stride pred_img_stride)
+ * -> out/wsum [B][H][W] at (sh, sw), weight = ramp-tapered ones (ramp[ov] =
+ * linspace(0, 1, ov); leading taper if top/left, trailing (1 - ramp) if
+ * bottom/right, each only when the patch extent > 2*ov).  Launches of
+ * overlapping patches accumulate in launch order (no atomics). */
+int vu_patch_blend(const float* pred, int64_t pred_img_stride, int B, int ph,
+                   int pw, float* out, float* wsum, int H, int W, int sh,
+                   int sw, const float* ramp, int overlap, int top,
+                   int bottom, int left, int right, void* stream);
+/* out = out / (wsum + 1e-8) */
+int vu_blend_finish(float* out, const float* wsum, int64_t n, void* stream);
+/* calculate_uncertainty_metrics (visualize_vae.py:90-117) over the sample
+ * axis of seg [samples][n]: mean, unbiased std, entropy of the mean,
+ * mutual information, coefficient of variation (eps 1e-7) */
+int vu_uncertainty(const float* seg, int samples, int64_t n, float* mean,
+                   float* std, float* entropy, float* mutual_info,
+                   float* coeff_var, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

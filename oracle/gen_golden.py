@@ -51,7 +51,8 @@ sys.path.insert(0, REF)
 from vaeunet_amd.init import seeded_init_  # noqa: E402
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from golden_util import (_rand, seed_vae_tail, vae_feature, vae_feature_shapes,  # noqa: E402
-                         vae_eps, vae_target)
+                         vae_eps, vae_target, pyramid_encoder, seed_bn_stats, infer_inputs,
+                         INFER_SEED, INFER_GEN, INFER_PATCH)
 from unet.unet_parts import AttentionGate, DoubleConv, Down, Up, OutConv  # noqa: E402
 from unet.unet_model import UNet  # noqa: E402
 from utils.loss import dice_loss, CombinedLoss, KLAnnealer, kl_with_free_bits  # noqa: E402
@@ -311,6 +312,61 @@ def gen_unet(n_classes, bilinear, tag, batch=2, size=64, steps=1):
     print(f"{tag}: loss {rec['loss']:.6f} total_norm {rec['total_norm']:.6f}")
 
 
+def _load_visualize_fns():
+    """predict_full_image (61-87), calculate_uncertainty_metrics (90-117),
+    predict_with_patches (243-415) compiled from visualize_vae.py's AST (the
+    module itself imports matplotlib/psutil/timm-dependent code)."""
+    import logging
+    import math
+    path = os.path.join(REF, "visualize_vae.py")
+    tree = ast.parse(open(path).read())
+    want = ("predict_full_image", "calculate_uncertainty_metrics", "predict_with_patches")
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name in want]
+    ns = {"torch": torch, "F": F, "math": math, "logging": logging, "np": np}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), path, "exec"), ns)
+    return [ns[k] for k in want]
+
+
+def gen_inference():
+    """Inference sampling path fixtures from the reference's
+    own functions: utils/vae_utils.generate_predictions / encode_images and
+    visualize_vae.predict_full_image / predict_with_patches /
+    calculate_uncertainty_metrics, on the reference UNetResNet with an
+    input-dependent encoder TEST DOUBLE (golden_util.pyramid_encoder) and
+    seeded eval-mode BatchNorm statistics; randn_like patched to fixture eps."""
+    from utils.vae_utils import generate_predictions, encode_images
+    predict_full_image, calculate_uncertainty_metrics, predict_with_patches = _load_visualize_fns()
+    UNetResNet = _load_unet_resnet(lambda: pyramid_encoder(INFER_SEED))
+    torch.manual_seed(0)
+    model = UNetResNet(3, 1, pretrained=False, latent_injection="all")
+    seed_vae_tail(model, INFER_SEED)
+    seed_bn_stats(model, INFER_SEED + 50)
+    model.eval()
+    inp = infer_inputs()
+    rec = {}
+    imgs = torch.from_numpy(inp["gen_images"])
+    mu, lv = encode_images(model, imgs)
+    rec["enc_mu"], rec["enc_logvar"] = _np(mu), _np(lv)
+    draws = iter([torch.from_numpy(e) for e in inp["gen_eps"]])
+    real = torch.randn_like
+    torch.randn_like = lambda t, **kw: next(draws).to(t.dtype)
+    try:
+        rec["gen_out"] = _np(generate_predictions(model, imgs, temperature=INFER_GEN["temperature"],
+                                                  num_samples=INFER_GEN["samples"]))
+    finally:
+        torch.randn_like = real
+    rec["full_out"] = _np(predict_full_image(model, torch.from_numpy(inp["full_img"]),
+                                             torch.from_numpy(inp["full_z"])))
+    rec["patch_out"] = _np(predict_with_patches(model, torch.from_numpy(inp["patch_img"]),
+                                                torch.from_numpy(inp["patch_z"]), INFER_PATCH["patch"], None,
+                                                INFER_PATCH["batch"]))
+    unc = calculate_uncertainty_metrics(torch.from_numpy(inp["segs"]))
+    for k, v in unc.items():
+        rec[f"unc_{k}"] = _np(v)
+    np.savez_compressed(os.path.join(OUT, "inference.npz"), **rec)
+    print("inference:", {k: v.shape for k, v in rec.items()})
+
+
 def gen_decoder_spatial():
     """DecoderBlock with the reference's spatial z [B, L, h, w] (not constant)."""
     DecoderBlock = _load_decoder_block()
@@ -321,7 +377,7 @@ def gen_decoder_spatial():
 if __name__ == "__main__":
     # python oracle/gen_golden.py [parts losses unet vae decoder_spatial]  (default: all)
     os.makedirs(OUT, exist_ok=True)
-    what = set(sys.argv[1:]) or {"parts", "losses", "unet", "vae", "decoder_spatial"}
+    what = set(sys.argv[1:]) or {"parts", "losses", "unet", "vae", "decoder_spatial", "inference"}
     if "parts" in what:
         gen_parts()
     if "losses" in what:
@@ -335,3 +391,5 @@ if __name__ == "__main__":
     if "vae" in what:
         for mode in ("all", "none", "first", "bottleneck"):
             gen_vae(mode)
+    if "inference" in what:
+        gen_inference()

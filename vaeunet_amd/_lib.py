@@ -125,6 +125,11 @@ _SIGS = {
     "vu_linear_small_bwd": (_i, [_p, _i, _i, _p, _i, _p, _p, _i, _p, _p, _i, _p]),
     "vu_reparam_fwd": (_i, [_p, _p, _p, _i, _p, _p]),
     "vu_reparam_bwd": (_i, [_p, _p, _p, _i, _p, _p, _i, _p]),
+    "vu_mean_groups": (_i, [_p, _i, _l, _p, _p]),
+    "vu_sigmoid": (_i, [_p, _l, _p, _p]),
+    "vu_patch_blend": (_i, [_p, _l, _i, _i, _i, _p, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p]),
+    "vu_blend_finish": (_i, [_p, _p, _l, _p]),
+    "vu_uncertainty": (_i, [_p, _i, _l, _p, _p, _p, _p, _p, _p]),
 }
 
 _lib = None
