@@ -113,10 +113,13 @@ def _latents(mu, logvar, n, temperature, eps, sample):
     eps = eps.to(device=mu.device, dtype=torch.float32).reshape(n * B, L)
     if temperature != 1.0:
         eps = eps * float(temperature)
+    eps = eps.contiguous()
+    # keep every operand referenced until the launch is enqueued (a temporary
+    # freed early goes straight back to the caching allocator)
+    mu_r = mu.repeat(n, 1) if n > 1 else mu
+    lv_r = logvar.repeat(n, 1) if n > 1 else logvar
     z = torch.empty((n * B, L), dtype=torch.float32, device=mu.device)
-    K.call("vu_reparam_fwd", K.ptr(mu.repeat(n, 1) if n > 1 else mu),
-           K.ptr(logvar.repeat(n, 1) if n > 1 else logvar), K.ptr(eps.contiguous()), n * B * L, K.ptr(z),
-           K.stream())
+    K.call("vu_reparam_fwd", K.ptr(mu_r), K.ptr(lv_r), K.ptr(eps), n * B * L, K.ptr(z), K.stream())
     return z
 
 
