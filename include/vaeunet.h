@@ -437,6 +437,12 @@ int vu_blend_finish(float* out, const float* wsum, int64_t n, void* stream);
 int vu_uncertainty(const float* seg, int samples, int64_t n, float* mean,
                    float* std, float* entropy, float* mutual_info,
                    float* coeff_var, void* stream);
+/* Per-sample integer pixel map over NHWC images (flips and 90-degree
+ * rotations of patch batches, utils/data_loading.py:116-120):
+ * y[b, i, j, :] = x[b, m0*i + m1*j + m2, m3*i + m4*j + m5, :], map = int32
+ * [B][6] in device memory; x (B, H, W, C) -> y (B, Ho, Wo, C). */
+int vu_gather_affine(const void* x, int B, int H, int W, int C, const int* map,
+                     void* y, int Ho, int Wo, int dtype, void* stream);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,9 @@
 //   * vu_blend_finish  : output / (weight + 1e-8)           (visualize_vae.py:409)
 //   * vu_uncertainty   : mean / std / entropy / mutual information / coefficient
 //                        of variation over the sample axis (visualize_vae.py:90-117)
+//   * vu_gather_affine : per-sample integer pixel map (flips / 90-degree
+//                        rotations of the patch-cache batches: the geometric
+//                        part of utils/data_loading.py:116-120's augmentation)
 // All fp32, one thread per output element, fixed summation order (the
 // results do not depend on the launch geometry).
 #include "common.h"
@@ -95,6 +98,33 @@ __global__ void uncertainty_kernel(const float* seg, int S, int64_t n, float* me
   }
 }
 
+// y[b, i, j, :] = x[b, m0*i + m1*j + m2, m3*i + m4*j + m5, :] (NHWC, 16-byte
+// vectors when C*elem is a multiple of 16, else element-wise)
+template <typename T>
+__global__ void gather_affine_kernel(const T* x, int B, int H, int W, int C, const int* m, T* y, int Ho, int Wo) {
+  const int V = (C % 8 == 0) ? C / 8 : C;
+  const bool vec = C % 8 == 0;
+  const int64_t n = (int64_t)B * Ho * Wo * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int v = (int)(e % V);
+    int64_t t = e / V;
+    const int j = (int)(t % Wo);
+    t /= Wo;
+    const int i = (int)(t % Ho);
+    const int b = (int)(t / Ho);
+    const int* mb = m + 6 * b;
+    const int sy = mb[0] * i + mb[1] * j + mb[2], sx = mb[3] * i + mb[4] * j + mb[5];
+    const int64_t src = (((int64_t)b * H + sy) * W + sx) * C, dst = (((int64_t)b * Ho + i) * Wo + j) * C;
+    if (vec) {
+      Vec8<T> q;
+      q.load(x + src + v * 8);
+      q.store(y + dst + v * 8);
+    } else {
+      y[dst + v] = x[src + v];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int vu_mean_groups(const float* x, int groups, int64_t n, float* out, void* stream) {
@@ -131,5 +161,18 @@ extern "C" int vu_uncertainty(const float* seg, int samples, int64_t n, float* m
   if (n == 0) return 0;
   hipLaunchKernelGGL(uncertainty_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, seg, samples, n, mean,
                      std, entropy, mutual_info, coeff_var);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_gather_affine(const void* x, int B, int H, int W, int C, const int* map, void* y, int Ho,
+                                int Wo, int dtype, void* stream) {
+  const int64_t n = (int64_t)B * Ho * Wo * ((C % 8 == 0) ? C / 8 : C);
+  if (n == 0) return 0;
+  if (dtype == VU_BF16)
+    hipLaunchKernelGGL(gather_affine_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)x, B, H, W, C, map, (bf16_t*)y, Ho, Wo);
+  else
+    hipLaunchKernelGGL(gather_affine_kernel<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)x, B, H, W, C, map, (float*)y, Ho, Wo);
   return (int)hipGetLastError();
 }
