@@ -94,7 +94,7 @@ VU_DEV float ror_add(float v) {
 }
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
-template <int BN>
+template <int BN, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -127,11 +127,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int tx_n = W / TW, ty_n = H / TH;
   const int mtiles = g.N * ty_n * tx_n;
   const int ntiles = p.ncol / BN;
-  const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
+  // split-K (SPLIT): the block index also picks a K range (kidx); a separate
+  // instantiation so the plain kernel carries none of it (register pressure)
+  const int ksplit = SPLIT ? p.ksplit : 1;
   const int btiles = mtiles * ntiles;
   const int bid0 = xcd_remap(blockIdx.x, btiles * ksplit);
-  const int kidx = bid0 / btiles;  // K-split index (0 without split-K)
-  const int bid = bid0 - kidx * btiles;
+  const int kidx = SPLIT ? bid0 / btiles : 0;
+  const int bid = SPLIT ? bid0 - kidx * btiles : bid0;
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int img = mt / (ty_n * tx_n);
   const int trem = mt - img * (ty_n * tx_n);
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int grp = wid >> 2;  // ping-pong half (one wave of each half per SIMD)
   // this block's contiguous range of 32-channel chunks
   const int call = g.C / 32;
-  const int cbeg = kidx * call / ksplit, cend = (kidx + 1) * call / ksplit;
+  const int cbeg = SPLIT ? kidx * call / ksplit : 0, cend = SPLIT ? (kidx + 1) * call / ksplit : call;
   const int nk = (cend - cbeg) * 9;
 
   // ---- DMA roles ------------------------------------------------------------
@@ -310,17 +312,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   // ---- epilogue ---------------------------------------------------------------
   // acc[i][j][r]: pixel wm*128 + i*16 + (lane&15), channel wn*64 + j*16 + 4*(lane>>4) + r
   const int cbase = wn * 64 + 4 * (lane >> 4);
-  if (ksplit > 1) {
+  if (SPLIT) {
     // split-K: raw fp32 partial tile -> slab kidx (16-byte stores of 4 channels)
-    float* slab = p.workspace + (int64_t)kidx * ((int64_t)g.N * H * W) * p.ncol;
+    float* slab = p.workspace + (int64_t)kidx * ((int64_t)g.N * H * W) * p.ncol + n0 + cbase;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = wm * 128 + i * 16 + (lane & 15);
       const int ty = m / TW, tx = m - (m / TW) * TW;
-      const int64_t gm = ((int64_t)img * H + y0 + ty) * W + x0 + tx;
+      float* row = slab + (((int64_t)img * H + y0 + ty) * W + x0 + tx) * p.ncol;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<f32x4*>(slab + gm * p.ncol + n0 + cbase + j * 16) = acc[i][j];
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(row + j * 16) = acc[i][j];
     }
     return;
   }
@@ -528,13 +529,13 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
   if (ks <= 1) {
     VuGemmFwd q = p;
     q.ksplit = 1;
-    hipLaunchKernelGGL((conv3x3_pp_kernel<BN>), grid, dim3(512), 0, st, q);
+    hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false>), grid, dim3(512), 0, st, q);
     return (int)hipGetLastError();
   }
   if (!p.workspace) return (int)hipErrorInvalidValue;
   VuGemmFwd q = p;
   q.ksplit = ks;
-  hipLaunchKernelGGL((conv3x3_pp_kernel<BN>), grid, dim3(512), 0, st, q);
+  hipLaunchKernelGGL((conv3x3_pp_kernel<BN, true>), grid, dim3(512), 0, st, q);
   const int64_t M = (int64_t)g.N * g.H * g.W;
   hipLaunchKernelGGL(splitk_finish_kernel, dim3((unsigned)((M / 128) * (p.ncol / 64))), dim3(256), 0, st, q);
   return (int)hipGetLastError();
