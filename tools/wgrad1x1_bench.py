@@ -71,7 +71,7 @@ def main():
         g = torch.empty(fi, c, 1, 1, device=dev)
         byts = dy.numel() * 2 + x.numel() * 2
         ms = timeit(lambda: K.gemm_wgrad(K.gather1x1([dy]), K.gather1x1([x]), fi, c, g, (c, 0, 1), _lib.BF16, False))
-        line = f"{name} {fi:4d}x{c:4d} @{h:3d} | dispatch {ms * 1e3:7.1f}us {byts / ms / 1e9:6.0f}GB/s"
+        line = f"{name} {fi:4d}x{c:4d} @{h:3d} | dispatch {ms * 1e3:7.1f}us {byts / ms / 1e6:6.0f}GB/s"
         slab = torch.empty(1024, fi, c, device=dev)
         for s in [int(v) for v in args.splits.split(",")]:
             ms = timeit(lambda: run(K.gather1x1([dy]), K.gather1x1([x]), fi, c, s, slab))

@@ -154,18 +154,26 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
 
   const int nsteps = mend > mbeg ? (int)((mend - mbeg + BMR - 1) / BMR) : 0;
-  // counted-vmcnt ring (see gemm_fwd2.hip): stage st+2 issued after the
-  // barrier of step st into the slot step st-1 finished reading
+  // counted-vmcnt ring, two stages in flight WHILE waiting: at step st the
+  // block first agrees that slot (st-1)%3 has been read (barrier), refills
+  // it with stage st+2, and only then waits for stage st (vmcnt leaves the
+  // two younger stages outstanding) and publishes it (barrier).  These
+  // kernels are HBM/L2-latency bound (SQ_WAIT_ANY 65 % with one stage in
+  // flight at the wait), so the bytes in flight are what sets the rate.
   constexpr int NL = LI + LJ;
   if (nsteps > 0) stage(mbeg, 0);
   if (nsteps > 1) stage(mbeg + BMR, 1);
   const int g4 = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
   for (int st = 0; st < nsteps; ++st) {
-    if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool more = st + 2 < nsteps;
+    if (more) stage(mbeg + (int64_t)(st + 2) * BMR, (st + 2) % NSTAGE);
+    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL) : "memory");
+    else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + 2 < nsteps) stage(mbeg + (int64_t)(st + 2) * BMR, (st + 2) % NSTAGE);
     const int cur = st % NSTAGE;
     const char* Pb = smem + cur * STAGE;
     const char* Qb = Pb + BMR * RBP;
