@@ -35,9 +35,36 @@ template <int RB> VU_DEV int tr_off(int m, int col) {
   return m * RB + (((col >> 4) ^ fsw<RB>(m)) << 5) + ((col & 15) << 1);
 }
 
+// Transposed 16-bit LDS read as inline asm.  Through the builtin, the
+// compiler cannot tell these reads from the LDS-DMA destinations still in
+// flight and puts an s_waitcnt vmcnt(0) in front of them, which drains the
+// whole DMA ring every step; here the ring's counted vmcnt waits + barriers
+// order DMA and reads, and lgkm_wait() below orders reads and MFMAs.
+VU_DEV u32x2 tr_read(const char* p) {
+  u32x2 r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const lds_void*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+// wait until at most N LDS reads are outstanding; the fragments passed are
+// tied to the wait so their consumers cannot be scheduled above it
+template <int N> VU_DEV void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N > 15 ? 15 : N) : "memory");
+}
+VU_DEV void tie(u32x4& v) { asm volatile("" : "+v"(v)); }
+
+// A DMA slot's fixed column: tap, source and channel, with the source's base
+// pointer (channel offset applied) and pixel stride resolved ONCE into
+// registers.  Indexing the kernel-argument arrays g.src[t] / g.stride[t] with
+// a per-lane t inside the step loop makes the compiler fetch them with vector
+// loads and wait for them with s_waitcnt vmcnt(0) -- which, vmcnt being in
+// order, also drains every LDS-DMA stage in flight and serialises the ring
+// (measured: ~12 GB/s per CU).
 struct Col {
-  int r, s, t;
-  int64_t coff;
+  int r, s;
+  const bf16_t* base;
+  int64_t stride;
   bool ok;
 };
 
@@ -48,8 +75,11 @@ VU_DEV Col decode_col(const VuGather& g, int col, int ncols) {
   int tap = cc / g.C, ch = cc - tap * g.C;
   d.r = tap / g.S;
   d.s = tap - d.r * g.S;
-  d.t = (ch >= g.cend[0]) + (g.nsrc > 2 && ch >= g.cend[1]);
-  d.coff = ch - (d.t == 0 ? 0 : g.cend[d.t - 1]);
+  const int t = (ch >= g.cend[0]) + (g.nsrc > 2 && ch >= g.cend[1]);
+  const int coff = ch - (t == 0 ? 0 : (t == 1 ? g.cend[0] : g.cend[1]));
+  const void* src = t == 0 ? g.src[0] : (t == 1 ? g.src[1] : g.src[2]);
+  d.stride = t == 0 ? g.stride[0] : (t == 1 ? g.stride[1] : g.stride[2]);
+  d.base = reinterpret_cast<const bf16_t*>(src) + coff;
   return d;
 }
 
@@ -124,8 +154,7 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     int hs = h * g.sy + d.r * g.dy + g.oy;
     int ws = w * g.sx + d.s * g.dx + g.ox;
     if ((unsigned)hs >= (unsigned)g.Hs || (unsigned)ws >= (unsigned)g.Ws) return zp;
-    const bf16_t* base = reinterpret_cast<const bf16_t*>(g.src[d.t]);
-    return base + (((int64_t)n * g.Hs + hs) * g.Ws + ws) * g.stride[d.t] + d.coff;
+    return d.base + (((int64_t)n * g.Hs + hs) * g.Ws + ws) * d.stride;
   };
 
   auto stage = [&](int64_t mb, int buf) {
@@ -183,17 +212,13 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
 #pragma unroll
       for (int a = 0; a < TI; ++a) {
         int col = wi * (BI / WI) + a * 16 + 4 * pp;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Pb + tr_off<RBP>(m, col)));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Pb + tr_off<RBP>(m + 4, col)));
-        u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        u32x2 l2 = tr_read(Pb + tr_off<RBP>(m, col)), h2 = tr_read(Pb + tr_off<RBP>(m + 4, col));
         af[a] = u32x4{l2[0], l2[1], h2[0], h2[1]};
       }
 #pragma unroll
       for (int b = 0; b < TJ; ++b) {
         int col = wj * (BJ / WJ) + b * 16 + 4 * pp;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qb + tr_off<RBQ>(m, col)));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Qb + tr_off<RBQ>(m + 4, col)));
-        u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+        u32x2 l2 = tr_read(Qb + tr_off<RBQ>(m, col)), h2 = tr_read(Qb + tr_off<RBQ>(m + 4, col));
         bf[b] = u32x4{l2[0], l2[1], h2[0], h2[1]};
       }
     };
@@ -201,7 +226,16 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     load(0, af[0], bf[0]);
 #pragma unroll
     for (int ks = 0; ks < BMR / 32; ++ks) {
-      if (ks + 1 < BMR / 32) load(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+      if (ks + 1 < BMR / 32) {
+        load(ks + 1, af[(ks + 1) & 1], bf[(ks + 1) & 1]);
+        lgkm_wait<2 * (TI + TJ)>();  // k-step ks's reads done, ks+1's may fly
+      } else {
+        lgkm_wait<0>();
+      }
+#pragma unroll
+      for (int a = 0; a < TI; ++a) tie(af[ks & 1][a]);
+#pragma unroll
+      for (int b = 0; b < TJ; ++b) tie(bf[ks & 1][b]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TI; ++a)
