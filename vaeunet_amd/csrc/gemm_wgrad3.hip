@@ -23,7 +23,6 @@
 //     a fixed order: deterministic).
 #include "common.h"
 #include "../../include/vaeunet.h"
-#include <stdlib.h>
 
 static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page_w3[16];
 
@@ -47,17 +46,48 @@ template <int RB> VU_DEV int swz_col(int m, int pc) {
   return ((((pc >> 1) ^ fsw<RB>(m)) << 1) | (pc & 1)) * 8;
 }
 
+// Transposed LDS reads as inline asm: through the builtin the compiler cannot
+// tell them from the next tile's LDS-DMA destinations and inserts an
+// s_waitcnt vmcnt(0) before the first read of a tile -- right after that
+// tile's successor was issued -- which serialises DMA and MFMA (the double
+// buffer never overlapped).  Ordering is explicit instead: vmcnt + barrier
+// for DMA -> reads, lgkm_wait() + tie() for reads -> MFMAs.
+VU_DEV u32x2 tr_read(const char* p) {
+  u32x2 r;
+  const uint32_t a = (uint32_t)(uintptr_t)(const lds_void*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
 VU_DEV u32x4 tr_frag(const char* base, int off_lo, int off_hi) {
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off_lo));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off_hi));
-  u32x2 l2 = __builtin_bit_cast(u32x2, lo), h2 = __builtin_bit_cast(u32x2, hi);
+  u32x2 l2 = tr_read(base + off_lo), h2 = tr_read(base + off_hi);
   return u32x4{l2[0], l2[1], h2[0], h2[1]};
 }
 
-// XM: experiment mode for timing studies (0 in production): 1 = no DMA after
-// the first tile, 2 = no MFMA, 3 = the old full-pitch halo DMA (padding
-// pixels loaded from a zero page).
-template <int BI, int XM, int TJ>
+// at most n LDS operations outstanding (n folds to a constant after unrolling)
+VU_DEV void lgkm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt lgkmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt lgkmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory"); break;
+  }
+}
+VU_DEV void tie(u32x4& v) { asm volatile("" : "+v"(v)); }
+
+template <int BI, int TJ>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   constexpr int NT = 512;
   constexpr int RBP = BI * 2, CPI = BI / 8;
@@ -98,22 +128,23 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   const bf16_t* dsrc = reinterpret_cast<const bf16_t*>(gp.src[0]);
   const int64_t dst_ = gp.stride[0];
 
-  // fixed per-thread DMA slot geometry
-  int p_ty[LP], p_tx[LP], p_col[LP];
+  // fixed per-thread DMA slots, one register each (the accumulators leave
+  // little room): dy slot = element offset from the tile's first pixel (-1:
+  // channel past ni, zero page); halo slot = hy | hx << 4 | col << 10 (-1:
+  // pitch padding / past the last row, no load)
+  int p_off[LP];
 #pragma unroll
   for (int k = 0; k < LP; ++k) {
     int e = k * NT + tid, row = e / CPI, pc = e - row * CPI;
-    p_ty[k] = row / TW;
-    p_tx[k] = row - p_ty[k] * TW;
-    p_col[k] = i0 + swz_col<RBP>(row, pc);
+    const int ty = row / TW, tx = row - ty * TW, col = i0 + swz_col<RBP>(row, pc);
+    p_off[k] = col < p.ni ? (int)((int64_t)(ty * W + tx) * dst_ + col) : -1;
   }
-  int q_hy[NH], q_hx[NH], q_col[NH];
+  int q_pk[NH];
 #pragma unroll
   for (int k = 0; k < NH; ++k) {
     int e = k * NT + tid, hp = e >> 3, pc = e & 7;
-    q_hy[k] = hp / HWP;
-    q_hx[k] = hp - q_hy[k] * HWP;
-    q_col[k] = swz_col<128>(hp, pc);
+    const int hy = hp / HWP, hx = hp - hy * HWP;
+    q_pk[k] = (hy < HROWS && hx < TW + 2) ? (hy | hx << 4 | swz_col<128>(hp, pc) << 10) : -1;
   }
 
   auto stage = [&](int t, int buf) {
@@ -121,25 +152,24 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     const int y0 = (tr / tiles_w) * TH, x0 = (tr - (tr / tiles_w) * tiles_w) * TW;
     char* Pb = smem + buf * STAGE;
     char* Qb = Pb + PB;
+    const bf16_t* dtile = dsrc + (((int64_t)img * H + y0) * W + x0) * dst_;
 #pragma unroll
     for (int k = 0; k < LP; ++k) {
-      const void* s = zp;
-      if (p_col[k] < p.ni) {
-        int64_t pix = ((int64_t)img * H + y0 + p_ty[k]) * W + x0 + p_tx[k];
-        s = dsrc + pix * dst_ + p_col[k];
-      }
+      const void* s = p_off[k] >= 0 ? (const void*)(dtile + p_off[k]) : zp;
       __builtin_amdgcn_global_load_lds(s, (lds_void*)(Pb + (k * NT + wid * 64) * 16), 16, 0, 0);
     }
     // halo: only the 34 used pixels of each 48-pixel row are loaded (lanes on
     // the pitch padding or past the last row issue nothing; a wave whose
     // lanes are all padding skips the instruction)
+    const bf16_t* ximg = xsrc + (int64_t)img * H * W * xst;
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
-      if (XM == 3 || (q_hy[k] < HROWS && q_hx[k] < TW + 2)) {
-        const int y = y0 - 1 + q_hy[k], x = x0 - 1 + q_hx[k];
+      const int q = q_pk[k];
+      if (q >= 0) {
+        const int y = y0 - 1 + (q & 15), x = x0 - 1 + ((q >> 4) & 63);
         const void* s = zp;
-        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W && q_hy[k] < HROWS && q_hx[k] < TW + 2)
-          s = xsrc + (((int64_t)img * H + y) * W + x) * xst + q_col[k];
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+          s = ximg + (int64_t)(y * W + x) * xst + (q >> 10);
         __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
       }
     }
@@ -177,7 +207,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (XM != 1 && st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
+    if (st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
     const char* Pb = smem + (st & 1) * STAGE;
     const char* Qb = Pb + PB;
     // software-pipelined fragment reads over the 36 (k-step, tap) MFMA groups
@@ -198,6 +228,9 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     load_a(0, aq[0]);
     load_b(0, bq[0]);
     load_b(1, bq[1]);
+    // LDS reads issued for group x (its B fragments, plus a k-step's A
+    // fragments ahead of its first tap)
+    auto nreads = [&](int x) { return x >= NG ? 0 : 2 * TJ + ((x % 9 == 0 && x > 0) ? 2 * TI : 0); };
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int ks = g / 9, t = g - (g / 9) * 9;
@@ -205,15 +238,21 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
         if ((g + 2) % 9 == 0) load_a((g + 2) / 9, aq[((g + 2) / 9) & 1]);
         load_b(g + 2, bq[(g + 2) % 3]);
       }
+      // group g's fragments (and every older read) are complete once only the
+      // reads of groups g+1 and g+2 may still be outstanding
+      lgkm_wait(nreads(g + 1) + nreads(g + 2));
+#pragma unroll
+      for (int a = 0; a < TI; ++a) tie(aq[ks & 1][a]);
+#pragma unroll
+      for (int b = 0; b < TJ; ++b) tie(bq[g % 3][b]);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TI; ++a)
 #pragma unroll
         for (int b = 0; b < TJ; ++b)
-          if (XM != 2) acc[a][b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          acc[a][b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8, aq[ks & 1][a]), __builtin_bit_cast(bf16x8, bq[g % 3][b]), acc[a][b][t], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
-      if (XM == 2) asm volatile("" ::"v"(bq[g % 3][0]), "v"(aq[ks & 1][0]));
     }
   }
 
@@ -233,26 +272,11 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       }
 }
 
-int xmode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("VU_W3_XM");
-    m = e ? atoi(e) : 0;
-  }
-  return m;
-}
-
 template <int BI>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int64_t nblk = (int64_t)((p.ni + BI - 1) / BI) * (p.q.C / 64) * p.splits;
   if (nblk <= 0) return 0;
-  const dim3 grid((unsigned)nblk), blk(512);
-  switch (xmode()) {
-    case 1: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, 1>), grid, blk, 0, st, p); break;
-    case 2: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 2, 1>), grid, blk, 0, st, p); break;
-    case 3: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 3, 1>), grid, blk, 0, st, p); break;
-    default: hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 0, 1>), grid, blk, 0, st, p);
-  }
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -277,6 +301,7 @@ int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
     if (g.cend[t] % 64 || g.stride[t] % 8) return 0;
   if (g.W % TW || g.H % TH) return 0;
   if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
+  if ((int64_t)TH * g.W * a.stride[0] >= (int64_t)1 << 31) return 0;   // 32-bit dy slot offsets
   *bi = p.ni <= 64 ? 64 : 128;
   *bj = 9 * 64;
   return 1;
