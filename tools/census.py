@@ -1,0 +1,136 @@
+"""Per-call-site GPU time of one training step: every C-ABI launch of the
+engine is bracketed by HIP events (on the launch stream) and attributed to
+its engine call site and, for the GEMMs, to its shape and algorithmic HBM
+bytes.  A tuning aid, not part of the product.
+
+usage: python tools/census.py [--model unet|vae] [--steps 2] [--top 60]
+"""
+import argparse
+import collections
+import ctypes as C
+import os
+import sys
+import traceback
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vaeunet_amd import _lib, kernels as K  # noqa: E402
+
+RECS = []
+ON = [False]
+_orig = _lib.call
+ENGINE = ("engine.py", "vae_engine.py", "unet_parts.py", "unet_resnet.py", "loss.py", "optim.py", "functional.py")
+
+
+def _site():
+    for f in reversed(traceback.extract_stack()[:-3]):
+        if f.filename.endswith(ENGINE):
+            return f"{os.path.basename(f.filename)}:{f.name}:{f.lineno}"
+    return "?"
+
+
+def _shape(name, args):
+    try:
+        if name == "vu_gemm_fwd":
+            a = args[0]._obj
+            g = a.a
+            M = g.N * g.H * g.W
+            K_ = g.R * g.S * g.C
+            b = M * g.C * 2 + M * a.ncol * 2 + a.ncol * K_ * 2
+            return f"fwd R{g.R} C{g.C} {g.H}x{g.W} N{a.ncol}", b, 2 * M * K_ * a.ncol
+        if name == "vu_gemm_wgrad":
+            w = args[0]._obj
+            M = w.p.N * w.p.H * w.p.W
+            b = M * (w.p.C + w.q.C) * 2
+            return f"wgrad R{w.q.R} {w.q.H}x{w.q.W} ni{w.ni} nj{w.nj} s{w.splits}", b, 2 * M * w.ni * w.nj
+    except Exception:  # noqa: BLE001
+        pass
+    return "", 0, 0
+
+
+def tcall(name, *args):
+    if not ON[0]:
+        return _orig(name, *args)
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    rc = _orig(name, *args)
+    e.record()
+    shp, b, fl = _shape(name, args)
+    RECS.append((name, _site(), shp, b, fl, s, e))
+    return rc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="unet")
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--top", type=int, default=70)
+    args = ap.parse_args()
+    import importlib
+    _lib.call = tcall
+    for m in ("kernels", "loss", "optim", "metrics", "fp8"):
+        mod = importlib.import_module("vaeunet_amd." + m)
+        if hasattr(mod, "call"):
+            mod.call = tcall
+    dev = torch.device("cuda")
+    from vaeunet_amd import UNet, UNetResNet
+    from vaeunet_amd.init import seeded_init_
+    from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
+    from vaeunet_amd.optim import FusedAdamW, clip_grad_norm_
+    vae = args.model == "vae"
+    model = (UNetResNet(3, 1, pretrained=False) if vae else UNet(3, 2))
+    model = seeded_init_(model, 0).to(dev).to(memory_format=torch.channels_last).train()
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-5)
+    crit = CombinedLoss()
+    from bench import synthetic
+    x, t = synthetic(8, 512, 1 if vae else 2, 0, dev)
+
+    def step():
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if vae:
+                lg, mu, lv = model(x)
+                loss = crit(lg, t) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+            else:
+                loss = crit(model(x), t)
+        loss.backward()
+        clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    ON[0] = True
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ON[0] = False
+    agg = collections.OrderedDict()
+    tot = 0.0
+    for name, site, shp, b, fl, s, e in RECS:
+        ms = s.elapsed_time(e)
+        tot += ms
+        d = agg.setdefault((name, site, shp), [0, 0.0, b, fl])
+        d[0] += 1
+        d[1] += ms
+    n = args.steps
+    print(f"# {len(RECS) // n} launches/step, {tot / n:.3f} ms/step inside events")
+    rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    for (name, site, shp), (cnt, ms, b, fl) in rows[:args.top]:
+        us = ms / cnt * 1e3
+        extra = ""
+        if b:
+            extra = f" {b / (us * 1e-6) / 1e9:7.0f}GB/s {fl / (us * 1e-6) / 1e12:6.0f}TF"
+        print(f"{ms / n:7.3f} ms/step {cnt // n:3d}x {us:8.1f}us  {name[:22]:22s} {site[:44]:44s} {shp}{extra}")
+    by = collections.defaultdict(float)
+    for (name, _, _), (cnt, ms, b, fl) in agg.items():
+        by[name] += ms / n
+    print("# by entry point")
+    for k, v in sorted(by.items(), key=lambda kv: -kv[1]):
+        print(f"{v:7.3f} ms/step  {k}")
+
+
+if __name__ == "__main__":
+    main()

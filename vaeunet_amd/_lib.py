@@ -11,6 +11,10 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvaeunet_hip.so")
+# A/B timing of two builds of the same sources (tools/*_bench.py): an
+# alternative library file; the product never sets it
+if os.environ.get("VU_LIB_PATH"):
+    LIB_PATH = os.environ["VU_LIB_PATH"]
 
 F32, BF16 = 0, 1
 

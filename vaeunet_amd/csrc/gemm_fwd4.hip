@@ -29,7 +29,13 @@
 //     partial statistics a register + 16-lane reduction and the bf16 output
 //     staging 8-byte LDS writes;
 //   * epilogue: bias, storage rounding, per-wave (sum, centered M2) of the
-//     rounded values (same contract as v1-v3), 16-byte NHWC stores;
+//     rounded values (same contract as v1-v3) by DPP row sums, then each
+//     wave stages its tile 32 pixels at a time through a private LDS strip
+//     and stores whole 128-byte pixel rows (16 bytes per lane);
+//   * the step loop is (chunk, tap) with the weight ring slot = tap % 3 and
+//     the halo slot addresses recomputed per chunk: no per-step divisions and
+//     no per-slot register arrays live across the MFMAs (measured 6 % faster
+//     than a flat step loop with precomputed slots);
 //   * split-K for grids under one block per CU (the 32x32 and 64x64 levels:
 //     down4 convs and their input gradients have 64-128 256x256 tiles for
 //     256 CUs): each block walks a contiguous range of 32-channel chunks and
@@ -37,7 +43,6 @@
 //     a fixed order and applies the epilogue above (deterministic).
 #include "common.h"
 #include "../../include/vaeunet.h"
-#include <stdlib.h>
 
 static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page4[16];
 
@@ -50,31 +55,12 @@ template <> struct PP<256> { static constexpr int WM = 2, WN = 4, TH = 8, TW = 3
 template <> struct PP<128> { static constexpr int WM = 4, WN = 2, TH = 16, TW = 32; };
 template <> struct PP<64> { static constexpr int WM = 8, WN = 1, TH = 32, TW = 32; };
 
-VU_DEV void wait_vm(int n) {
-  switch (n) {
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
-    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
-    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
+// at most N vector-memory operations of this wave outstanding (loads AND
+// stores: CDNA counts both in vmcnt, in issue order)
+template <int N>
+VU_DEV void wait_vm_c() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // A workgroup barrier nothing is scheduled across (the ping-pong relies on
@@ -98,7 +84,6 @@ template <int BN, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
-  constexpr int NT = 512;
   constexpr int BM = TH * TW;
   static_assert(BM == WM * 128 && BN == WN * 64 && WM * WN == 8, "wave grid");
   constexpr int HW = TW + 2, HP = (TH + 2) * HW;
@@ -110,27 +95,27 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int LB0A = (LB0 + 1) / 2;             // ... issued in phase 1 (rest in phase 2)
   constexpr int WSLOT = BN * 64;
   constexpr int PD = NBW - 1;                     // weight prefetch distance (steps)
-  // the whole next-chunk halo goes out at step 0 of the current chunk
-  // (measured 5 % faster than spreading it over steps 0..7: the HBM/MALL
-  // latency gets 8 steps of cover)
-  constexpr int PPS1 = NHP1;
   constexpr int MAIN = 2 * HALO + NBW * WSLOT;
-  constexpr int ROWB = BN * 2 + 16;               // bf16 staging row (padded)
-  constexpr int EPI = BM * ROWB;
-  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
-  static_assert(LDS_BYTES <= 163840, "LDS");
-  static_assert(NHP1 <= 8 * PPS1 && LB0 >= 1, "DMA schedule");
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  // epilogue: each wave stages 32-pixel rows of its tile through a private
+  // LDS strip (the main-loop buffers, free by then) and stores whole 128-byte
+  // pixel rows
+  constexpr int SPITCH = 144;                     // staged pixel row (128 B + pad)
+  constexpr int STG = 32 * SPITCH;
+  static_assert(MAIN <= 163840 && 8 * STG <= MAIN, "LDS");
+  static_assert(LB0 >= 1, "DMA schedule");
+  static_assert(9 % NBW == 0, "ring slot = tap % NBW");
+  static_assert(TW == 32, "fragment geometry");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const VuGather& g = p.a;
   const int H = g.H, W = g.W;
   const int tx_n = W / TW, ty_n = H / TH;
   const int mtiles = g.N * ty_n * tx_n;
   const int ntiles = p.ncol / BN;
+  const int btiles = mtiles * ntiles;
   // split-K (SPLIT): the block index also picks a K range (kidx); a separate
   // instantiation so the plain kernel carries none of it (register pressure)
   const int ksplit = SPLIT ? p.ksplit : 1;
-  const int btiles = mtiles * ntiles;
   const int bid0 = xcd_remap(blockIdx.x, btiles * ksplit);
   const int kidx = SPLIT ? bid0 / btiles : 0;
   const int bid = SPLIT ? bid0 - kidx * btiles : bid0;
@@ -139,15 +124,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int trem = mt - img * (ty_n * tx_n);
   const int y0 = (trem / tx_n) * TH, x0 = (trem - (trem / tx_n) * tx_n) * TW;
   const int n0 = nt * BN;
+  // this block's contiguous range of 32-channel chunks
+  const int call = g.C / 32;
+  const int cbeg = SPLIT ? kidx * call / ksplit : 0, cend = SPLIT ? (kidx + 1) * call / ksplit : call;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int grp = wid >> 2;  // ping-pong half (one wave of each half per SIMD)
-  // this block's contiguous range of 32-channel chunks
-  const int call = g.C / 32;
-  const int cbeg = SPLIT ? kidx * call / ksplit : 0, cend = SPLIT ? (kidx + 1) * call / ksplit : call;
-  const int nk = (cend - cbeg) * 9;
 
   // ---- DMA roles ------------------------------------------------------------
   // vmcnt counts a wave's loads in issue order, so a wave that mixes slow
@@ -157,16 +141,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   // next chunk's halo (and wait for it once per chunk).
   const int gt = tid & 255;        // thread index inside the half
   const int gw = wid & 3;          // wave index inside the half
-  int hpix[NHP1];  // (half 1) halo pixel of each halo slot (-1 = zero pad)
-#pragma unroll
-  for (int i = 0; i < NHP1; ++i) {
-    const int P = i * 256 + gt;
-    const int px = P >> 2;
-    const int hy = px / HW, hx = px - (px / HW) * HW;
-    const int y = y0 - 1 + hy, x = x0 - 1 + hx;
-    const bool ok = P < HPIECES && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-    hpix[i] = ok ? (img * H + y) * W + x : -1;
-  }
   const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
   const void* zp = (const void*)vu_zero_page4;
   char* const hbuf = smem;
@@ -178,9 +152,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const bf16_t* const src2 = reinterpret_cast<const bf16_t*>(g.src[2]);
   const int64_t st0 = g.stride[0], st1 = g.stride[1], st2 = g.stride[2];
   const int ce0 = g.cend[0], ce1 = g.nsrc > 2 ? g.cend[1] : (1 << 30);
-  // chunk c's source pointer (channel offset applied) and pixel stride
-  auto chunk_src = [&](int c, const bf16_t*& src, int64_t& st) {
+  // (half 1) the whole halo of chunk c into buffer buf; slot geometry is
+  // recomputed per chunk (a per-slot register array would stay live through
+  // the MFMA loop: 19 registers at BN = 64)
+  auto halo_chunk = [&](int c, int buf) {
+    int ib = img, yb = y0, xb = x0;
+    asm volatile("" : "+s"(ib), "+s"(yb), "+s"(xb));  // keep the slot math inside the loop
     const int cb = c * 32;
+    const bf16_t* src;
+    int64_t st;
     if (cb < ce0) {
       src = src0 + cb;
       st = st0;
@@ -191,22 +171,26 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       src = src2 + (cb - ce1);
       st = st2;
     }
-  };
-  // (half 1) halo slot i of chunk c; the last slot may cover a partial wave
-  auto halo_slot = [&](const bf16_t* src, int64_t st, int c, int i) {
-    if (i * 256 + gw * 64 >= HPIECES) return;  // wave-uniform
-    const int P = i * 256 + gt;
-    if (P < HPIECES) {
-      const void* gp = hpix[i] >= 0 ? (const void*)(src + (int64_t)hpix[i] * st + (P & 3) * 8) : zp;
-      char* dst = hbuf + (c & 1) * HALO + (i * 256 + gw * 64) * 16;
-      __builtin_amdgcn_global_load_lds(gp, (lds_void*)dst, 16, 0, 0);
+    src += (int64_t)ib * H * W * st + (gt & 3) * 8;
+#pragma unroll
+    for (int i = 0; i < NHP1; ++i) {
+      if (i * 256 + gw * 64 >= HPIECES) continue;  // wave-uniform
+      const int P = i * 256 + gt;
+      if (P < HPIECES) {
+        const int px = P >> 2;
+        const int hy = px / HW, hx = px - (px / HW) * HW;
+        const int y = yb - 1 + hy, x = xb - 1 + hx;
+        const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        const void* gp = ok ? (const void*)(src + (int64_t)(y * W + x) * st) : zp;
+        char* dst = hbuf + buf * HALO + (i * 256 + gw * 64) * 16;
+        __builtin_amdgcn_global_load_lds(gp, (lds_void*)dst, 16, 0, 0);
+      }
     }
   };
-  // (half 0) weight slots [i0, i1) of step s
-  auto wstage = [&](int s, int i0, int i1) {
-    const int c = cbeg + s / 9, t = s - (s / 9) * 9;
+  // (half 0) weight slots [i0, i1) of (chunk c, tap t) into ring slot `slot`
+  auto wstage = [&](int c, int t, int slot, int i0, int i1) {
     const int k0 = t * g.C + c * 32;
-    char* B = wbuf + (s % NBW) * WSLOT;
+    char* B = wbuf + slot * WSLOT;
 #pragma unroll
     for (int i = 0; i < LB0; ++i) {
       if (i < i0 || i >= i1) continue;
@@ -216,24 +200,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * 256 + gw * 64) * 16), 16, 0, 0);
     }
   };
-  auto halo_chunk = [&](int c, int t) {  // (half 1) slots of chunk c issued at chunk step t
-    const bf16_t* src;
-    int64_t st;
-    chunk_src(c, src, st);
-#pragma unroll
-    for (int i = 0; i < NHP1; ++i)
-      if (t < 0 || i / PPS1 == t) halo_slot(src, st, c, i);
-  };
 
   // ---- fragment addressing -------------------------------------------------
-  int arow[8];  // halo byte offset of this lane's pixel in each A fragment (tap (0,0))
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = wm * 128 + i * 16 + (lane & 15);
-    const int ty = m / TW, tx = m - (m / TW) * TW;
-    arow[i] = (ty * HW + tx) * 64 + (lane >> 4) * 16;
-  }
+  // A fragment i of a wave covers tile pixels wm*128 + i*16 + (0..15): row
+  // wm*4 + i/2, columns (i&1)*16 + (0..15) (TW = 32), so its halo byte offset
+  // (tap (0,0)) is one per-lane base plus a compile-time constant
+  const int abase = ((wm * 4) * HW + (lane & 15)) * 64 + (lane >> 4) * 16;
+  auto arow = [&](int i) { return abase + ((i >> 1) * HW + (i & 1) * 16) * 64; };
   const int brow = (wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16;
+  const int cbase = wn * 64 + 4 * (lane >> 4);
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -243,83 +218,94 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
 
   // ---- prologue: halo of chunk 0, weights of steps 0 and 1 -----------------
   if (grp) {
-    halo_chunk(cbeg, -1);
+    halo_chunk(cbeg, 0);
   } else {
-#pragma unroll
-    for (int q = 0; q < PD; ++q)
-      if (q < nk) wstage(q, 0, LB0);
+    wstage(cbeg, 0, 0, 0, LB0);
+    wstage(cbeg, 1, 1, 0, LB0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
   if (grp) pp_barrier();  // the stagger: half 1 runs one barrier behind
 
-  for (int s = 0; s < nk; ++s) {
-    const int c = cbeg + s / 9, t = s - (s / 9) * 9;
-    const char* A = hbuf + (c & 1) * HALO + ((t / 3) * HW + (t - (t / 3) * 3)) * 64;
-    const char* Bw = wbuf + (s % NBW) * WSLOT;
-    u32x4 bf[4], af[4];
-    // -- phase 1: weights + pixel fragments 0..3; half 0 prefetches weights(s+2)
+  // steps = (chunk c, tap t); a chunk has 9 = 3 x NBW taps, so the weight
+  // ring slot of tap t is t % 3 in every chunk
+  int hb = 0;  // halo buffer of the current chunk
+  for (int c = cbeg; c < cend; ++c) {
+    const bool next_here = c + 1 < cend;
+    const char* Ah = hbuf + hb * HALO;
+    for (int t = 0; t < 9; ++t) {
+      const int ty = (t * 11) >> 5, tx = t - ty * 3;  // t / 3, t % 3 (t < 9)
+      const char* A = Ah + (ty * HW + tx) * 64;
+      const int slot = tx;                             // t % NBW (= t % 3)
+      const char* Bw = wbuf + slot * WSLOT;
+      const int pslot = slot == 0 ? 2 : slot - 1;      // (t + 2) % NBW
+      const int pt = t + PD < 9 ? t + PD : t + PD - 9;
+      const bool pref = t + PD < 9 || next_here;      // the step two ahead exists
+      const int pc = t + PD < 9 ? c : c + 1;
+      u32x4 bf[4], af[4];
+      // -- phase 1: weights + pixel fragments 0..3; half 0 prefetches the
+      //    weights two steps ahead
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(Bw + brow + j * 16 * 64);
+      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(Bw + brow + j * 16 * 64);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[i]);
-    if (!grp && s + PD < nk) wstage(s + PD, 0, LB0A);
-    pp_barrier();
-    __builtin_amdgcn_s_setprio(1);
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow(i));
+      if (!grp && pref) wstage(pc, pt, pslot, 0, LB0A);
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
-                                                            __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    // -- phase 2: pixel fragments 4..7; half 0 finishes weights(s+2) and waits
-    //    for weights(s+1); half 1 streams the next chunk's halo and waits for
-    //    it at the chunk's last step
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+                                                              __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+      // -- phase 2: pixel fragments 4..7; half 0 finishes the prefetch and
+      //    waits for the next step's weights; half 1 streams the next chunk's
+      //    halo and waits for it at the chunk's last tap
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow[4 + i]);
-    if (!grp) {
-      // outstanding weight steps after this issue: s+1 .. min(nk-1, s+PD);
-      // step s+1 must have landed
-      if (s + PD < nk) {
-        wstage(s + PD, LB0A, LB0);
-        wait_vm((PD - 1) * LB0);
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const u32x4*>(A + arow(4 + i));
+      if (!grp) {
+        if (pref) {
+          wstage(pc, pt, pslot, LB0A, LB0);
+          wait_vm_c<(PD - 1) * LB0>();  // only the prefetch just issued may be in flight
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       } else {
-        const int out = nk - 2 - s;
-        wait_vm(out > 0 ? out * LB0 : 0);
+        if (t == 0 && next_here) halo_chunk(c + 1, hb ^ 1);
+        if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-    } else if (c + 1 < cend) {
-      if (t * PPS1 < NHP1) halo_chunk(c + 1, t);
-      if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+                                                                  __builtin_bit_cast(bf16x8, af[i]), acc[4 + i][j], 0,
+                                                                  0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
     }
-    pp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
-                                                                __builtin_bit_cast(bf16x8, af[i]), acc[4 + i][j], 0, 0,
-                                                                0);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
+    hb ^= 1;
   }
   if (!grp) pp_barrier();  // re-align the halves
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
 
-  // ---- epilogue ---------------------------------------------------------------
-  // acc[i][j][r]: pixel wm*128 + i*16 + (lane&15), channel wn*64 + j*16 + 4*(lane>>4) + r
-  const int cbase = wn * 64 + 4 * (lane >> 4);
+  // ---- epilogue -------------------------------------------------------------
+  // acc[i][j][r]: pixel wm*128 + i*16 + (lane&15), channel n0 + cbase + j*16 + r
+  // Epilogue-only arguments are re-read from the kernarg segment through an
+  // opaque pointer so that they are not held in SGPRs across the MFMA loop.
+  const __attribute__((address_space(4))) VuGemmFwd* ep =
+      (const __attribute__((address_space(4))) VuGemmFwd*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ep));
   if (SPLIT) {
     // split-K: raw fp32 partial tile -> slab kidx (16-byte stores of 4 channels)
-    float* slab = p.workspace + (int64_t)kidx * ((int64_t)g.N * H * W) * p.ncol + n0 + cbase;
+    float* const sbase = ep->workspace + (int64_t)kidx * ((int64_t)g.N * H * W) * ep->ncol + n0 + cbase +
+                         (((int64_t)img * H + y0 + wm * 4) * W + x0 + (lane & 15)) * ep->ncol;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int m = wm * 128 + i * 16 + (lane & 15);
-      const int ty = m / TW, tx = m - (m / TW) * TW;
-      float* row = slab + (((int64_t)img * H + y0 + ty) * W + x0 + tx) * p.ncol;
+      float* row = sbase + ((i >> 1) * (int64_t)W + (i & 1) * 16) * ep->ncol;
 #pragma unroll
       for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(row + j * 16) = acc[i][j];
     }
@@ -329,15 +315,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float bv = p.bias ? p.bias[n0 + cbase + j * 16 + r] : 0.f;
+      const float bv = ep->bias ? ep->bias[n0 + cbase + j * 16 + r] : 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
     }
   }
-  if (p.stat_sum) {
+  if (ep->stat_sum) {
     // per-wave statistics tile: its 128 pixels (8 fragments x one 16-lane DPP
-    // row), two-pass (sum, centered M2); no block barrier, no LDS
-    const int64_t so = (int64_t)(mt * WM + wm) * p.ncol + n0 + cbase;
+    // row), two-pass (sum, centered M2) of the rounded values; lane (g4, x)
+    // keeps column (x/4)*16 + 4*g4 + x%4 of the wave's 64, so the tile's 64
+    // columns go out in one store per statistic
+    float ms = 0.f, mq = 0.f;
+    const int x = lane & 15;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -354,42 +343,67 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
           q += d * d;
         }
         q = row16_sum(q);
-        if ((lane & 15) == 0) {
-          p.stat_sum[so + j * 16 + r] = sv;
-          p.stat_m2[so + j * 16 + r] = q;
+        if (x == j * 4 + r) {
+          ms = sv;
+          mq = q;
         }
       }
+    const int64_t so = (int64_t)(mt * WM + wm) * ep->ncol + n0 + wn * 64 + (x >> 2) * 16 + 4 * (lane >> 4) + (x & 3);
+    ep->stat_sum[so] = ms;
+    ep->stat_m2[so] = mq;
   }
-  // bf16 staging: 8-byte writes of 4 consecutive channels of one pixel
+  u32x2 pk[8][4];  // bf16 pairs: channels (4*g4 + j*16) + {0,1}, {2,3}
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = wm * 128 + i * 16 + (lane & 15);
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      u32x2 v;
-      v[0] = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
-      v[1] = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
-      *reinterpret_cast<u32x2*>(smem + m * ROWB + (cbase + j * 16) * 2) = v;
+      pk[i][j][0] = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+      pk[i][j][1] = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
     }
-  }
+  // the main-loop buffers are free once every wave is past its last fragment read
   __syncthreads();
-  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-  constexpr int CPR = BN / 8;
-#pragma unroll 4
-  for (int e = tid; e < BM * CPR; e += NT) {
-    const int row = e / CPR, cc = e - (e / CPR) * CPR;
-    const int ty = row / TW, tx = row - (row / TW) * TW;
-    const int64_t m = ((int64_t)img * H + y0 + ty) * W + x0 + tx;
-    bf16_t* dst = out + m * p.out_stride + p.out_coff + n0 + cc * 8;
-    Vec8<bf16_t> v;
-    v.v = *reinterpret_cast<const u32x4*>(smem + row * ROWB + cc * 16);
-    if (p.accumulate) {
-      Vec8<bf16_t> o;
-      o.load(dst);
+  // fragments 2h and 2h+1 are the 32 pixels of tile row wm*4 + h
+  bf16_t* const orow0 = reinterpret_cast<bf16_t*>(ep->out) + ep->out_coff + n0 + wn * 64 +
+                        (((int64_t)img * H + y0 + wm * 4) * W + x0) * ep->out_stride;
+  const int64_t orow_y = (int64_t)W * ep->out_stride;
+  char* const stg = smem + wid * STG;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v.set(q, o.get(q) + v.get(q));
+  for (int h = 0; h < 4; ++h) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<u32x2*>(stg + (ii * 16 + (lane & 15)) * SPITCH + (j * 16 + 4 * (lane >> 4)) * 2) =
+            pk[2 * h + ii][j];
+    u32x4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = q * 64 + lane;
+      v[q] = *reinterpret_cast<const u32x4*>(stg + (e >> 3) * SPITCH + (e & 7) * 16);
     }
-    v.store(dst);
+    bf16_t* const orow = orow0 + h * orow_y;
+    if (ep->accumulate) {
+      // out += result, rounded once more (a bf16 tensor add)
+      u32x4 old[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = q * 64 + lane;
+        old[q] = *reinterpret_cast<const u32x4*>(orow + (e >> 3) * ep->out_stride + (e & 7) * 8);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float lo = __uint_as_float(old[q][w] << 16) + __uint_as_float(v[q][w] << 16);
+          const float hi = __uint_as_float(old[q][w] & 0xffff0000u) + __uint_as_float(v[q][w] & 0xffff0000u);
+          v[q][w] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = q * 64 + lane;
+      *reinterpret_cast<u32x4*>(orow + (e >> 3) * ep->out_stride + (e & 7) * 8) = v[q];
+    }
   }
 }
 
@@ -525,13 +539,14 @@ template <int BN>
 int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
   const VuGather& g = p.a;
   const int64_t mt = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW);
-  const dim3 grid((unsigned)(mt * (p.ncol / BN) * ks));
+  const int64_t tiles = mt * (p.ncol / BN);
   if (ks <= 1) {
     VuGemmFwd q = p;
     q.ksplit = 1;
-    hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false>), grid, dim3(512), 0, st, q);
+    hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     return (int)hipGetLastError();
   }
+  const dim3 grid((unsigned)(tiles * ks));
   if (!p.workspace) return (int)hipErrorInvalidValue;
   VuGemmFwd q = p;
   q.ksplit = ks;
