@@ -251,6 +251,9 @@ STREAM_CASES = [
     (64, 32, False),
     (128, 64, False),
     (32, 64, True),
+    (64, 128, False),   # 8 column fragments per wave tile
+    (128, 256, False),  # 16 column fragments, 16-pixel wave tiles
+    (64, 128, True),
 ]
 
 
@@ -271,7 +274,7 @@ def test_gemm_stream_kernel(case):
     ref = F.conv2d(x, w.to(torch.bfloat16).float(), b)
     if not acc:
         out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
-        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out, K.gather1x1)) in (32, 64)
+        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out, K.gather1x1)) in (16, 32, 64)
         st = K.gemm_fwd(K.gather1x1([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
         _close(out, ref, "bf16", what="stream fwd")
         stored = out.float().cpu()
@@ -290,6 +293,24 @@ def test_gemm_stream_kernel(case):
         exp = base.clone()
         exp[:, 32:] += ref
         _close(wide, exp, "bf16", what="stream accumulate")
+
+
+@pytest.mark.parametrize("cin,cout", [(128, 64), (64, 32)])
+def test_gemm_stream_convT(cin, cout):
+    """ConvTranspose2d 2x2/s2 (unet_parts.py:76) on the stream kernel: N = 4*cout
+    columns stored through the pixel shuffle, bias per output channel."""
+    K, E = _k()
+    N, H, W = 2, 128, 128
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(N, cin, H, W, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(cin, cout, 2, 2, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g)
+    d = _code("bf16")
+    out = K.empty_act(N, cout, 2 * H, 2 * W, torch.bfloat16, DEV)
+    K.gemm_fwd(K.gather1x1([_act(x, "bf16")]), E.wT_fwd(w.to(DEV), d), 4 * cout, out, d, bias=b.to(DEV),
+               convT=(2 * H, 2 * W, 0, 0, cout))
+    ref = F.conv_transpose2d(x, w.to(torch.bfloat16).float(), b, stride=2)
+    _close(out, ref, "bf16", what="stream convT")
 
 
 def _row_tile_args(K, srcs, wmat, ncol, out, gather=None):

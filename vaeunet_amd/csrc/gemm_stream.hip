@@ -1,14 +1,17 @@
-// Short-K, narrow-N 1x1 GEMMs as HBM streams ("stream" kernel, bf16):
+// Short-K 1x1 GEMMs as HBM streams ("stream" kernel, bf16):
 // out[m][j] = sum_k A[m][k] B[j][k] (+bias) with K = 32, 64 or 128 and
-// N <= 64 -- the AttentionGate W_g / W_x convolutions of the 256^2 / 512^2
-// levels (unet_parts.py:11,15) and the 512^2 level's input gradients
-// (accumulated into the skip / gate gradients); the ConvTranspose2d
-// pixel-shuffle store (unet_parts.py:76) is supported for N <= 64.  These move 2-3 bytes per flop: at 256-row LDS tiles
-// (gemm_fwd2.hip) a block's life is its load latency and epilogue, so they
-// ran at 2.5-4 TB/s.  Here:
+// N <= 256 -- the AttentionGate W_g / W_x convolutions of the 256^2 / 512^2
+// levels (unet_parts.py:11,15), their input gradients (accumulated into the
+// skip / gate gradients) and the 256^2 -> 512^2 ConvTranspose2d
+// (unet_parts.py:76, pixel-shuffle store).  These move 2-3 bytes per flop: at
+// 256-row LDS tiles (gemm_fwd2.hip) a block's life is its load latency and
+// epilogue, so they ran at 1.5-4 TB/s.  Here:
 //
-//   * the weight matrix (<= 16 KB) is copied into LDS ONCE per block and the
-//     blocks are persistent (one pass over the pixel tiles);
+//   * the weight matrix (<= 64 KB) and bias are copied into LDS ONCE per
+//     block and the blocks are persistent (one pass over the pixel tiles);
+//     an opaque per-tile LDS offset keeps the compiler from hoisting the
+//     weight fragments out of the tile loop (KS x NJ fragments would not fit
+//     the register file at N = 256);
 //   * each wave streams its own 16*NF-pixel tiles straight from global: all
 //     K of a tile (16 bytes = 8 channels per lane and k-step) is in flight
 //     before the first MFMA;
@@ -39,8 +42,8 @@ template <int KS, int NJ, int NF>
 __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
   constexpr int K = 32 * KS, N = 16 * NJ, PX = 16 * NF;
   constexpr int GS = NJ < 4 ? NJ : 4;   // fragments per column group (4*GS consecutive columns per lane)
-  constexpr int RB = K * 2;             // LDS bytes per weight row
-  __shared__ __attribute__((aligned(16))) char wsm[N * RB];
+  __shared__ __attribute__((aligned(16))) char wsm[N * K * 2];
+  __shared__ __attribute__((aligned(16))) float bsm[N];  // bias per output column (ConvT: per cout, expanded)
 
   const VuGather& g = p.a;
   const int64_t M = (int64_t)g.N * g.H * g.W;
@@ -49,33 +52,57 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int gq = lane >> 4, r16 = lane & 15;
 
-  // weights -> LDS (row j = output column j, K contiguous bf16), plain 16-byte copies
+  // A-row r of fragment j -> weight row (output column) of the permuted order
+  auto wrow = [&](int j, int r) { return (j / GS) * 16 * GS + 4 * GS * (r >> 2) + 4 * (j % GS) + (r & 3); };
+  // weights -> LDS in FRAGMENT order: the 64 lanes' 16-byte pieces of
+  // fragment (j, ks) are one contiguous KiB, so every fragment read is a
+  // conflict-free ds_read_b128 (row-major rows of 128/256 bytes put the 16
+  // rows a read touches on the same banks: 16-way conflicts)
   {
     const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
-    constexpr int PIECES = N * K / 8;
+    constexpr int PIECES = NJ * KS * 64;
     for (int e = threadIdx.x; e < PIECES; e += NT) {
-      const int row = e / (K / 8), c8 = e - row * (K / 8);
-      *reinterpret_cast<u32x4*>(wsm + row * RB + c8 * 16) =
-          *reinterpret_cast<const u32x4*>(bmat + (int64_t)row * p.ldb + c8 * 8);
+      const int l = e & 63, jk = e >> 6, j = jk / KS, ks = jk - j * KS;
+      *reinterpret_cast<u32x4*>(wsm + e * 16) =
+          *reinterpret_cast<const u32x4*>(bmat + (int64_t)wrow(j, l & 15) * p.ldb + 32 * ks + 8 * (l >> 4));
     }
+    for (int c = threadIdx.x; c < N; c += NT) bsm[c] = p.bias ? p.bias[p.out_mode == 1 ? c % p.cout : c] : 0.f;
     __syncthreads();
   }
-  // A-row r16 of fragment j -> weight row (column) of the permuted order
-  auto wrow = [&](int j) { return (j / GS) * 16 * GS + 4 * GS * (r16 >> 2) + 4 * (j % GS) + (r16 & 3); };
 
   const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[0]);
   const int64_t st = g.stride[0];
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
   const int HW = g.H * g.W;
 
-  for (int tile = blockIdx.x * (NT / 64) + wid; tile < ntiles; tile += gridDim.x * (NT / 64)) {
+  // the next tile's operands are loaded before this tile's MFMAs and stores:
+  // one tile of loads always in flight per wave (latency, not bandwidth,
+  // bounded a wave that loaded, computed and stored in turn)
+  const int tstride = gridDim.x * (NT / 64);
+  auto load = [&](int tile, u32x4 (&dst)[NF][KS]) {
     const int64_t pb = (int64_t)tile * PX;
-    u32x4 pf[NF][KS];
 #pragma unroll
     for (int f = 0; f < NF; ++f)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
-        pf[f][ks] = *reinterpret_cast<const u32x4*>(src + (pb + 16 * f + r16) * st + 32 * ks + 8 * gq);
+        dst[f][ks] = *reinterpret_cast<const u32x4*>(src + (pb + 16 * f + r16) * st + 32 * ks + 8 * gq);
+  };
+  u32x4 pn[NF][KS];
+  int tile = blockIdx.x * (NT / 64) + wid;
+  if (tile < ntiles) load(tile, pn);
+  for (; tile < ntiles; tile += tstride) {
+    const int64_t pb = (int64_t)tile * PX;
+    // opaque LDS offset: the weight fragments and bias are re-read per tile
+    // instead of being hoisted out of the tile loop (KS x NJ fragments would
+    // not fit the register file at N = 256)
+    int lo = 0;
+    asm volatile("" : "+v"(lo));
+    u32x4 pf[NF][KS];
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) pf[f][ks] = pn[f][ks];
+    if (tile + tstride < ntiles) load(tile + tstride, pn);
     f32x4 acc[NF][NJ];
 #pragma unroll
     for (int f = 0; f < NF; ++f)
@@ -85,7 +112,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const u32x4 wf = *reinterpret_cast<const u32x4*>(wsm + wrow(j) * RB + (32 * ks + 8 * gq) * 2);
+        const u32x4 wf = *reinterpret_cast<const u32x4*>(wsm + lo + ((j * KS + ks) * 64 + lane) * 16);
 #pragma unroll
         for (int f = 0; f < NF; ++f)
           acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf),
@@ -93,14 +120,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
       }
     // acc[f][j][r]: pixel pb + 16f + r16, column (j/GS)*16*GS + 4*GS*gq + 4*(j%GS) + r
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(
+          reinterpret_cast<const char*>(bsm) + lo + ((j / GS) * 16 * GS + 4 * GS * gq + 4 * (j % GS)) * 4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = (j / GS) * 16 * GS + 4 * GS * gq + 4 * (j % GS) + r;
-        const float bv = p.bias ? p.bias[p.out_mode == 1 ? col % p.cout : col] : 0.f;
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(acc[f][j][r] + bv);
-      }
+        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(acc[f][j][r] + bv[r]);
+    }
     if (p.stat_sum) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -128,44 +155,70 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
         }
       }
     }
-    // stores: per column group, 4*GS consecutive bf16 of one pixel
+    // stores.  GS = 4: a lane holds 16 consecutive columns (two 16-byte
+    // chunks) of one pixel per 64-column group; two lane-row swaps
+    // (permlane16 + permlane32) regroup them so that each store instruction
+    // writes 64 contiguous bytes per pixel (lane row q: columns 32h + 8q ..
+    // +7 of the group) instead of 16-byte pieces at a 32-byte stride.
+    auto dst_of = [&](int64_t m, int col0) -> bf16_t* {
+      if (p.out_mode == 1) {
+        const int n = (int)(m / HW);
+        const int rem = (int)(m - (int64_t)n * HW);
+        const int h = rem / g.W, w = rem - (rem / g.W) * g.W;
+        const int ab = col0 / p.cout, co = col0 - ab * p.cout;
+        const int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
+        return out + ((int64_t)(n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
+      }
+      return out + m * p.out_stride + p.out_coff + col0;
+    };
+    auto add_old = [&](u32x4& v, const bf16_t* dst) {
+      const u32x4 o = *reinterpret_cast<const u32x4*>(dst);
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        v[w] = pack2(__uint_as_float(o[w] << 16) + __uint_as_float(v[w] << 16),
+                     __uint_as_float(o[w] & 0xffff0000u) + __uint_as_float(v[w] & 0xffff0000u));
+    };
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       const int64_t m = pb + 16 * f + r16;
 #pragma unroll
       for (int grp = 0; grp < NJ / GS; ++grp) {
-        const int col0 = grp * 16 * GS + 4 * GS * gq;
-        bf16_t* dst;
-        if (p.out_mode == 1) {
-          const int n = (int)(m / HW);
-          const int rem = (int)(m - (int64_t)n * HW);
-          const int h = rem / g.W, w = rem - (rem / g.W) * g.W;
-          const int ab = col0 / p.cout, co = col0 - ab * p.cout;
-          const int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
-          dst = out + ((int64_t)(n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
-        } else {
-          dst = out + m * p.out_stride + p.out_coff + col0;
-        }
+        if constexpr (GS == 4) {
+          u32x4 c[2];
 #pragma unroll
-        for (int h2 = 0; h2 < GS / 2; ++h2) {
-          f32x4 a = acc[f][grp * GS + 2 * h2], b = acc[f][grp * GS + 2 * h2 + 1];
-          if (p.accumulate) {
-            const u32x4 o = *reinterpret_cast<const u32x4*>(dst + 8 * h2);
-            a[0] += __uint_as_float(o[0] << 16);
-            a[1] += __uint_as_float(o[0] & 0xffff0000u);
-            a[2] += __uint_as_float(o[1] << 16);
-            a[3] += __uint_as_float(o[1] & 0xffff0000u);
-            b[0] += __uint_as_float(o[2] << 16);
-            b[1] += __uint_as_float(o[2] & 0xffff0000u);
-            b[2] += __uint_as_float(o[3] << 16);
-            b[3] += __uint_as_float(o[3] & 0xffff0000u);
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const f32x4 a = acc[f][grp * 4 + 2 * h2], b = acc[f][grp * 4 + 2 * h2 + 1];
+            c[h2] = u32x4{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
           }
-          u32x4 pk;
-          pk[0] = pack2(a[0], a[1]);
-          pk[1] = pack2(a[2], a[3]);
-          pk[2] = pack2(b[0], b[1]);
-          pk[3] = pack2(b[2], b[3]);
-          *reinterpret_cast<u32x4*>(dst + 8 * h2) = pk;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const auto r1 = __builtin_amdgcn_permlane16_swap(c[0][w], c[1][w], false, false);
+            const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
+            c[0][w] = r2[0];
+            c[1][w] = r2[1];
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            bf16_t* dst = dst_of(m, grp * 64 + 32 * h + 8 * gq);
+            if (p.accumulate) add_old(c[h], dst);
+            *reinterpret_cast<u32x4*>(dst) = c[h];
+          }
+        } else {
+          bf16_t* dst = dst_of(m, grp * 16 * GS + 4 * GS * gq);
+#pragma unroll
+          for (int h2 = 0; h2 < GS / 2; ++h2) {
+            const f32x4 a = acc[f][grp * GS + 2 * h2], b = acc[f][grp * GS + 2 * h2 + 1];
+            u32x4 v{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
+            if (p.accumulate) {
+              // out += result: unpack the stored pairs and round the sums once
+              const u32x4 o = *reinterpret_cast<const u32x4*>(dst + 8 * h2);
+              v = u32x4{pack2(__uint_as_float(o[0] << 16) + a[0], __uint_as_float(o[0] & 0xffff0000u) + a[1]),
+                        pack2(__uint_as_float(o[1] << 16) + a[2], __uint_as_float(o[1] & 0xffff0000u) + a[3]),
+                        pack2(__uint_as_float(o[2] << 16) + b[0], __uint_as_float(o[2] & 0xffff0000u) + b[1]),
+                        pack2(__uint_as_float(o[3] << 16) + b[2], __uint_as_float(o[3] & 0xffff0000u) + b[3])};
+            }
+            *reinterpret_cast<u32x4*>(dst + 8 * h2) = v;
+          }
         }
       }
     }
@@ -204,6 +257,8 @@ int launch_ks(const VuGemmFwd& p, hipStream_t st) {
   switch (p.ncol / 16) {
     case 2: return launch_nj<KS, 2>(p, st);
     case 4: return launch_nj<KS, 4>(p, st);
+    case 8: return launch_nj<KS, 8>(p, st);
+    case 16: return launch_nj<KS, 16>(p, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -214,7 +269,7 @@ bool g_enabled = true;  // VU_TUNE_STREAM
 
 // Row tile (16*NF pixels) when the stream kernel serves this problem, else 0:
 // bf16 1x1 gather of ONE NHWC source with K = C in {32, 64, 128}, N in {32,
-// 64}, plain (mode 0, optional accumulate) or ConvT pixel-shuffle
+// 64, 128, 256}, plain (mode 0, optional accumulate) or ConvT pixel-shuffle
 // (mode 1, no statistics) output, whole tiles, enough tiles to fill the chip.
 int gemm_stream_bm(const VuGemmFwd& p, int dtype) {
   const VuGather& g = p.a;
@@ -224,8 +279,7 @@ int gemm_stream_bm(const VuGemmFwd& p, int dtype) {
     return 0;
   if (g.C != 32 && g.C != 64 && g.C != 128) return 0;
   const int nj = p.ncol / 16;
-  // N <= 64: wider tiles spill (the epilogue's per-column state outgrows the register file)
-  if (p.ncol % 16 != 0 || (nj != 2 && nj != 4)) return 0;
+  if (p.ncol % 16 != 0 || (nj != 2 && nj != 4 && nj != 8 && nj != 16)) return 0;
   if (g.stride[0] % 8 != 0 || p.ldb % 8 != 0 || p.ldb < g.C || p.out_stride % 8 != 0 || p.out_coff % 8 != 0)
     return 0;
   if (p.out_mode == 1) {
