@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--cpu-no-bf16", action="store_true", help="skip the CPU autocast-bf16 leg")
     ap.add_argument("--torch-optim", action="store_true",
                     help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="replay the step as one captured HIP graph (vaeunet_amd.graph); auto = on "
+                         "at world size 1 with the fused optimizer")
     return ap.parse_args()
 
 
@@ -245,7 +248,28 @@ def main():
         opt.zero_grad(set_to_none=reducer is None)
         return loss
 
-    for _ in range(args.warmup):
+    graphed = None
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and not args.torch_optim)
+    if use_graph:
+        if world > 1 or args.torch_optim:
+            raise SystemExit("--graph on needs world size 1 and the fused optimizer")
+        from vaeunet_amd.graph import GraphedTrainStep
+
+        def fwd_bwd():
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                if vae:
+                    logits, mu, lv = model(x)
+                    loss = crit(logits, t) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+                else:
+                    loss = crit(model(x), t)
+            loss.backward()
+            return loss
+        # warm-up steps run eagerly inside (weights, optimizer state), then one capture
+        graphed = GraphedTrainStep(fwd_bwd, opt, max_norm=1.0, warmup=max(1, args.warmup))
+    eager_step = step
+    if graphed is not None:
+        step = graphed.step
+    for _ in range(0 if graphed else args.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -272,7 +296,7 @@ def main():
         # 2 further steps (events on the launch stream, one pair per launch)
         K.TIMER = K.LaunchTimer()
         for _ in range(2):
-            step()
+            eager_step()   # the same kernels, launched one by one so each can be bracketed
         summ = K.TIMER.summary()
         K.TIMER = None
         fl = sum(v[0] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
@@ -301,7 +325,8 @@ def main():
                                         f"UNet(3,{args.classes}) train step (fwd+CombinedLoss+bwd"
                                         "+clip+AdamW), random-init weights"),
                            "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
-                           "global_batch": args.batch * world, "parallelism": f"dp{world}"},
+                           "global_batch": args.batch * world, "parallelism": f"dp{world}",
+                           "execution": "hipgraph-replay" if graphed is not None else "eager"},
                 "loss": round(float(loss.item()), 6),
                 "roofline": roof, "cpu_baseline": cpu, "parity": parity}
         print(json.dumps(line), flush=True)

@@ -232,6 +232,8 @@ int vu_chan_sum(const void* x, int64_t stride, int N, int H, int W, int y0,
                 float* workspace, int dtype, void* stream);
 int64_t vu_reduce_workspace_bytes(int64_t P, int C);
 int64_t vu_bn_finalize_workspace_bytes(int tiles, int C);
+/* y[p][0..C) = 0 for P pixels at pixel stride ys (channel-slice zero fill) */
+int vu_zero(void* y, int64_t ys, int64_t P, int C, int dtype, void* stream);
 /* generic NHWC copy/cast: y[p*ys + c] = x[p*xs + c] (+ y if accumulate) */
 int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys,
             int ydtype, int64_t P, int C, int accumulate, void* stream);
@@ -373,6 +375,14 @@ int vu_mt_adamw(const VuMtEntry* table, int ntensors, int64_t nchunks,
                 float decay, float one_minus_beta1, float beta2,
                 float one_minus_beta2, float eps, const float* grad_scale,
                 void* stream);
+
+/* Graph-capturable AdamW: *step (device, shared by the table) is incremented
+ * first and the bias corrections are derived from it on the device (double,
+ * rounded to float once: the same values as the host path); zero_grad != 0
+ * clears each gradient after use (persistent .grad buffers for replays). */
+int vu_mt_adamw_dev(const VuMtEntry* table, int ntensors, int64_t nchunks,
+                    double lr, double weight_decay, double beta1, double beta2,
+                    double eps, float* step, int zero_grad, void* stream);
 
 /* ---- VAE-U-Net (unet/unet_resnet.py) ----------------------------------- */
 /* ResNet34 stem max-pool 3x3/s2/p1 (timm resnet34, unet_resnet.py:131):

@@ -115,6 +115,7 @@ V4_CASES = [
     (2, [128], 32, 32, 128),
     (1, [64], 32, 64, 64),           # 1024x64 block tile (32x32 pixels)
     (1, [96, 32], 32, 32, 64),
+    (1, [128, 64], 32, 32, 192),    # 1024x64 tiles, three column tiles (padded-concat widths)
 ]
 
 

@@ -93,6 +93,7 @@ _SIGS = {
     "vu_reduce_workspace_bytes": (_l, [_l, _i]),
     "vu_chan_sum": (_i, [_p, _l, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
     "vu_copy": (_i, [_p, _l, _i, _p, _l, _i, _l, _i, _i, _p]),
+    "vu_zero": (_i, [_p, _l, _l, _i, _i, _p]),
     "vu_input_pack": (_i, [_p, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),
     "vu_maxpool2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _p]),
     "vu_maxpool2_bwd": (_i, [_p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _p, _l, _i, _p]),
@@ -119,6 +120,8 @@ _SIGS = {
     "vu_mt_grad_norm": (_i, [_p, _i, _l, _f, _p, _p, _p, _p]),
     "vu_mt_scale_grads": (_i, [_p, _i, _l, _p, _p]),
     "vu_mt_adamw": (_i, [_p, _i, _l, _f, _f, _f, _f, _f, _p, _p]),
+    "vu_mt_adamw_dev": (_i, [_p, _i, _l, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, _p, _i,
+                             _p]),
     "vu_maxpool3s2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _p, _i, _p]),
     "vu_maxpool3s2_bwd": (_i, [_p, _l, _p, _i, _i, _i, _i, _p, _l, _i, _i, _p]),
     "vu_bn_add_relu": (_i, [_p, _l, _p, _p, _p, _l, _p, _p, _l, _i, _p, _l, _i, _p]),

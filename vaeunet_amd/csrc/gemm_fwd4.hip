@@ -507,6 +507,9 @@ int pick_bn(const VuGemmFwd& p) {
   if (p.ncol % 256 != 0 && tiles_ok<128>(p) && (pix / 512) * (p.ncol / 128) >= mb) return 128;
   // 64 x 64 problems (18 K steps) are prologue/epilogue bound at 1 block/CU: v3 wins
   if (p.ncol == 64 && (g.C > 64 || mb < 256) && tiles_ok<64>(p) && pix / 1024 >= mb) return 64;
+  // column counts that are 64- but not 128-multiples (padded decoder concats:
+  // 704, 832): 1024 x 64 tiles, several column tiles per pixel tile
+  if (p.ncol % 128 != 0 && p.ncol > 64 && tiles_ok<64>(p) && (pix / 1024) * (p.ncol / 64) >= mb) return 64;
   return 0;
 }
 

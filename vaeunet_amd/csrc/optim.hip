@@ -105,7 +105,56 @@ __global__ void mt_adamw_kernel(const VuMtEntry* t, int n, float decay, float w1
   }
 }
 
+// Capturable AdamW (one HIP graph replays the whole training step): the step
+// count lives on the device, the bias corrections are derived from it in
+// double exactly as the host path computes them (1 - beta^step, lr / bc1,
+// sqrt(bc2)) and rounded to float once; all tensors share the group's step.
+// zero_grad: the gradient is cleared after use, so the next backward can
+// accumulate into persistent .grad buffers (graph replays need fixed
+// addresses).
+__global__ void mt_step_incr_kernel(float* step) { *step += 1.f; }
+
+__global__ void mt_adamw_dev_kernel(const VuMtEntry* t, int n, float decay, float w1, float beta2, float w2,
+                                    float eps, double lr, double beta1d, double beta2d, const float* step,
+                                    int zero_grad) {
+  const int64_t chunk = blockIdx.x;
+  const int k = find_tensor(t, n, chunk);
+  const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
+  const int64_t end = min(t[k].numel, off + MT_CHUNK);
+  float* p = reinterpret_cast<float*>(t[k].param);
+  float* g = reinterpret_cast<float*>(t[k].grad);
+  float* m = reinterpret_cast<float*>(t[k].exp_avg);
+  float* v = reinterpret_cast<float*>(t[k].exp_avg_sq);
+  const double sc = (double)*step;
+  const float step_size = (float)(lr / (1.0 - pow(beta1d, sc)));
+  const float bc2s = (float)sqrt(1.0 - pow(beta2d, sc));
+  for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
+    const float gi = g[i];
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = mi + w1 * (gi - mi);
+    float vi = v[i] * beta2;
+    vi = vi + w2 * gi * gi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    pi = pi + (-step_size) * (mi / denom);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+    if (zero_grad) g[i] = 0.f;
+  }
+}
+
 }  // namespace
+
+extern "C" int vu_mt_adamw_dev(const VuMtEntry* table, int ntensors, int64_t nchunks, double lr,
+                               double weight_decay, double beta1, double beta2, double eps, float* step,
+                               int zero_grad, void* stream) {
+  if (ntensors <= 0 || nchunks <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(mt_step_incr_kernel, dim3(1), dim3(1), 0, st, step);
+  hipLaunchKernelGGL(mt_adamw_dev_kernel, dim3((unsigned)nchunks), dim3(MT_THREADS), 0, st, table, ntensors,
+                     (float)(1.0 - lr * weight_decay), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
+                     (float)eps, lr, beta1, beta2, step, zero_grad);
+  return (int)hipGetLastError();
+}
 
 extern "C" int64_t vu_mt_chunk_elems() { return MT_CHUNK; }
 

@@ -468,6 +468,30 @@ extern "C" int vu_permute4_batch(const VuPermJob* jobs, int njobs, int64_t nchun
   return (int)hipGetLastError();
 }
 
+namespace {
+__global__ void zero_kernel(char* y, int64_t ys_bytes, int64_t P, int row_bytes) {
+  // 4-byte words of each pixel's channel run (row_bytes % 4 == 0)
+  const int wpr = row_bytes >> 2;
+  const int64_t tot = P * wpr;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = e / wpr;
+    reinterpret_cast<uint32_t*>(y + p * ys_bytes)[e - p * wpr] = 0u;
+  }
+}
+}  // namespace
+
+// y[p][0..C) = 0 for P pixels at pixel stride ys (a channel slice of an NHWC
+// tensor: the zero channels a 64-aligned concat source is padded with)
+extern "C" int vu_zero(void* y, int64_t ys, int64_t P, int C, int dtype, void* stream) {
+  const int eb = dtype == VU_BF16 ? 2 : 4;
+  if ((C * eb) % 4 != 0) return (int)hipErrorInvalidValue;
+  const int64_t tot = P * (C * eb / 4);
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(zero_kernel, dim3(ew_grid(tot)), dim3(256), 0, (hipStream_t)stream, (char*)y, ys * eb, P,
+                     C * eb);
+  return (int)hipGetLastError();
+}
+
 extern "C" int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys, int ydtype, int64_t P, int C,
                        int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;

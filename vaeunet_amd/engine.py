@@ -80,10 +80,51 @@ def _cached(p, key, build):
     return ent[1]
 
 
+class StaticRefresh:
+    """Every derived weight image of ``params`` rebuilt IN PLACE by one
+    prebuilt vu_permute4_batch launch (no allocation, no host upload): what a
+    captured HIP graph of the training step replays at its start.  Built
+    after a warm-up step, when every image the step uses exists."""
+
+    def __init__(self, params):
+        self.entries = []
+        with K.record_permutes() as rec:
+            for p in params:
+                builders = p.__dict__.get("_vu_build")
+                if not builders:
+                    continue
+                cache = p.__dict__["_vu_cache"]
+                for key, build in builders.items():
+                    n0 = len(rec.jobs)
+                    build()
+                    if len(rec.jobs) != n0 + 1:
+                        raise RuntimeError("StaticRefresh: an image build must be one permute")
+                    src, base, strides, dims, d3v, out, dtype = rec.jobs[n0]
+                    img = cache[key][1]
+                    if img.numel() < out.numel() or not img.is_contiguous():
+                        raise RuntimeError("StaticRefresh: cached image layout changed")
+                    rec.jobs[n0] = (src, base, strides, dims, d3v, img.view(-1)[:out.numel()], dtype)
+                    self.entries.append((p, cache, key))
+        self.jobs = rec.jobs
+        self.table, self.nchunks = K.job_table(self.jobs) if self.jobs else (None, 0)
+
+    def launch(self):
+        if self.jobs:
+            K.call("vu_permute4_batch", K.ptr(self.table), len(self.jobs), self.nchunks, K.stream())
+        for p, cache, key in self.entries:
+            cache[key] = ((p._version, p.data_ptr()), cache[key][1])
+
+
+_STATIC_REFRESH = None  # a StaticRefresh while a graph of the step is captured
+
+
 def refresh_weights(params):
     """Rebuild every stale derived weight image of ``params`` (those built in
     earlier steps, i.e. after an optimizer step bumped the version) in ONE
     batched launch, instead of one permute launch per image mid-step."""
+    if _STATIC_REFRESH is not None:
+        _STATIC_REFRESH.launch()
+        return
     stale = []
     for p in params:
         builders = p.__dict__.get("_vu_build")
@@ -112,15 +153,30 @@ def w3x3_fwd(w, d, cin_pad=None):
     return _cached(w, ("w3f", d, cp), build)
 
 
-def w3x3_dgrad(w, d):
-    """Input-gradient weights: B[ci][(r'*S+s')*Cout + co] = W[co][ci][R-1-r'][S-1-s']."""
+def w3x3_dgrad(w, d, rows_pad=None):
+    """Input-gradient weights: B[ci][(r'*S+s')*Cout + co] = W[co][ci][R-1-r'][S-1-s'].
+    rows_pad > Cin: zero rows for the padded input channels of a 64-aligned
+    concat (a persistent zero-initialised image whose first Cin rows are
+    rebuilt each step)."""
     co, ci, R, S = w.shape
+    rp = rows_pad or ci
 
     def build():
         s = w.stride()
         base = (R - 1) * s[2] + (S - 1) * s[3]
+        out = None
+        if rp > ci:
+            bufs = w.__dict__.setdefault("_vu_pad", {})
+            key = ("w3d", d, rp)
+            if key not in bufs:
+                bufs[key] = torch.zeros((rp, R * S * co), device=w.device,
+                                        dtype=torch.bfloat16 if d == BF16 else torch.float32)
+            out = bufs[key]
+            K.permute4(w.detach(), base, (s[1], -s[2], -s[3], s[0]), (ci, R, S, co), co, d,
+                       out=out[:ci].view(ci, R, S, co))
+            return out
         return K.permute4(w.detach(), base, (s[1], -s[2], -s[3], s[0]), (ci, R, S, co), co, d).view(ci, -1)
-    return _cached(w, ("w3d", d), build)
+    return _cached(w, ("w3d", d, rp), build)
 
 
 def w1x1_fwd(w, d):
@@ -261,7 +317,11 @@ def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None):
     return a, (y, coef)
 
 
-def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False):
+def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False,
+                     cin_pad=None):
+    """cin_pad: compute the input gradient for cin_pad channels (zero weight
+    rows past conv.in_channels) so that its column count stays a tile
+    multiple; the caller reads the real channels only."""
     y, coef = saved
     dy = bn_bwd(da, y, coef, bn, True, M)
     wgrad3x3(dy, srcs, conv.weight, M, cvalid)
@@ -271,10 +331,10 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     N, _, H, W = y.shape
     # a channel-padded input (the 3-channel image) gets a gradient for its
     # real channels only: the dgrad weights have conv.in_channels rows
-    cin = conv.in_channels
+    cin = cin_pad or conv.in_channels
     if dsrc is None:
         dsrc = M.act(N, cin, H, W)
-    K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d), cin, dsrc, M.d, accumulate=dsrc_acc,
+    K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d, cin), cin, dsrc, M.d, accumulate=dsrc_acc,
                kind="dgrad")
     return dsrc
 

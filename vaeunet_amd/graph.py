@@ -1,0 +1,115 @@
+"""Whole training step as one HIP graph (launch reduction).
+
+The reference's step (train.py:381-411) is ~300 (U-Net) to ~600 (VAE-U-Net)
+kernel launches; issued from Python each one costs tens of microseconds of
+host time, which for the VAE-U-Net exceeds the GPU time of the step.
+``GraphedTrainStep`` captures forward + loss + backward + clip_grad_norm_ +
+AdamW once (``torch.cuda.CUDAGraph`` over HIP graphs) and replays it:
+
+* static inputs: the caller's ``forward_backward`` closure reads fixed
+  tensors (copy each new batch into them before ``step()``);
+* persistent ``.grad`` buffers: zero-initialised before capture, the
+  backward accumulates into them and the capturable AdamW kernel
+  (``vu_mt_adamw_dev``) clears them after use, so every replay sees zeros;
+* the step count lives on the device (one per parameter group) and the
+  AdamW bias corrections are derived from it in the kernel (same double
+  arithmetic as the eager path);
+* the derived bf16 weight images are rebuilt in place by one prebuilt
+  permute launch at the start of each replay (``engine.StaticRefresh``);
+* the multi-tensor tables of the clip and AdamW launches are uploaded once,
+  before capture.
+
+The learning rate, betas, eps, weight decay and max_norm are frozen at
+capture (rebuild the object to change them).  Single process: the data-
+parallel reducer's collectives are not captured (``bench.py`` replays only
+at world size 1).
+"""
+import torch
+
+from . import _lib
+from . import engine as E
+from .optim import FusedAdamW, _Table, clip_grad_norm_
+
+
+class GraphedTrainStep:
+    """forward_backward(): runs the forward, the loss and ``loss.backward()``
+    on static inputs and returns the loss tensor."""
+
+    def __init__(self, forward_backward, optimizer, max_norm=None, warmup=2):
+        if not isinstance(optimizer, FusedAdamW):
+            raise TypeError("GraphedTrainStep needs vaeunet_amd.optim.FusedAdamW")
+        self.fb = forward_backward
+        self.opt = optimizer
+        self.max_norm = max_norm
+        params = [p for g in optimizer.param_groups for p in g["params"] if p.requires_grad]
+        self.params = params
+        # eager warm-up: builds the weight images, optimizer state and every
+        # workspace the step touches
+        for _ in range(max(1, warmup)):
+            self.fb()
+            if max_norm is not None:
+                clip_grad_norm_(params, max_norm)
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
+        dev = params[0].device
+        # persistent zero gradients (the backward accumulates into them)
+        for p in params:
+            p.grad = torch.zeros_like(p)
+        self.clip_tab = _Table([(p.grad, p.grad, None, None, 0.0, 1.0) for p in params], dev)
+        self.norm = torch.empty(2, dtype=torch.float32, device=dev)
+        self.ws = torch.empty(max(1, self.clip_tab.nchunks), dtype=torch.float64, device=dev)
+        self.groups = []
+        for group in optimizer.param_groups:
+            rows, step0 = [], 0.0
+            for p in group["params"]:
+                if not p.requires_grad:
+                    continue
+                st = optimizer.state[p]
+                rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], 0.0, 1.0))
+                step0 = float(st["step"])
+            if rows:
+                step = torch.full((1,), step0, dtype=torch.float32, device=dev)
+                self.groups.append((group, _Table(rows, dev), step))
+        # images, then capture
+        self.refresh = E.StaticRefresh(params)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        E._STATIC_REFRESH = self.refresh
+        try:
+            with torch.cuda.graph(self.graph):
+                self.loss = self.fb()
+                self._tail()
+        finally:
+            E._STATIC_REFRESH = None
+        torch.cuda.synchronize()
+
+    def _tail(self):
+        s = _lib.stream()
+        if self.max_norm is not None:
+            t = self.clip_tab
+            _lib.call("vu_mt_grad_norm", t.ptr(), t.n, t.nchunks, float(self.max_norm), _lib.ptr(self.norm[0:1]),
+                      _lib.ptr(self.norm[1:2]), _lib.ptr(self.ws), s)
+            _lib.call("vu_mt_scale_grads", t.ptr(), t.n, t.nchunks, _lib.ptr(self.norm[1:2]), s)
+        for group, t, step in self.groups:
+            b1, b2 = group["betas"]
+            _lib.call("vu_mt_adamw_dev", t.ptr(), t.n, t.nchunks, float(group["lr"]), float(group["weight_decay"]),
+                      float(b1), float(b2), float(group["eps"]), _lib.ptr(step), 1, s)
+
+    def step(self):
+        """Replay one training step; returns the (static) loss tensor."""
+        self.graph.replay()
+        return self.loss
+
+    @property
+    def grad_norm(self):
+        """Total gradient norm of the last replay (device tensor)."""
+        return self.norm[0]
+
+    def sync_optimizer_state(self):
+        """Write the device step counts back into the optimizer's state (for
+        checkpoints: train.py:542-565 saves optimizer.state_dict())."""
+        for group, _, step in self.groups:
+            v = float(step.item())
+            for p in group["params"]:
+                if p.requires_grad:
+                    self.opt.state[p]["step"] = torch.tensor(v, dtype=torch.float32)

@@ -240,11 +240,13 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
 _PBATCH = None  # job list while a permute_batch() context is open
 
 
-def permute4(src, base, strides, dims, d3v, dtype):
+def permute4(src, base, strides, dims, d3v, dtype, out=None):
     """out[i0][i1][i2][i3] = src[base + sum i*s] (0 for i3 >= d3v), in the
-    storage dtype.  Inside permute_batch() the launch is deferred and merged."""
-    out = torch.empty(dims, dtype=torch.bfloat16 if dtype == _lib.BF16 else torch.float32,
-                      device=src.device)
+    storage dtype (``out``: a contiguous destination, else a new tensor).
+    Inside permute_batch() the launch is deferred and merged."""
+    if out is None:
+        out = torch.empty(dims, dtype=torch.bfloat16 if dtype == _lib.BF16 else torch.float32,
+                          device=src.device)
     if _PBATCH is not None:
         _PBATCH.append((src, base, strides, dims, d3v, out, dtype))
         return out
@@ -271,34 +273,56 @@ class permute_batch:
         jobs, _PBATCH = _PBATCH, None
         if not jobs or exc[0] is not None:
             return False
-        chunk = query("vu_permute4_chunk")
-        arr = (_lib.VuPermJob * len(jobs))()
-        c0 = 0
-        for i, (src, base, strides, dims, d3v, out, dtype) in enumerate(jobs):
-            e = arr[i]
-            e.inp = src.data_ptr()
-            e.base = base
-            e.s0, e.s1, e.s2, e.s3 = strides
-            e.d0, e.d1, e.d2, e.d3 = dims
-            e.d3v, e.dtype = d3v, dtype
-            e.out = out.data_ptr()
-            e.chunk0 = c0
-            # input-fastest dim (among those of extent > 1); a transpose if not dim 3
-            cand = [k for k in range(4) if dims[k] > 1] or [3]
-            q = min(cand, key=lambda k: (abs(strides[k]), k != cand[-1]))
-            if q == cand[-1] or dims[3] == 1:
-                q = 3  # output-fast == input-fast: stream
-            e.q = q
-            if q == 3:
-                c0 += -(-out.numel() // chunk)
-            else:
-                a, cc = [k for k in range(3) if k != q]
-                c0 += dims[a] * dims[cc] * (-(-dims[q] // 32)) * (-(-dims[3] // 32))
-        dev = jobs[0][5].device
-        host = torch.frombuffer(bytearray(arr), dtype=torch.uint8).pin_memory()
-        table = host.to(dev, non_blocking=True)
+        table, c0 = job_table(jobs)
         call("vu_permute4_batch", ptr(table), len(jobs), c0, stream())
         return False
+
+
+class record_permutes:
+    """Context collecting the permute4 jobs issued inside WITHOUT launching
+    them (``.jobs``: (src, base, strides, dims, d3v, out, dtype) tuples)."""
+
+    def __enter__(self):
+        global _PBATCH
+        if _PBATCH is not None:
+            raise RuntimeError("record_permutes inside an open permute_batch")
+        _PBATCH = self.jobs = []
+        return self
+
+    def __exit__(self, *exc):
+        global _PBATCH
+        _PBATCH = None
+        return False
+
+
+def job_table(jobs):
+    """Device VuPermJob table of permute4 jobs -> (table tensor, total blocks)."""
+    chunk = query("vu_permute4_chunk")
+    arr = (_lib.VuPermJob * len(jobs))()
+    c0 = 0
+    for i, (src, base, strides, dims, d3v, out, dtype) in enumerate(jobs):
+        e = arr[i]
+        e.inp = src.data_ptr()
+        e.base = base
+        e.s0, e.s1, e.s2, e.s3 = strides
+        e.d0, e.d1, e.d2, e.d3 = dims
+        e.d3v, e.dtype = d3v, dtype
+        e.out = out.data_ptr()
+        e.chunk0 = c0
+        # input-fastest dim (among those of extent > 1); a transpose if not dim 3
+        cand = [k for k in range(4) if dims[k] > 1] or [3]
+        q = min(cand, key=lambda k: (abs(strides[k]), k != cand[-1]))
+        if q == cand[-1] or dims[3] == 1:
+            q = 3  # output-fast == input-fast: stream
+        e.q = q
+        if q == 3:
+            c0 += -(-out.numel() // chunk)
+        else:
+            a, cc = [k for k in range(3) if k != q]
+            c0 += dims[a] * dims[cc] * (-(-dims[q] // 32)) * (-(-dims[3] // 32))
+    dev = jobs[0][5].device
+    host = torch.frombuffer(bytearray(arr), dtype=torch.uint8).pin_memory()
+    return host.to(dev, non_blocking=True), c0
 
 
 def bn_finalize(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps):
@@ -353,6 +377,12 @@ def chan_sum(x, out, acc, dtype, window=None):
                      dtype=torch.float32, device=x.device)
     call("vu_chan_sum", ptr(x), pstride(x), N, H, W, y0, x0, Hr, Wr, Cc, ptr(out),
          1 if acc else 0, ptr(ws), dtype, stream())
+
+
+def zero(y):
+    """Zero an NHWC tensor or channel slice (HIP fill, no ATen launch)."""
+    N, Cc, H, W = y.shape
+    call("vu_zero", ptr(y), pstride(y), N * H * W, Cc, dcode(y.dtype), stream())
 
 
 def copy(x, y, accumulate=False):

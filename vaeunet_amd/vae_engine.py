@@ -219,11 +219,11 @@ def latent_map(M, z, N, H, W):
     return zb
 
 
-def cbr1x1_fwd(M, seq, x):
+def cbr1x1_fwd(M, seq, x, out=None):
     conv, bn = seq[0], seq[1]
     y, st = conv_fwd(M, [x], conv, bn.training)
     c = E.bn_coef(bn, st, y.shape[1])
-    a = torch.empty_like(y)
+    a = torch.empty_like(y) if out is None else out
     K.bn_apply(y, a, c, True, M.d)
     return a, (x, y, c)
 
@@ -269,6 +269,7 @@ def decoder_fwd(M, blk, x, skip, z):
             sk = skip
         srcs.append(sk)
     szp = None
+    cpad = None
     if blk.use_latent:
         if z.dim() == 2:
             # interpolate([B, L, 1, 1] -> (H, W), align_corners) is a broadcast
@@ -277,19 +278,33 @@ def decoder_fwd(M, blk, x, skip, z):
             # a spatial z [B, L, h, w] (the reference's z_spatial, unet_resnet.py:93)
             zb = M.act(N, z.shape[1], H, W)
             K.upsample_fwd(z, zb, H, W, 0, 0, M.d)
-        zp, szp = cbr1x1_fwd(M, blk.z_proj, zb)
+        L = blk.z_proj[0].out_channels
+        lead = sum(t.shape[1] for t in srcs)
+        Lp = -(-L // 64) * 64
+        if lead % 64 == 0 and Lp != L:
+            # pad the z_proj source to 64 channels (zeros): every concat group
+            # is then 64-aligned, so conv1's weight gradient runs on the halo
+            # kernel and its input gradient keeps a tile-multiple column count
+            zp = M.act(N, Lp, H, W)
+            K.zero(zp[:, L:])
+            _, szp = cbr1x1_fwd(M, blk.z_proj, zb, out=zp[:, :L])
+            cpad = lead + Lp
+        else:
+            zp, szp = cbr1x1_fwd(M, blk.z_proj, zb)
         srcs.append(zp)
-    a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1])
+    a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1], cin_pad=cpad)
     a2, s2 = E.conv_bn_relu_fwd(M, [a1], blk.conv2[0], blk.conv2[1])
-    return a2, (x, skip, xu, srcs, satt, szp, a1, s1, s2)
+    return a2, (x, skip, xu, srcs, satt, szp, a1, s1, s2, cpad)
 
 
 def decoder_bwd(M, blk, saved, dout, z=None):
     """-> (dx, dskip or None, dz or None): dz is [B, L] fp32 for a vector z,
     an NHWC map like ``z`` for a spatial one."""
-    x, skip, xu, srcs, satt, szp, a1, s1, s2 = saved
+    x, skip, xu, srcs, satt, szp, a1, s1, s2, cpad = saved
     da1 = E.conv_bn_relu_bwd(M, [a1], blk.conv2[0], blk.conv2[1], s2, dout, True)
-    dsrc = E.conv_bn_relu_bwd(M, srcs, blk.conv1[0], blk.conv1[1], s1, da1, True)
+    conv1 = blk.conv1[0]
+    dsrc = E.conv_bn_relu_bwd(M, srcs, conv1, blk.conv1[1], s1, da1, True,
+                              cvalid=conv1.in_channels if cpad else None, cin_pad=cpad)
     cx = xu.shape[1]
     off = cx
     dskip = dz = None
@@ -302,7 +317,7 @@ def decoder_bwd(M, blk, saved, dout, z=None):
             dskip = dsk
         off += cs
     if blk.use_latent:
-        dzp = dsrc[:, off:]
+        dzp = dsrc[:, off:off + blk.z_proj[0].out_channels]
         dzb = cbr1x1_bwd(M, blk.z_proj, szp, dzp)
         if z is not None and z.dim() == 4:
             dz = torch.empty_like(z)
