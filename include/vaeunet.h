@@ -112,11 +112,17 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     0 = CU count; tests use small caps so that every block walks several
  *     tiles);
  *   VU_TUNE_STREAM: 1 (default) lets the short-K 1x1 stream kernel
- *     (gemm_stream.hip) serve the problems it takes, 0 routes them to v2. */
+ *     (gemm_stream.hip) serve the problems it takes, 0 routes them to v2;
+ *   VU_TUNE_V4_SPLIT_CHUNKS: fewest 32-channel chunks per automatic split-K
+ *     slice (default 2);
+ *   VU_TUNE_V2_SMALL: 1 (default) serves small grids (too few 256-row
+ *     tiles) with 128x64 4-wave v2 tiles instead of split-K / v3. */
 #define VU_TUNE_V4_MIN_BLOCKS 0
 #define VU_TUNE_FP8_GRID 4
 #define VU_TUNE_STREAM 5
 #define VU_TUNE_V4_SPLITK 6
+#define VU_TUNE_V4_SPLIT_CHUNKS 8
+#define VU_TUNE_V2_SMALL 9
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */
@@ -405,7 +411,10 @@ int vu_relu_mask(const void* dout, int64_t ds, const void* out, int64_t os,
 /* out[n][c] (+)= scale * sum over the HW pixels of sample n (avg-pool head,
  * latent-broadcast backward) */
 int vu_sample_sum(const void* x, int64_t xs, int N, int HW, int C, float scale,
-                  float* out, int accumulate, int dtype, void* stream);
+                  float* out, int accumulate, float* workspace, int dtype,
+                  void* stream);
+/* workspace bytes of vu_sample_sum (per-split partial sums) */
+int64_t vu_sample_sum_workspace_bytes(int N, int C);
 /* y[n,p,c] (+)= scale * v[n][c]: interpolate(z[...,None,None], align_corners)
  * as an exact broadcast (unet_resnet.py:217-221, 93) */
 int vu_sample_broadcast(const float* v, int N, int HW, int C, float scale,

@@ -202,6 +202,21 @@ def test_conv3x3_pingpong_splitk(case):
         _tune(*TUNE_DEFAULTS)
 
 
+SMALL_GRID_CASES = [
+    # (N, [cin], H, W, cout): ResNet34 encoder levels on the 128x64 v2 tiles
+    (8, [512], 16, 16, 512),   # 16^2 (too narrow for the halo kernels): 4-way split-K
+    (8, [256], 32, 32, 256),   # 2-way split-K
+    (8, [128], 64, 64, 128),   # no split
+]
+
+
+@pytest.mark.parametrize("case", SMALL_GRID_CASES)
+def test_conv3x3_small_grid_v2(case):
+    """small grids (gemm_fwd2.hip small-grid mode + split-K finish): bias,
+    BN partials per 128 rows, accumulate, input gradient."""
+    _check_halo_conv(case, (128,))
+
+
 def test_conv3x3_splitk_auto_32x32_level():
     """the production dispatch of a down4-like layer (512 -> 1024 at 32x32):
     16..255 256x256 tiles -> automatic split-K (default tuning)."""

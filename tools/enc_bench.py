@@ -1,0 +1,68 @@
+"""Per-layer timing of the ResNet34 encoder's 3x3 convolutions (UNetResNet,
+B=8, 3x512^2 input) through the C-ABI: forward and input gradient.
+
+usage: python tools/enc_bench.py [--tune KEY=VAL,...]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vaeunet_amd import kernels as K  # noqa: E402
+from vaeunet_amd import _lib  # noqa: E402
+from vaeunet_amd.engine import w3x3_fwd, w3x3_dgrad  # noqa: E402
+
+B = 8
+LAYERS = [("layer1", 64, 64, 128), ("layer2", 128, 128, 64), ("layer3", 256, 256, 32), ("layer4", 512, 512, 16)]
+
+
+def timeit(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tune", default="")
+    args = ap.parse_args()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(k), int(v))
+    dev = torch.device("cuda")
+    d = _lib.BF16
+    tot = 0.0
+    for name, ci, co, S in LAYERS:
+        x = K.empty_act(B, ci, S, S, torch.bfloat16, dev).normal_()
+        w = torch.randn(co, ci, 3, 3, device=dev) / (3 * ci ** 0.5)
+        y = K.empty_act(B, co, S, S, torch.bfloat16, dev)
+        fl = 2.0 * B * S * S * co * ci * 9
+        import ctypes as C
+        a = _lib.VuGemmFwd()
+        a.a = K.gather3x3([x])
+        a.b = w3x3_fwd(w, d).data_ptr()
+        a.ldb = 9 * ci
+        a.ncol = co
+        a.out = y.data_ptr()
+        a.out_stride = K.pstride(y)
+        a.out_mode = 0
+        diag = (K.query("vu_gemm_fwd_row_tile", C.byref(a), d), K.query("vu_gemm_fwd_workspace_bytes", C.byref(a), d))
+        tf = timeit(lambda: K.gemm_fwd(K.gather3x3([x]), w3x3_fwd(w, d), co, y, d, stats=True))
+        dx = K.empty_act(B, ci, S, S, torch.bfloat16, dev)
+        tb = timeit(lambda: K.gemm_fwd(K.gather3x3([y]), w3x3_dgrad(w, d), ci, dx, d, kind="dgrad"))
+        tot += tf + tb
+        print(f"{name} {ci}->{co} @{S:3d} | fwd {tf * 1e3:7.1f}us {fl / tf / 1e9:6.0f}TF | "
+              f"dgrad {tb * 1e3:7.1f}us {fl / tb / 1e9:6.0f}TF | row_tile,ws {diag}")
+    print(f"TOTAL {tot:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

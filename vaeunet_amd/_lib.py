@@ -126,7 +126,8 @@ _SIGS = {
     "vu_maxpool3s2_bwd": (_i, [_p, _l, _p, _i, _i, _i, _i, _p, _l, _i, _i, _p]),
     "vu_bn_add_relu": (_i, [_p, _l, _p, _p, _p, _l, _p, _p, _l, _i, _p, _l, _i, _p]),
     "vu_relu_mask": (_i, [_p, _l, _p, _l, _l, _i, _p, _l, _i, _p]),
-    "vu_sample_sum": (_i, [_p, _l, _i, _i, _i, _f, _p, _i, _i, _p]),
+    "vu_sample_sum": (_i, [_p, _l, _i, _i, _i, _f, _p, _i, _p, _i, _p]),
+    "vu_sample_sum_workspace_bytes": (_l, [_i, _i]),
     "vu_sample_broadcast": (_i, [_p, _i, _i, _i, _f, _p, _l, _i, _i, _p]),
     "vu_linear_small_fwd": (_i, [_p, _i, _i, _p, _p, _i, _p, _p]),
     "vu_linear_small_bwd": (_i, [_p, _i, _i, _p, _i, _p, _p, _i, _p, _p, _i, _p]),

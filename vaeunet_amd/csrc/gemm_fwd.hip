@@ -323,6 +323,9 @@ int dispatch_fwd(const VuGemmFwd& p, hipStream_t st) {
 // large-tile LDS-DMA variant (gemm_fwd2.hip)
 int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v2_small_launch(const VuGemmFwd& p, hipStream_t st);
+int64_t gemm_fwd_v2_small_workspace(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype);
@@ -371,6 +374,7 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
     int bm = gemm_fwd_v4_bm(*args, dtype);
     if (bm) return bm;
   }
+  if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return 128;
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 256;
   if (use_v2(dtype)) {
     int bm = gemm_fwd_v2_bm(*args, dtype);
@@ -381,7 +385,9 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
 
 extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype) && (conv_image_bm(*args, dtype) || gemm_stream_bm(*args, dtype))) return 0;
-  return use_v4(dtype) ? gemm_fwd_v4_workspace(*args, dtype) : 0;
+  if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_workspace(*args, dtype);
+  if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_workspace(*args, dtype);
+  return 0;
 }
 
 extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
@@ -395,6 +401,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return conv_image_launch(*args, st);
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
+  if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);

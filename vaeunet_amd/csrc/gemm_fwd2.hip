@@ -35,7 +35,7 @@ VU_DEV int swz(int row, int chunk) { return row * KB + ((chunk ^ (row & 7)) << 4
 
 struct Pix { int n, h, w; bool ok; };
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, bool SPLIT = false>
 __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd p) {
   constexpr int NT = WM * WN * 64;
   constexpr int EPC = 8;                  // bf16 per 16-byte chunk
@@ -58,7 +58,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
   const int K = g.R * g.S * g.C;
   const int mtiles = (int)((M + BM - 1) / BM);
   const int ntiles = (p.ncol + BN - 1) / BN;
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  // SPLIT: the block index also picks a contiguous range of K steps (kidx)
+  const int ksplit = SPLIT ? p.ksplit : 1;
+  const int bid0 = xcd_remap(blockIdx.x, mtiles * ntiles * ksplit);
+  const int kidx = SPLIT ? bid0 / (mtiles * ntiles) : 0;
+  const int bid = SPLIT ? bid0 - kidx * (mtiles * ntiles) : bid0;
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int64_t m0 = (int64_t)mt * BM;
   const int n0 = nt * BN;
@@ -126,22 +130,24 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 
-  const int nk = (K + BKE - 1) / BKE;
+  const int nkt = (K + BKE - 1) / BKE;
+  const int kb = SPLIT ? kidx * nkt / ksplit : 0;
+  const int nk = (SPLIT ? (kidx + 1) * nkt / ksplit : nkt) - kb;
   // Pipeline: stage kt+2 is issued right after the barrier of step kt, into
   // the ring slot step kt-1 just finished reading.  Each thread's own DMA is
   // retired by a COUNTED vmcnt (the NL loads of the newest stage may stay in
   // flight), then the raw s_barrier makes every thread's landed bytes
   // visible; no __syncthreads() (it would drain vmcnt to 0) in the loop.
   constexpr int NL = LA + LB;
-  stage(0, 0);
-  if (NSTAGE >= 3 && nk > 1) stage(1, 1);
+  stage(kb, 0);
+  if (NSTAGE >= 3 && nk > 1) stage(kb + 1, 1);
   for (int kt = 0; kt < nk; ++kt) {
     if (NSTAGE >= 3 && kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (NSTAGE >= 3 && kt + 2 < nk) stage(kt + 2, (kt + 2) % NSTAGE);
-    else if (NSTAGE == 2 && kt + 1 < nk) stage(kt + 1, (kt + 1) % NSTAGE);
+    if (NSTAGE >= 3 && kt + 2 < nk) stage(kb + kt + 2, (kt + 2) % NSTAGE);
+    else if (NSTAGE == 2 && kt + 1 < nk) stage(kb + kt + 1, (kt + 1) % NSTAGE);
     const int cur = kt % NSTAGE;
     const char* A = smem + cur * STAGE;
     const char* B = A + BM * KB;
@@ -168,6 +174,22 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
                                                               __builtin_bit_cast(bf16x8, bf[kk][j]), acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
+  }
+  if (SPLIT) {
+    // raw fp32 partial tile -> slab kidx (rows m0 + ..., all valid: M % BM == 0)
+    float* slab = p.workspace + (int64_t)kidx * M * p.ncol;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm * (BM / WM) + i * 16 + 4 * (lane >> 4) + r;
+          slab[row * p.ncol + col] = acc[i][j][r];
+        }
+      }
+    return;
   }
   __syncthreads();  // every wave is done with the ring before the epilogue reuses it
 
@@ -312,6 +334,58 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
   int64_t tiles = ((M + 255) / 256) * ((p.ncol + bn - 1) / bn);
   if (tiles < 256) return 0;
   return v2_cfg(p) ? 128 : 256;
+}
+
+// Small grids (the ResNet34 encoder's 64^2 / 32^2 / 16^2 levels: too few
+// 256-row tiles to fill the chip, 16^2 images too narrow for the 3x3 halo
+// kernels' 32-pixel rows): 128 x 64 tiles of 4 waves, two blocks per CU,
+// split-K to >= 2 blocks per CU when the tiles alone do not reach it (fp32
+// slabs + the deterministic finish of gemm_fwd4.hip).  Returns the split
+// (>= 1) when served, else 0.
+bool g_small = true;  // VU_TUNE_V2_SMALL
+
+int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype) {
+  if (!g_small || dtype != VU_BF16 || p.out_mode != 0) return 0;
+  const VuGather& g = p.a;
+  for (int t = 0; t < g.nsrc; ++t)
+    if (g.stride[t] % 8 != 0 || g.cend[t] % 64 != 0) return 0;
+  if (p.ncol % 64 != 0 || p.ldb % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0) return 0;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  if (M % 128 != 0) return 0;
+  const int64_t big = ((M + 255) / 256) * ((p.ncol + 127) / 128);
+  const int64_t tiles = (M / 128) * (p.ncol / 64);
+  const int nk = (g.R * g.S * g.C + 63) / 64;
+  if (big >= 256 || tiles < 64 || nk < 8) return 0;
+  int ks = (int)((512 + tiles - 1) / tiles);
+  if (ks > nk / 8) ks = nk / 8;
+  return ks < 1 ? 1 : ks;
+}
+
+int64_t gemm_fwd_v2_small_workspace(const VuGemmFwd& p, int dtype) {
+  const int ks = gemm_fwd_v2_small(p, dtype);
+  return ks > 1 ? (int64_t)ks * p.a.N * p.a.H * p.a.W * p.ncol * (int64_t)sizeof(float) : 0;
+}
+
+int splitk_finish_launch(const VuGemmFwd& p, hipStream_t st);  // gemm_fwd4.hip
+
+int gemm_fwd_v2_small_launch(const VuGemmFwd& p, hipStream_t st) {
+  const int ks = gemm_fwd_v2_small(p, VU_BF16);
+  if (ks <= 1) return launch_ns<128, 64, 2, 2>(p, st);
+  if (!p.workspace) return (int)hipErrorInvalidValue;
+  VuGemmFwd q = p;
+  q.ksplit = ks;
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  const int64_t nblk = (M / 128) * (p.ncol / 64) * ks;
+  hipLaunchKernelGGL((gemm_fwd_v2_kernel<128, 64, 2, 2, 3, true>), dim3((unsigned)nblk), dim3(256), 0, st, q);
+  return splitk_finish_launch(q, st);
+}
+
+int gemm_fwd_v2_tune(int key, int value) {
+  if (key == VU_TUNE_V2_SMALL) {
+    g_small = value != 0;
+    return 0;
+  }
+  return -1;
 }
 
 int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st) {

@@ -517,9 +517,23 @@ struct Plan {
   int bn, ks;
 };
 
-// Tile and K-split.  A grid of 16..255 256x256 tiles gets the smallest split
-// that reaches one block per CU (down4: 128 tiles -> 2, its input gradient:
-// 64 tiles -> 4); at least 2 chunks per split.
+// Tile and K-split.  A grid under one block per CU gets the widest column
+// tile that divides the output and the smallest split that reaches one block
+// per CU (down4: 128 256x256 tiles -> 2, its input gradient: 64 tiles -> 4;
+// the ResNet34 encoder's 64^2 / 32^2 levels: 64 512x128 / 32 256x256 tiles),
+// at least g_split_min_chunks 32-channel chunks per split.
+int g_split_min_chunks = 2;  // vu_gemm_set_tuning(VU_TUNE_V4_SPLIT_CHUNKS, ...)
+
+}  // namespace
+int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype);  // gemm_fwd2.hip
+namespace {
+
+template <int BN>
+int64_t tile_count(const VuGemmFwd& p) {
+  const VuGather& g = p.a;
+  return (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW) * (p.ncol / BN);
+}
+
 Plan plan(const VuGemmFwd& p) {
   const VuGather& g = p.a;
   const int chunks = g.C / 32;
@@ -528,14 +542,27 @@ Plan plan(const VuGemmFwd& p) {
     if (g_splitk >= 2) r.ks = g_splitk < chunks ? g_splitk : chunks;
     return r;
   }
-  if (g_splitk == 0 || !tiles_ok<256>(p) || chunks < 4) return r;
-  const int64_t blocks = ((int64_t)g.N * g.H * g.W / 256) * (p.ncol / 256);
+  const int maxks = chunks / (g_split_min_chunks > 0 ? g_split_min_chunks : 1);
+  if (g_splitk == 0 || maxks < 2) return r;
+  // small grids the 128x64 v2 tiles fill without split-K slabs go there
+  if (g_splitk == 1 && gemm_fwd_v2_small(p, VU_BF16)) return r;
+  int bn = 0;
+  int64_t blocks = 0;
+  if (tiles_ok<256>(p)) {
+    bn = 256;
+    blocks = tile_count<256>(p);
+  } else if (tiles_ok<128>(p)) {
+    bn = 128;
+    blocks = tile_count<128>(p);
+  } else {
+    return r;
+  }
   if (blocks < 16) return r;
   int ks = (int)((g_min_blocks + blocks - 1) / blocks);
   if (g_splitk >= 2) ks = g_splitk;
-  if (ks > chunks / 2) ks = chunks / 2;
+  if (ks > maxks) ks = maxks;
   if (ks < 2) return r;
-  return Plan{256, ks};
+  return Plan{bn, ks};
 }
 
 template <int BN>
@@ -584,6 +611,15 @@ int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype) {
 }
 
 // fp32 split-K slab bytes the ping-pong kernel needs for this problem (0 = none)
+// the deterministic split-K finish over p.ksplit fp32 slabs in p.workspace
+// (also used by the v2 small-grid split, gemm_fwd2.hip)
+int splitk_finish_launch(const VuGemmFwd& p, hipStream_t st) {
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  if (M % 128 != 0 || p.ncol % 64 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(splitk_finish_kernel, dim3((unsigned)((M / 128) * (p.ncol / 64))), dim3(256), 0, st, p);
+  return (int)hipGetLastError();
+}
+
 int64_t gemm_fwd_v4_workspace(const VuGemmFwd& p, int dtype) {
   if (!operands_ok(p, dtype)) return 0;
   const Plan r = plan(p);
@@ -603,6 +639,7 @@ int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st) {
 
 int conv_fp8_tune(int key, int value);     // conv_fp8.hip
 int gemm_stream_tune(int key, int value);  // gemm_stream.hip
+int gemm_fwd_v2_tune(int key, int value);  // gemm_fwd2.hip
 
 extern "C" int vu_gemm_set_tuning(int key, int value) {
   if (key == VU_TUNE_V4_MIN_BLOCKS) {
@@ -613,6 +650,11 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
     g_splitk = value;
     return 0;
   }
-  if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0) return 0;
+  if (key == VU_TUNE_V4_SPLIT_CHUNKS) {
+    g_split_min_chunks = value;
+    return 0;
+  }
+  if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0 || gemm_fwd_v2_tune(key, value) == 0)
+    return 0;
   return (int)hipErrorInvalidValue;
 }

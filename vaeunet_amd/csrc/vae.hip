@@ -149,18 +149,22 @@ __global__ void relu_mask_kernel(const T* dout, int64_t ds, const T* out, int64_
 }
 
 // out[n][c] (+)= scale * sum_{p of sample n} x[n,p,c]; one block per sample
+// stage 1: grid (N, S): block (n, s) sums pixels [s*per, (s+1)*per) of
+// sample n into part[n][s][C] (16-byte rows, fixed order)
+constexpr int SS_SPLITS = 64;
 template <typename T>
-__global__ void sample_sum_kernel(const T* x, int64_t xs, int HW, int C, float scale, float* out, int accumulate) {
+__global__ void sample_sum_partial(const T* x, int64_t xs, int HW, int C, int per, float* part) {
   __shared__ float sh[256 * 8];
-  const int n = blockIdx.x;
+  const int n = blockIdx.x, sidx = blockIdx.y;
   const int V = C >> 3, R = 256 / V;
   const int cv = threadIdx.x % V, row = threadIdx.x / V;
   const int c = cv * 8;
+  const int p0 = sidx * per, p1 = min(HW, p0 + per);
   float s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = 0.f;
   if (row < R)
-    for (int p = row; p < HW; p += R) {
+    for (int p = p0 + row; p < p1; p += R) {
       Vec8<T> v;
       v.load(x + ((int64_t)n * HW + p) * xs + c);
 #pragma unroll
@@ -173,9 +177,18 @@ __global__ void sample_sum_kernel(const T* x, int64_t xs, int HW, int C, float s
   for (int cc = threadIdx.x; cc < C; cc += 256) {
     float t = 0.f;
     for (int q = 0; q < R; ++q) t += sh[q * C + cc];
-    float* o = out + (int64_t)n * C + cc;
-    *o = accumulate ? *o + scale * t : scale * t;
+    part[((int64_t)n * gridDim.y + sidx) * C + cc] = t;
   }
+}
+
+// stage 2: out[n][c] (+)= scale * sum_s part[n][s][c] (fixed order)
+__global__ void sample_sum_final(const float* part, int N, int S, int C, float scale, float* out, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)N * C) return;
+  const int n = (int)(e / C), c = (int)(e - (int64_t)n * C);
+  float t = 0.f;
+  for (int s = 0; s < S; ++s) t += part[((int64_t)n * S + s) * C + c];
+  out[e] = accumulate ? out[e] + scale * t : scale * t;
 }
 
 // y[n,p,c] (+)= scale * v[n][c] for every pixel p (exact broadcast)
@@ -300,14 +313,22 @@ extern "C" int vu_relu_mask(const void* dout, int64_t ds, const void* out, int64
   return (int)hipGetLastError();
 }
 
+extern "C" int64_t vu_sample_sum_workspace_bytes(int N, int C) {
+  return (int64_t)N * SS_SPLITS * C * (int64_t)sizeof(float);
+}
+
 extern "C" int vu_sample_sum(const void* x, int64_t xs, int N, int HW, int C, float scale, float* out,
-                             int accumulate, int dtype, void* stream) {
+                             int accumulate, float* workspace, int dtype, void* stream) {
   if (C % 8 || xs % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
+  if (N == 0 || C == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int per = (HW + SS_SPLITS - 1) / SS_SPLITS;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((sample_sum_kernel<T>), dim3(N), dim3(256), 0, st, (const T*)x, xs, HW, C, scale, out,
-                       accumulate);
+    hipLaunchKernelGGL((sample_sum_partial<T>), dim3(N, SS_SPLITS), dim3(256), 0, st, (const T*)x, xs, HW, C, per,
+                       workspace);
   })
+  hipLaunchKernelGGL(sample_sum_final, dim3((unsigned)(((int64_t)N * C + 255) / 256)), dim3(256), 0, st, workspace,
+                     N, SS_SPLITS, C, scale, out, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -244,8 +244,10 @@ def sample_sum(M, x, scale=1.0, out=None, accumulate=False):
     N, C_, H, W = x.shape
     if out is None:
         out = torch.empty((N, C_), dtype=torch.float32, device=x.device)
+    ws = torch.empty(K.query("vu_sample_sum_workspace_bytes", N, C_) // 4 + 1, dtype=torch.float32,
+                     device=x.device)
     K.call("vu_sample_sum", K.ptr(x), K.pstride(x), N, H * W, C_, float(scale), K.ptr(out),
-           1 if accumulate else 0, K.dcode(x.dtype), K.stream())
+           1 if accumulate else 0, K.ptr(ws), K.dcode(x.dtype), K.stream())
     return out
 
 
