@@ -116,13 +116,17 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *   VU_TUNE_V4_SPLIT_CHUNKS: fewest 32-channel chunks per automatic split-K
  *     slice (default 2);
  *   VU_TUNE_V2_SMALL: 1 (default) serves small grids (too few 256-row
- *     tiles) with 128x64 4-wave v2 tiles instead of split-K / v3. */
+ *     tiles) with 128x64 4-wave v2 tiles instead of split-K / v3;
+ *   VU_TUNE_V5: 1 (default) serves the short-K 1x1 / ConvTranspose GEMMs
+ *     with the persistent v5 kernel (gemm_fwd5.hip), 0 routes them to v2,
+ *     k >= 2 caps its grid at k blocks (tests: several tiles per block). */
 #define VU_TUNE_V4_MIN_BLOCKS 0
 #define VU_TUNE_FP8_GRID 4
 #define VU_TUNE_STREAM 5
 #define VU_TUNE_V4_SPLITK 6
 #define VU_TUNE_V4_SPLIT_CHUNKS 8
 #define VU_TUNE_V2_SMALL 9
+#define VU_TUNE_V5 10
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */

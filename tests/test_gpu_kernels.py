@@ -329,6 +329,93 @@ def test_gemm_stream_convT(cin, cout):
     _close(out, ref, "bf16", what="stream convT")
 
 
+TUNE_V5 = 10
+V5_CASES = [
+    # (N, Cin, H, W, Cout, grid cap): persistent short-K GEMM (gemm_fwd5.hip)
+    (8, 256, 64, 64, 256, 0),    # 4 K steps, 2 column tiles, one tile per block
+    (8, 512, 64, 64, 256, 7),    # 8 K steps, ~37 tiles per block
+    (16, 256, 64, 64, 64, 5),    # 64-column tiles
+    (8, 1024, 32, 64, 512, 3),   # 16 K steps, 4 column tiles
+]
+
+
+def _stats_check(st, stored):
+    n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                     dtype=torch.float64)
+    s_ = st.psum.double().cpu()
+    mean = s_.sum(0) / n.sum()
+    m2 = st.pm2.double().cpu() + n[:, None] * (s_ / n[:, None] - mean) ** 2
+    torch.testing.assert_close(mean.float(), stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close((m2.sum(0) / n.sum()).float(), stored.var((0, 2, 3), unbiased=False),
+                               rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("case", V5_CASES)
+def test_gemm_v5_fwd_stats_accumulate(case):
+    """1x1 conv with K = 256..1024 on the persistent v5 kernel: bias + BN
+    partials (64-row tiles), and the accumulating input gradient into a
+    channel slice of a wider tensor; grid caps force several tiles per block
+    (the flattened tile / k-step ring crossing tile boundaries)."""
+    K, E = _k()
+    N, cin, H, W, co, cap = case
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(N, cin, H, W, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(co, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(co, generator=g)
+    wq = w.to(torch.bfloat16).float()
+    d = _code("bf16")
+    xs = _act(x, "bf16")
+    wm = E.w1x1_fwd(w.to(DEV), d)
+    _tune((TUNE_V5, cap if cap else 1))
+    try:
+        out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
+        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out, K.gather1x1)) == 64
+        st = K.gemm_fwd(K.gather1x1([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
+        _close(out, F.conv2d(x, wq, b), "bf16", what="v5 fwd")
+        _stats_check(st, out.float().cpu())
+        # input gradient: K = co, N = cin, accumulated into channels [64, 64 + cin)
+        du = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
+        base = torch.randn(N, cin + 64, H, W, generator=g).to(torch.bfloat16).float()
+        wide = _act(base, "bf16")
+        K.gemm_fwd(K.gather1x1([_act(du, "bf16")]), E.w1x1_dgrad(w.to(DEV), d), cin, wide, d, out_coff=64,
+                   accumulate=True)
+        exp = base.clone()
+        exp[:, 64:] += torch.nn.grad.conv2d_input((N, cin, H, W), wq, du)
+        _close(wide, exp, "bf16", what="v5 dgrad accumulate")
+    finally:
+        _tune((TUNE_V5, 1))
+
+
+@pytest.mark.parametrize("ci,co,h,cap", [(512, 256, 32, 0), (256, 128, 64, 6), (1024, 512, 32, 0)])
+def test_gemm_v5_convT(ci, co, h, cap):
+    """ConvTranspose2d 2x2/s2 of the deeper decoder levels on v5: forward with
+    the pixel-shuffle store (bias per output channel) and the input gradient
+    as a 2x2 parity gather (K = 4*co)."""
+    K, E = _k()
+    N = 8
+    g = torch.Generator().manual_seed(37)
+    x = torch.randn(N, ci, h, h, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(ci, co, 2, 2, generator=g) / ci ** 0.5
+    b = torch.randn(co, generator=g)
+    wq = w.to(torch.bfloat16).float()
+    d = _code("bf16")
+    _tune((TUNE_V5, cap if cap else 1))
+    try:
+        out = K.empty_act(N, co, 2 * h, 2 * h, torch.bfloat16, DEV)
+        K.gemm_fwd(K.gather1x1([_act(x, "bf16")]), E.wT_fwd(w.to(DEV), d), 4 * co, out, d, bias=b.to(DEV),
+                   convT=(2 * h, 2 * h, 0, 0, co))
+        xr = x.clone().requires_grad_(True)
+        ref = F.conv_transpose2d(xr, wq, b, stride=2)
+        _close(out, ref, "bf16", what="v5 convT fwd")
+        du = torch.randn(N, co, 2 * h, 2 * h, generator=g).to(torch.bfloat16).float()
+        ref.backward(du)
+        dx = K.empty_act(N, ci, h, h, torch.bfloat16, DEV)
+        K.gemm_fwd(K.gather_convT(_act(du, "bf16"), N, h, h), E.wT_dgrad(w.to(DEV), d), ci, dx, d)
+        _close(dx, xr.grad, "bf16", what="v5 convT dgrad")
+    finally:
+        _tune((TUNE_V5, 1))
+
+
 def _row_tile_args(K, srcs, wmat, ncol, out, gather=None):
     import ctypes as C
     from vaeunet_amd import _lib

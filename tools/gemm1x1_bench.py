@@ -1,7 +1,7 @@
 """Per-call timing of the short-K GEMMs of UNet(3,2) at 3x512x512 B=8 (attention
 1x1 fwd / input-grad, ConvTranspose fwd / input-grad) through the C-ABI, with
 an optional check against torch fp32 ops on the GPU.
-usage: python tools/gemm1x1_bench.py [--check] [--reps N]"""
+usage: python tools/gemm1x1_bench.py [--check] [--reps N] [--tune KEY=VAL,...]"""
 import argparse
 import os
 import sys
@@ -39,7 +39,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tune", default="", help="KEY=VAL,... for vu_gemm_set_tuning")
     args = ap.parse_args()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(k), int(v))
     dev = torch.device("cuda")
     torch.manual_seed(0)
     d = _lib.BF16

@@ -335,6 +335,8 @@ int conv_image_bm(const VuGemmFwd& p, int dtype);      // conv_image.hip (3-chan
 int conv_image_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_stream_bm(const VuGemmFwd& p, int dtype);     // gemm_stream.hip (short-K 1x1 streams)
 int gemm_stream_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd5.hip (persistent short-K GEMM)
+int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st);
 
 static bool use_v2(int dtype) {
   static int mode = -1;
@@ -377,7 +379,9 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return 128;
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 256;
   if (use_v2(dtype)) {
-    int bm = gemm_fwd_v2_bm(*args, dtype);
+    int bm = gemm_fwd_v5_bm(*args, dtype);
+    if (bm) return bm;
+    bm = gemm_fwd_v2_bm(*args, dtype);
     if (bm) return bm;
   }
   return pick_bm(*args);
@@ -403,6 +407,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
+  if (use_v2(dtype) && gemm_fwd_v5_bm(*args, dtype)) return gemm_fwd_v5_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);
 }

@@ -35,8 +35,8 @@ VU_DEV int swz(int row, int chunk) { return row * KB + ((chunk ^ (row & 7)) << 4
 
 struct Pix { int n, h, w; bool ok; };
 
-template <int BM, int BN, int WM, int WN, int NS, bool SPLIT = false>
-__global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd p) {
+template <int BM, int BN, int WM, int WN, int NS, bool SPLIT = false, int OCC = 1>
+__global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFwd p) {
   constexpr int NT = WM * WN * 64;
   constexpr int EPC = 8;                  // bf16 per 16-byte chunk
   constexpr int BKE = 64;                 // K elements per step
@@ -279,11 +279,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void gemm_fwd_v2_kernel(VuGemmFwd 
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NS>
+template <int BM, int BN, int WM, int WN, int NS, int OCC = 1>
 int launch(const VuGemmFwd& p, hipStream_t st) {
   int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
   int64_t nblk = ((M + BM - 1) / BM) * ((p.ncol + BN - 1) / BN);
-  hipLaunchKernelGGL((gemm_fwd_v2_kernel<BM, BN, WM, WN, NS>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0, st, p);
+  hipLaunchKernelGGL((gemm_fwd_v2_kernel<BM, BN, WM, WN, NS, false, OCC>), dim3((unsigned)nblk), dim3(WM * WN * 64), 0,
+                     st, p);
   return (int)hipGetLastError();
 }
 
@@ -299,13 +300,14 @@ int launch_ns(const VuGemmFwd& p, hipStream_t st) {
 // block's life is dominated by its load latency and epilogue: 0 = 256-row
 // tiles, 1 = 128-row tiles (8 waves), 2 = 128-row tiles (4 waves).
 int v2_cfg(const VuGemmFwd& p) {
-  static int mode = -1;
+  static int mode = -1, all = 0;
   if (mode < 0) {
     const char* e = getenv("VU_V2_CFG");
     mode = e ? atoi(e) : 0;
+    all = getenv("VU_V2_CFG_ALL") != nullptr;
   }
   const int nk = (p.a.R * p.a.S * p.a.C + 63) / 64;
-  return nk <= 2 ? mode : 0;
+  return nk <= 2 || all ? mode : 0;
 }
 
 }  // namespace
@@ -333,7 +335,8 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
   int bn = p.ncol <= 64 ? 64 : 128;
   int64_t tiles = ((M + 255) / 256) * ((p.ncol + bn - 1) / bn);
   if (tiles < 256) return 0;
-  return v2_cfg(p) ? 128 : 256;
+  const int cfg = v2_cfg(p);
+  return cfg == 0 || cfg == 4 ? 256 : 128;
 }
 
 // Small grids (the ResNet34 encoder's 64^2 / 32^2 / 16^2 levels: too few
@@ -396,6 +399,15 @@ int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st) {
     case 2:
       if (p.ncol <= 64) return launch_ns<128, 64, 2, 2>(p, st);
       return launch_ns<128, 128, 2, 2>(p, st);
+    case 3:
+      if (p.ncol <= 64) return launch<128, 64, 2, 2, 2, 2>(p, st);
+      return launch<128, 128, 2, 2, 2, 2>(p, st);
+    case 4:
+      if (p.ncol <= 64) return launch<256, 64, 8, 1, 2>(p, st);
+      return launch<256, 128, 4, 2, 2>(p, st);
+    case 5:
+      if (p.ncol <= 128) return launch<128, 128, 2, 4, 2>(p, st);
+      return launch<128, 256, 2, 4, 2>(p, st);
     default:
       if (p.ncol <= 64) return launch_ns<256, 64, 8, 1>(p, st);
       return launch_ns<256, 128, 4, 2>(p, st);

@@ -1,0 +1,350 @@
+// Persistent short-K GEMM ("v5", bf16): out[m][j] = sum_k A[m][k] B[j][k]
+// for the 1x1-type problems of gemm_fwd2.hip whose K is a few 64-wide steps
+// (K = 128..2048: attention-gate convs and their input gradients below the
+// 256^2 level, ConvTranspose2d forward with the pixel-shuffle store, the
+// ConvTranspose2d input gradient as a 2x2 parity gather).
+//
+// With 4-16 K steps per 256-row tile, a block that loads, computes and then
+// stages its tile through LDS for the stores spends most of its life in the
+// pipeline fill and the epilogue (gemm_fwd2.hip measured 270-450 TFLOP/s
+// here).  This kernel keeps one block per CU alive over a strided walk of
+// tiles and flattens (tile, k-step) into ONE stream of steps, so the LDS-DMA
+// ring never drains: the first stages of tile t+1 are in flight while tile t
+// finishes and stores.
+//
+//   * MFMA(B-fragment, A-fragment): the accumulator rows are output COLUMNS,
+//     so a lane owns 4*GS consecutive output columns of one pixel (B rows are
+//     read in a permuted order, as in gemm_stream.hip) and stores 16/32-byte
+//     pieces straight from registers -- no LDS staging, no barrier;
+//   * the B tile's LDS swizzle takes bit 3/4 of the row instead of bit 2 so
+//     the permuted fragment reads stay conflict-free;
+//   * BatchNorm partial statistics per wave (64 rows) by DPP row sums;
+//   * accumulate (input gradients): the old output values are loaded at the
+//     start of the tile's last step, before the next stage's DMA, so waiting
+//     for them does not drain the ring.
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+static __device__ __attribute__((aligned(16))) uint32_t v5_zero_page[16];
+
+namespace {
+
+constexpr int KB = 128;  // bytes of K per LDS row per step (64 bf16)
+constexpr int BM = 256, WM = 4, WN = 2, NT = WM * WN * 64, NS = 3;
+typedef __attribute__((address_space(3))) void lds_void;
+
+VU_DEV int swz_a(int row, int chunk) { return row * KB + ((chunk ^ (row & 7)) << 4); }
+template <int GS>
+VU_DEV int fb(int row) { return (row & 3) | (((row >> (GS == 4 ? 4 : 3)) & 1) << 2); }
+template <int GS>
+VU_DEV int swz_b(int row, int chunk) { return row * KB + ((chunk ^ fb<GS>(row)) << 4); }
+
+template <int N>
+VU_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <int R>
+VU_DEV float ror_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xf, 0xf, false));
+}
+VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
+VU_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+VU_DEV float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
+VU_DEV float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+struct Pix { int n, h, w; bool ok; };
+
+template <int BN, bool STATS, bool ACC>
+__global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
+  constexpr int WNC = BN / WN;          // columns per wave: 64 or 32
+  constexpr int TM = BM / WM / 16;      // 4 pixel fragments per wave
+  constexpr int TN = WNC / 16;          // 4 or 2 column fragments per wave
+  constexpr int GS = TN;                // a lane owns 4*GS consecutive columns
+  constexpr int CPL = GS / 2;           // 16-byte pieces per lane and pixel
+  constexpr int LA = BM * 8 / NT, LB = BN * 8 / NT, NL = LA + LB;
+  constexpr int NST = TM * CPL + (STATS ? 2 * TN : 0);  // vector stores per epilogue
+  constexpr int STAGE = (BM + BN) * KB;
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+
+  const VuGather& g = p.a;
+  const int M = g.N * g.H * g.W;  // < 2^31 (host check)
+  const int HW = g.H * g.W;
+  const int K = g.R * g.S * g.C;
+  const int nk = (K + 63) / 64;
+  const int ntiles = p.ncol / BN;
+  const int T = (M / BM) * ntiles;
+  const int G = gridDim.x;
+  const int lb = xcd_remap(blockIdx.x, G);
+  const int mine = (T - lb + G - 1) / G;
+  const int S = mine * nk;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int gq = lane >> 4, r16 = lane & 15;
+  const int pchunk = lane & 7;
+  const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
+  const void* zp = (const void*)v5_zero_page;
+
+  // ---- staging state: the tile / k-step the next stage() call loads ----
+  int sg_t = lb, sg_kt = 0, sg_n0 = 0;
+  Pix pa[LA];
+  auto stage = [&](int slot) {
+    if (sg_kt == 0) {
+      const int mt = sg_t / ntiles;
+      sg_n0 = (sg_t - mt * ntiles) * BN;
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        const int m = mt * BM + ((i * NT + tid) >> 3);
+        pa[i].n = m / HW;
+        const int rem = m - pa[i].n * HW;
+        pa[i].h = rem / g.W;
+        pa[i].w = rem - pa[i].h * g.W;
+      }
+    }
+    const int k0 = sg_kt * 64;
+    const int tap = k0 / g.C;
+    const int r = tap / g.S, s = tap - (tap / g.S) * g.S;
+    const int cbase = k0 - tap * g.C;
+    const int t = (cbase >= g.cend[0]) + (g.nsrc > 2 && cbase >= g.cend[1]);
+    const int c0 = t == 0 ? 0 : g.cend[t - 1];
+    const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[t]);
+    const int64_t st = g.stride[t];
+    char* A = smem + slot * STAGE;
+    char* B = A + BM * KB;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int row = (i * NT + tid) >> 3;
+      const int lchunk = pchunk ^ (row & 7);
+      const int hs = pa[i].h * g.sy + r * g.dy + g.oy;
+      const int ws = pa[i].w * g.sx + s * g.dx + g.ox;
+      const void* gp = zp;
+      if ((unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws && cbase + lchunk * 8 < g.cend[t]) {
+        const int64_t pix = ((int64_t)pa[i].n * g.Hs + hs) * g.Ws + ws;
+        gp = src + pix * st + (cbase - c0) + lchunk * 8;
+      }
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int row = (i * NT + tid) >> 3;
+      const int lchunk = pchunk ^ fb<GS>(row);
+      const void* gp = zp;
+      if (k0 + lchunk * 8 < K) gp = bmat + (int64_t)(sg_n0 + row) * p.ldb + k0 + lchunk * 8;
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
+    }
+    if (++sg_kt == nk) {
+      sg_kt = 0;
+      sg_t += G;
+    }
+  };
+
+  // B row (output column, wave-local) read by fragment j, lane row rr
+  auto wrow = [&](int j, int rr) { return 4 * GS * (rr >> 2) + 4 * j + (rr & 3); };
+  // destination of this lane's columns [col0, col0 + 4*GS) of pixel m
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  auto dst_of = [&](int m, int col0) -> bf16_t* {
+    if (p.out_mode == 0) return out + (int64_t)m * p.out_stride + p.out_coff + col0;
+    const int n = m / HW;
+    const int rem = m - n * HW;
+    const int h = rem / g.W, w = rem - (rem / g.W) * g.W;
+    if (p.out_mode == 2)
+      return out + ((int64_t)(n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx) * p.out_stride + p.out_coff + col0;
+    const int ab = col0 / p.cout, co = col0 - ab * p.cout;
+    const int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
+    return out + ((int64_t)(n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+  u32x4 old[TM][CPL];
+  bf16_t* dst[TM];
+
+  int ct = lb, ckt = 0;  // tile / k-step being computed
+  stage(0);
+  if (S > 1) stage(1);
+  for (int s = 0; s < S; ++s) {
+    const bool after_epi = s > 0 && ckt == 0;
+    if (s + 1 < S) {
+      if (after_epi) wait_vm<NL + NST>(); else wait_vm<NL>();
+    } else {
+      if (after_epi) wait_vm<NST>(); else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool last = ckt == nk - 1;
+    const int mt = ct / ntiles;
+    const int m0 = mt * BM, n0 = (ct - mt * ntiles) * BN;
+    const int col0 = n0 + wn * WNC + 4 * GS * gq;
+    if (last) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        dst[i] = dst_of(m0 + wm * 64 + 16 * i + r16, col0);
+        if (ACC) {
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) old[i][c] = *reinterpret_cast<const u32x4*>(dst[i] + 8 * c);
+        }
+      }
+    }
+    if (s + 2 < S) stage((s + 2) % NS);
+    const char* A = smem + (s % NS) * STAGE;
+    const char* B = A + BM * KB;
+    u32x4 af[2][TM], bf[2][TN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + gq;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[kk][i] = *reinterpret_cast<const u32x4*>(A + swz_a(wm * 64 + 16 * i + r16, ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bf[kk][j] = *reinterpret_cast<const u32x4*>(B + swz_b<GS>(wn * WNC + wrow(j, r16), ch));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[kk][j]),
+                                                              __builtin_bit_cast(bf16x8, af[kk][i]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (!last) {
+      ++ckt;
+      continue;
+    }
+    // ---- epilogue from registers: acc[i][j][r] = pixel m0 + wm*64 + 16i + r16,
+    //      column col0 + 4j + r ----
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      f32x4 bv = f32x4{0, 0, 0, 0};
+      if (p.bias) {
+        const int c = col0 + 4 * j;
+        bv = *reinterpret_cast<const f32x4*>(p.bias + (p.out_mode == 1 ? c % p.cout : c));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv[r]);
+    }
+    // the old values were loaded before stage(s + 2): only that stage may stay in flight
+    if (ACC) {
+      if (s + 2 < S) wait_vm<NL>(); else wait_vm<0>();
+    }
+    if (STATS) {
+      const int srow = (m0 >> 6) + wm;  // 64-row statistics tile
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        f32x4 sm, m2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float sv = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i) sv += acc[i][j][r];
+          sv = row16_sum(sv);
+          const float mean = sv * (1.f / 64.f);
+          float v = 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const float d = acc[i][j][r] - mean;
+            v += d * d;
+          }
+          sm[r] = sv;
+          m2[r] = row16_sum(v);
+        }
+        if (r16 == 0) {
+          *reinterpret_cast<f32x4*>(p.stat_sum + (int64_t)srow * p.ncol + col0 + 4 * j) = sm;
+          *reinterpret_cast<f32x4*>(p.stat_m2 + (int64_t)srow * p.ncol + col0 + 4 * j) = m2;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const f32x4 a = acc[i][2 * c], b = acc[i][2 * c + 1];
+        u32x4 v;
+        if (ACC) {
+          const u32x4 o = old[i][c];
+          v = u32x4{pack2(lo_f(o[0]) + a[0], hi_f(o[0]) + a[1]), pack2(lo_f(o[1]) + a[2], hi_f(o[1]) + a[3]),
+                    pack2(lo_f(o[2]) + b[0], hi_f(o[2]) + b[1]), pack2(lo_f(o[3]) + b[2], hi_f(o[3]) + b[3])};
+        } else {
+          v = u32x4{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
+        }
+        *reinterpret_cast<u32x4*>(dst[i] + 8 * c) = v;
+      }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+    ckt = 0;
+    ct += G;
+  }
+}
+
+int cu_count5() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+int g_v5 = 1;  // VU_TUNE_V5: 0 off, 1 on, k >= 2 on with the grid capped at k (tests)
+
+template <int BN, bool STATS, bool ACC>
+int launch5(const VuGemmFwd& p, hipStream_t st) {
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  const int64_t T = (M / BM) * (p.ncol / BN);
+  int64_t grid = T < cu_count5() ? T : cu_count5();
+  if (g_v5 >= 2 && grid > g_v5) grid = g_v5;
+  hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC>), dim3((unsigned)grid), dim3(NT), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+template <int BN>
+int launch_bn(const VuGemmFwd& p, hipStream_t st) {
+  const bool stats = p.stat_sum != nullptr, acc = p.accumulate != 0;
+  if (stats) return acc ? launch5<BN, true, true>(p, st) : launch5<BN, true, false>(p, st);
+  return acc ? launch5<BN, false, true>(p, st) : launch5<BN, false, false>(p, st);
+}
+
+}  // namespace
+
+int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype);  // gemm_fwd2.hip (shared eligibility)
+
+// Statistics row tile (64) when v5 serves this problem, else 0: every v2
+// problem with whole 256-row tiles, 64 / 128-multiple column counts, a
+// 32-bit pixel count and at least 2 K steps.
+int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype) {
+  if (g_v5 == 0 || gemm_fwd_v2_bm(p, dtype) == 0) return 0;
+  const VuGather& g = p.a;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  if (M % BM != 0 || M >= ((int64_t)1 << 31)) return 0;
+  if (p.ncol != 64 && p.ncol % 128 != 0) return 0;
+  if (p.out_mode == 1 && p.cout % 16 != 0) return 0;
+  if (p.out_mode != 0 && p.out_mode != 1 && p.out_mode != 2) return 0;
+  if (p.ldb < 0 || (p.out_stride % 8) != 0 || (p.out_coff % 8) != 0) return 0;
+  const int nk = (g.R * g.S * g.C + 63) / 64;
+  if (nk < 2) return 0;
+  return 64;
+}
+
+int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st) {
+  if (p.ncol == 64) return launch_bn<64>(p, st);
+  return launch_bn<128>(p, st);
+}
+
+int gemm_fwd_v5_tune(int key, int value) {
+  if (key == VU_TUNE_V5) {
+    g_v5 = value < 0 ? 0 : value;
+    return 0;
+  }
+  return -1;
+}
