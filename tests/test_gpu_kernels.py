@@ -592,6 +592,61 @@ def test_batchnorm_train(mode, relu, shape):
     torch.testing.assert_close(bn_dev.bias.grad.cpu(), bn.bias.grad, rtol=2e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("tiles,tile_rows,C", [(40000, 7, 64), (300, 128, 192), (5, 64, 8)])
+def test_bn_finalize_partials(tiles, tile_rows, C):
+    """vu_bn_finalize on synthetic per-tile (sum, M2) partials: several rounds
+    per block (tiles > 64 x 256), several blocks and channel groups, a ragged
+    last tile; mean / biased var / running stats vs an fp64 combination."""
+    K, _ = _k()
+    g = torch.Generator().manual_seed(41)
+    rows = tiles * tile_rows - 3
+    n = torch.full((tiles,), float(tile_rows), dtype=torch.float64)
+    n[-1] = tile_rows - 3
+    mu_t = torch.randn(tiles, C, generator=g, dtype=torch.float64) * 0.5 + 2.0
+    m2_t = torch.rand(tiles, C, generator=g, dtype=torch.float64) * n[:, None]
+    psum = (mu_t * n[:, None]).float()
+    pm2 = m2_t.float()
+    st = K.Stats(psum.to(DEV), pm2.to(DEV), tiles, tile_rows, rows)
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g)
+    rm, rv = torch.zeros(C), torch.ones(C)
+    nbt = torch.zeros((), dtype=torch.int64)
+    rm_d, rv_d, nbt_d = rm.to(DEV), rv.to(DEV), nbt.to(DEV)
+    coef = K.bn_finalize(st, C, gamma.to(DEV), beta.to(DEV), rm_d, rv_d, nbt_d, 0.1, 1e-5)
+    s64, q64 = psum.double(), pm2.double()
+    mean = s64.sum(0) / n.sum()
+    M2 = (q64 + n[:, None] * (s64 / n[:, None] - mean) ** 2).sum(0)
+    var = M2 / n.sum()
+    invstd = 1.0 / torch.sqrt(var + 1e-5)
+    c = coef.cpu().double()
+    torch.testing.assert_close(c[2], mean, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(c[3], invstd, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(c[0], gamma.double() * invstd, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv_d.cpu().double(), 0.9 + 0.1 * M2 / (n.sum() - 1), rtol=1e-5, atol=1e-6)
+    assert int(nbt_d) == 1
+    # a second launch reuses the self-resetting arrival counters
+    coef2 = K.bn_finalize(st, C, gamma.to(DEV), beta.to(DEV), None, None, None, 0.0, 1e-5)
+    assert torch.equal(coef2[:, :].cpu(), coef.cpu())
+
+
+@pytest.mark.parametrize("shape", [(16, 64, 128, 128), (8, 512, 32, 32), (4, 16, 20, 12)])
+def test_chan_sum_fused(shape):
+    """per-channel sums (bias gradients) on the fused one-launch reduction:
+    256 pixel blocks (the cap), several channel groups, narrow channel
+    counts; fixed-order, so two launches agree bitwise."""
+    K, _ = _k()
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(shape, generator=g).to(torch.bfloat16).float()
+    xa = _act(x, "bf16")
+    out = torch.zeros(shape[1], device=DEV)
+    K.chan_sum(xa, out, False, 1)
+    ref = x.double().sum((0, 2, 3))
+    torch.testing.assert_close(out.cpu().double(), ref, rtol=1e-5, atol=1e-3)
+    out2 = torch.full((shape[1],), 1.0, device=DEV)
+    K.chan_sum(xa, out2, True, 1)
+    assert torch.equal(out2.cpu(), out.cpu() + 1.0)
+
+
 def test_loss_kernels_vs_oracle():
     from vaeunet_amd.loss import CombinedLoss, dice_loss, kl_with_free_bits
     from oracle import cpu_ref as R

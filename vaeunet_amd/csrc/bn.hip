@@ -48,14 +48,23 @@ __global__ void bn_stats_stage1(const float* psum, const float* pm2, int tiles, 
   for (int tb = tb0; tb < te0; tb += STATS_TPB) {
     const int te = min(te0, tb + STATS_TPB);
     const int64_t n_r = min(rows, (int64_t)te * tile_rows) - (int64_t)tb * tile_rows;
+    // clamped addresses and unconditional loads, selected afterwards (a
+    // guarded load compiles to a branch + vmcnt(0) each: serial round trips)
     float sv[U], mv[U];
     double nv[U];
+    const int cc = ok ? c : 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(tb + tl + 4 * u, te - 1);
+      sv[u] = psum[(int64_t)t * C + cc];
+      mv[u] = pm2[(int64_t)t * C + cc];
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int t = tb + tl + 4 * u;
       const bool in = ok && t < te;
-      sv[u] = in ? psum[(int64_t)t * C + c] : 0.f;
-      mv[u] = in ? pm2[(int64_t)t * C + c] : 0.f;
+      sv[u] = in ? sv[u] : 0.f;
+      mv[u] = in ? mv[u] : 0.f;
       int64_t nt = rows - (int64_t)t * tile_rows;
       nv[u] = in ? (double)(nt > tile_rows ? tile_rows : nt) : 0.0;
     }
@@ -101,12 +110,17 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
   double nv[U], mv[U], qv[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int sidx = q + 32 * u;
-    const bool in = ok && sidx < S;
-    const double* o = ws + ((int64_t)(in ? sidx : 0) * C + (ok ? c : 0)) * 3;
-    nv[u] = in ? o[0] : 0.0;
-    mv[u] = in ? o[1] : 0.0;
-    qv[u] = in ? o[2] : 0.0;
+    const double* o = ws + ((int64_t)min(q + 32 * u, S - 1) * C + (ok ? c : 0)) * 3;
+    nv[u] = o[0];
+    mv[u] = o[1];
+    qv[u] = o[2];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool in = ok && q + 32 * u < S;
+    nv[u] = in ? nv[u] : 0.0;
+    mv[u] = in ? mv[u] : 0.0;
+    qv[u] = in ? qv[u] : 0.0;
   }
   double n = 0, sm = 0;
 #pragma unroll
@@ -249,7 +263,7 @@ __global__ void chan_partial_kernel(RedArgs r) {
     for (int u = 0; u < UNR; ++u) {
       const int64_t p = p0 + (int64_t)u * cm.R;
       if (p < r.P) {
-        va[u].load(reinterpret_cast<const T*>(r.a) + win_pix(r, p) * r.as + c);
+        va[u].load(reinterpret_cast<const T*>(r.a) + (MODE == 0 ? win_pix(r, p) : p) * r.as + c);
         if (MODE == 1) vb[u].load(reinterpret_cast<const T*>(r.b) + p * r.bs + c);
       }
     }

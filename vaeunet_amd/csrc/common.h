@@ -92,35 +92,37 @@ VU_DEV int xcd_remap(int bid, int nblk) {
 // Deterministic fp64 column sums of a partial matrix written by a stage-1
 // reduction: element (row r, quantity k, column c) lives at
 // part[r * row_stride + k * q_stride + c].  A 1024-thread block covers 32
-// columns x 32 row lanes; each lane keeps 4 independent accumulators so its
-// loads are issued back to back (the stage-2 pass is latency-, not
+// columns x 32 row lanes; a lane loads its rows COLSUM_U at a time from
+// clamped addresses, unconditionally (a guarded or loop-carried load per row
+// serialises the memory round trips: the stage-2 pass is latency-, not
 // bandwidth-bound), then a fixed-shape LDS tree folds the 32 lanes.  Every
 // thread of the block must call it; out[k] is valid for threads with lane 0
 // (threadIdx.x < 32).  Summation order is fixed: results are reproducible.
-constexpr int COLSUM_THREADS = 1024;
+constexpr int COLSUM_THREADS = 1024, COLSUM_U = 8;
 template <int NQ>
 VU_DEV void colsum32(const float* part, int rows, int64_t row_stride, int64_t q_stride, int col, bool valid,
                      double* out) {
   __shared__ double sh[NQ][32][32];
   const int cl = threadIdx.x & 31, q = threadIdx.x >> 5;
-  double s[NQ][4];
+  const int cc = valid ? col : 0;
+  double s[NQ];
 #pragma unroll
-  for (int k = 0; k < NQ; ++k)
+  for (int k = 0; k < NQ; ++k) s[k] = 0.0;
+  for (int r0 = 0; r0 < rows; r0 += 32 * COLSUM_U) {
+    float v[COLSUM_U][NQ];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s[k][u] = 0.0;
-  if (valid) {
-    int r = q;
-    for (; r + 96 < rows; r += 128)
+    for (int u = 0; u < COLSUM_U; ++u) {
+      const int r = min(r0 + q + 32 * u, rows - 1);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int k = 0; k < NQ; ++k) v[u][k] = part[(int64_t)r * row_stride + k * q_stride + cc];
+    }
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) s[k][u] += part[(int64_t)(r + 32 * u) * row_stride + k * q_stride + col];
-    for (; r < rows; r += 32)
+    for (int u = 0; u < COLSUM_U; ++u)
 #pragma unroll
-      for (int k = 0; k < NQ; ++k) s[k][0] += part[(int64_t)r * row_stride + k * q_stride + col];
+      for (int k = 0; k < NQ; ++k) s[k] += (valid && r0 + q + 32 * u < rows) ? (double)v[u][k] : 0.0;
   }
 #pragma unroll
-  for (int k = 0; k < NQ; ++k) sh[k][q][cl] = (s[k][0] + s[k][1]) + (s[k][2] + s[k][3]);
+  for (int k = 0; k < NQ; ++k) sh[k][q][cl] = s[k];
   __syncthreads();
 #pragma unroll
   for (int w = 16; w >= 1; w >>= 1) {
