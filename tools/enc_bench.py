@@ -1,7 +1,9 @@
-"""Per-layer timing of the ResNet34 encoder's 3x3 convolutions (UNetResNet,
-B=8, 3x512^2 input) through the C-ABI: forward and input gradient.
+"""Per-layer timing of the small-grid 3x3 convolutions (the ResNet34 encoder of
+UNetResNet and the UNet(3,2) bottleneck, B=8, 3x512^2 input) through the
+C-ABI: forward and input gradient.
 
 usage: python tools/enc_bench.py [--tune KEY=VAL,...]
+(also times the UNet(3,2) small-grid layers: down4 and up1 at B=8)
 """
 import argparse
 import os
@@ -15,7 +17,9 @@ from vaeunet_amd import _lib  # noqa: E402
 from vaeunet_amd.engine import w3x3_fwd, w3x3_dgrad  # noqa: E402
 
 B = 8
-LAYERS = [("layer1", 64, 64, 128), ("layer2", 128, 128, 64), ("layer3", 256, 256, 32), ("layer4", 512, 512, 16)]
+LAYERS = [("layer1", 64, 64, 128), ("layer2", 128, 128, 64), ("layer3", 256, 256, 32), ("layer4", 512, 512, 16),
+          # UNet(3,2) small grids: down4 conv1 / conv2, up1 conv2
+          ("unet.down4a", 512, 1024, 32), ("unet.down4b", 1024, 1024, 32), ("unet.up1b", 512, 512, 64)]
 
 
 def timeit(fn, reps=20):

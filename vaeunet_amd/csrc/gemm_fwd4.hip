@@ -423,15 +423,44 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) bv[e] = p.bias ? p.bias[c0 + e] : 0.f;
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  // slab sums in k order; the 4 row groups x 2 splits of loads are issued
+  // together (a per-row k loop waits one memory round trip per load)
+  f32x4 sa[4], sb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sa[q] = sb[q] = f32x4{0, 0, 0, 0};
+  const float* src0 = p.workspace + ((int64_t)rb * 128 + rs) * p.ncol + c0;
+  const int64_t qs = 32 * (int64_t)p.ncol;
+  int k = 0;
+  for (; k + 2 <= p.ksplit; k += 2) {
+    f32x4 ta[2][4], tb[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float* src = src0 + (k + h) * slab + q * qs;
+        ta[h][q] = *reinterpret_cast<const f32x4*>(src);
+        tb[h][q] = *reinterpret_cast<const f32x4*>(src + 4);
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sa[q] += ta[h][q];
+        sb[q] += tb[h][q];
+      }
+  }
+  if (k < p.ksplit) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float* src = src0 + k * slab + q * qs;
+      sa[q] += *reinterpret_cast<const f32x4*>(src);
+      sb[q] += *reinterpret_cast<const f32x4*>(src + 4);
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int64_t m = (int64_t)rb * 128 + rs + 32 * q;
-    f32x4 a = f32x4{0, 0, 0, 0}, b = f32x4{0, 0, 0, 0};
-    for (int k = 0; k < p.ksplit; ++k) {
-      const float* src = p.workspace + k * slab + m * p.ncol + c0;
-      a += *reinterpret_cast<const f32x4*>(src);
-      b += *reinterpret_cast<const f32x4*>(src + 4);
-    }
+    const f32x4 a = sa[q], b = sb[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       v[q][e] = rnd<bf16_t>(a[e] + bv[e]);
@@ -544,8 +573,10 @@ Plan plan(const VuGemmFwd& p) {
   }
   const int maxks = chunks / (g_split_min_chunks > 0 ? g_split_min_chunks : 1);
   if (g_splitk == 0 || maxks < 2) return r;
-  // small grids the 128x64 v2 tiles fill without split-K slabs go there
-  if (g_splitk == 1 && gemm_fwd_v2_small(p, VU_BF16)) return r;
+  // small grids the 128x64 v2 tiles fill go there -- unless K is long
+  // (>= 512 input channels: the UNet down4 input gradient, 1024 -> 512 at
+  // 32^2, ran 201 us on v2 tiles vs 80 us split 4 ways here, tools/enc_bench.py)
+  if (g_splitk == 1 && g.C < 512 && gemm_fwd_v2_small(p, VU_BF16)) return r;
   int bn = 0;
   int64_t blocks = 0;
   if (tiles_ok<256>(p)) {

@@ -86,12 +86,25 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
   const void* zp = (const void*)v5_zero_page;
 
   // ---- staging state: the tile / k-step the next stage() call loads ----
-  int sg_t = lb, sg_kt = 0, sg_n0 = 0;
+  // A lane's rows and chunks are fixed; per (tile, tap, source) SEGMENT of
+  // k-steps its row pointers are resolved once and then advance by 64
+  // channels per step (the per-step gather decode cost more VALU time than
+  // the MFMAs of the step).
+  const int lch_a = pchunk ^ ((tid >> 3) & 7);     // row & 7 is the same for all LA rows
+  int sg_t = lb, sg_kt = 0, seg_step = 0, seg_rem = 0;
+  const bf16_t* ap[LA];
+  const bf16_t* bp[LB];
+  int lch_b[LB];
+#pragma unroll
+  for (int i = 0; i < LB; ++i) lch_b[i] = pchunk ^ fb<GS>((i * NT + tid) >> 3);
   Pix pa[LA];
   auto stage = [&](int slot) {
+    const int k0 = sg_kt * 64;
+    const int tap = k0 / g.C;
+    const int cbase = k0 - tap * g.C;
     if (sg_kt == 0) {
       const int mt = sg_t / ntiles;
-      sg_n0 = (sg_t - mt * ntiles) * BN;
+      const int n0 = (sg_t - mt * ntiles) * BN;
 #pragma unroll
       for (int i = 0; i < LA; ++i) {
         const int m = mt * BM + ((i * NT + tid) >> 3);
@@ -100,38 +113,42 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
         pa[i].h = rem / g.W;
         pa[i].w = rem - pa[i].h * g.W;
       }
+#pragma unroll
+      for (int i = 0; i < LB; ++i)
+        bp[i] = bmat + (int64_t)(n0 + ((i * NT + tid) >> 3)) * p.ldb + lch_b[i] * 8;
     }
-    const int k0 = sg_kt * 64;
-    const int tap = k0 / g.C;
-    const int r = tap / g.S, s = tap - (tap / g.S) * g.S;
-    const int cbase = k0 - tap * g.C;
-    const int t = (cbase >= g.cend[0]) + (g.nsrc > 2 && cbase >= g.cend[1]);
-    const int c0 = t == 0 ? 0 : g.cend[t - 1];
-    const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[t]);
-    const int64_t st = g.stride[t];
+    if (sg_kt == 0 || cbase == 0 || cbase == g.cend[0] || (g.nsrc > 2 && cbase == g.cend[1])) {
+      const int r = tap / g.S, s = tap - (tap / g.S) * g.S;
+      const int t = (cbase >= g.cend[0]) + (g.nsrc > 2 && cbase >= g.cend[1]);
+      const int c0 = t == 0 ? 0 : g.cend[t - 1];
+      const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[t]);
+      const int64_t st = g.stride[t];
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        const int hs = pa[i].h * g.sy + r * g.dy + g.oy;
+        const int ws = pa[i].w * g.sx + s * g.dx + g.ox;
+        ap[i] = nullptr;
+        if ((unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws)
+          ap[i] = src + (((int64_t)pa[i].n * g.Hs + hs) * g.Ws + ws) * st + (cbase - c0) + lch_a * 8;
+      }
+      seg_step = 0;
+      seg_rem = g.cend[t] - cbase;
+    }
     char* A = smem + slot * STAGE;
     char* B = A + BM * KB;
+    const int off = seg_step * 64;
+    const bool cin = lch_a * 8 < seg_rem - off;  // channel tail of the source
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      const int row = (i * NT + tid) >> 3;
-      const int lchunk = pchunk ^ (row & 7);
-      const int hs = pa[i].h * g.sy + r * g.dy + g.oy;
-      const int ws = pa[i].w * g.sx + s * g.dx + g.ox;
-      const void* gp = zp;
-      if ((unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws && cbase + lchunk * 8 < g.cend[t]) {
-        const int64_t pix = ((int64_t)pa[i].n * g.Hs + hs) * g.Ws + ws;
-        gp = src + pix * st + (cbase - c0) + lchunk * 8;
-      }
+      const void* gp = (ap[i] != nullptr && cin) ? (const void*)(ap[i] + off) : zp;
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      const int row = (i * NT + tid) >> 3;
-      const int lchunk = pchunk ^ fb<GS>(row);
-      const void* gp = zp;
-      if (k0 + lchunk * 8 < K) gp = bmat + (int64_t)(sg_n0 + row) * p.ldb + k0 + lchunk * 8;
+      const void* gp = k0 + lch_b[i] * 8 < K ? (const void*)(bp[i] + k0) : zp;
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
+    ++seg_step;
     if (++sg_kt == nk) {
       sg_kt = 0;
       sg_t += G;
