@@ -33,7 +33,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 VU_DEV int swz(int row, int chunk) { return row * KB + ((chunk ^ (row & 7)) << 4); }
 
-struct Pix { int n, h, w; bool ok; };
 
 template <int BM, int BN, int WM, int WN, int NS, bool SPLIT = false, int OCC = 1>
 __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFwd p) {
@@ -71,22 +70,41 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int pchunk = lane & 7;  // physical chunk this lane writes
 
-  // rows this thread loads: row = (i*NT + tid) / 8
-  Pix pa[LA];
+  // rows this thread loads: row = (i*NT + tid) / 8; its 16-byte chunk of a
+  // row is the same for every row (row & 7 == (tid >> 3) & 7).  Per row the
+  // pixel index and the strided base coordinates are resolved once; a step
+  // then only adds the tap's (uniform) offset -- the per-step gather decode
+  // otherwise costs more VALU time than the step's MFMAs.
+  const int lchunk_a = pchunk ^ ((tid >> 3) & 7);
+  int64_t rpix[LA];   // pixel index of (n, h*sy, w*sx) in the source image
+  int rh[LA], rw[LA]; // h*sy, w*sx (-1 << 20 for rows beyond M: never in bounds)
 #pragma unroll
   for (int i = 0; i < LA; ++i) {
     int row = (i * NT + tid) >> 3;
     int64_t m = m0 + row;
-    pa[i].ok = m < M;
-    int64_t mm = pa[i].ok ? m : 0;
+    const bool ok = m < M;
+    int64_t mm = ok ? m : 0;
     int hw = g.H * g.W;
-    pa[i].n = (int)(mm / hw);
-    int rem = (int)(mm - (int64_t)pa[i].n * hw);
-    pa[i].h = rem / g.W;
-    pa[i].w = rem - pa[i].h * g.W;
+    const int n = (int)(mm / hw);
+    int rem = (int)(mm - (int64_t)n * hw);
+    const int h = rem / g.W;
+    const int w = rem - h * g.W;
+    rh[i] = ok ? h * g.sy : -(1 << 20);
+    rw[i] = w * g.sx;
+    rpix[i] = ((int64_t)n * g.Hs + h * g.sy) * g.Ws + w * g.sx;
   }
   const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
   const void* zp = (const void*)vu_zero_page;
+  const bf16_t* brow[LB];
+  int lchunk_b[LB];
+  bool bok[LB];
+#pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    int row = (i * NT + tid) >> 3;
+    lchunk_b[i] = pchunk ^ (row & 7);
+    bok[i] = n0 + row < p.ncol;
+    brow[i] = bmat + (int64_t)(bok[i] ? n0 + row : 0) * p.ldb + lchunk_b[i] * EPC;
+  }
 
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * BKE;
@@ -95,31 +113,23 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
     const int cbase = k0 - tap * g.C;
     const int t = (cbase >= g.cend[0]) + (g.nsrc > 2 && cbase >= g.cend[1]);
     const int c0 = t == 0 ? 0 : g.cend[t - 1];
-    const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[t]);
+    const bf16_t* src = reinterpret_cast<const bf16_t*>(g.src[t]) + (cbase - c0) + lchunk_a * EPC;
     const int64_t st = g.stride[t];
+    const int dh = r * g.dy + g.oy, dw = s * g.dx + g.ox;
+    const int64_t dpix = (int64_t)dh * g.Ws + dw;
+    const bool cin = cbase + lchunk_a * EPC < g.cend[t];
     char* A = smem + buf * STAGE;
     char* B = A + BM * KB;
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
-      int row = (i * NT + tid) >> 3;
-      int lchunk = pchunk ^ (row & 7);
-      int hs = pa[i].h * g.sy + r * g.dy + g.oy;
-      int ws = pa[i].w * g.sx + s * g.dx + g.ox;
       const void* gp = zp;
-      if (pa[i].ok && (unsigned)hs < (unsigned)g.Hs && (unsigned)ws < (unsigned)g.Ws &&
-          cbase + lchunk * EPC < g.cend[t]) {
-        int64_t pix = ((int64_t)pa[i].n * g.Hs + hs) * g.Ws + ws;
-        gp = src + pix * st + (cbase - c0) + lchunk * EPC;
-      }
+      if (cin && (unsigned)(rh[i] + dh) < (unsigned)g.Hs && (unsigned)(rw[i] + dw) < (unsigned)g.Ws)
+        gp = src + (rpix[i] + dpix) * st;
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
-      int row = (i * NT + tid) >> 3;
-      int lchunk = pchunk ^ (row & 7);
-      int j = n0 + row;
-      const void* gp = zp;
-      if (j < p.ncol && k0 + lchunk * EPC < K) gp = bmat + (int64_t)j * p.ldb + k0 + lchunk * EPC;
+      const void* gp = (bok[i] && k0 + lchunk_b[i] * EPC < K) ? (const void*)(brow[i] + k0) : zp;
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
   };
