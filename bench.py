@@ -29,14 +29,16 @@ PEAK_HBM_GBS = 8000.0
 # fwd 368.13 + dgrad 367.22 + wgrad 368.13 GFLOP (inc.0 included)
 CONV3_GFLOP_PER_IMG = 1103.5
 METRIC = "images/sec (whole node) at 3x512x512 bs=8/GPU; Dice parity vs CPU ref"   # BASELINE.json
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PMC_TRAFFIC = {"unet": os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+               "vae": os.path.join(ROOT, "profiles", "pmc_traffic_vae.json")}
 
 
-def pmc_traffic():
+def pmc_traffic(model):
     """HBM bytes per launch of the 3x3 conv kernels from the committed rocprofv3
-    PMC passes (tools/gpu_pmc.sh -> tools/pmc_traffic.py), or None."""
+    PMC passes over this model's bench (tools/gpu_r2_final.sh ->
+    tools/pmc_traffic.py), or None."""
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(PMC_TRAFFIC[model]) as f:
             v = json.load(f).get("conv3x3_hbm_bytes_per_launch")
         return None if v is None else round(float(v))
     except (OSError, ValueError):
@@ -96,50 +98,74 @@ def _cpu_threads():
     return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
 
 
+def _ref_model(args):
+    """The oracle model of the benched configuration, same seeded weights as the GPU model."""
+    from oracle import cpu_ref as R
+    from vaeunet_amd.init import seeded_init_
+    if args.model == "vae":
+        from vaeunet_amd import UNetResNet
+        return R.UNetResNetRef(seeded_init_(UNetResNet(3, 1, pretrained=False), 0).state_dict())
+    from vaeunet_amd import UNet
+    return R.UNetRef(seeded_init_(UNet(3, args.classes), 0).state_dict())
+
+
+def _latent_eps(B):
+    """A fixed reparameterisation draw (latent 32) shared by the oracle and the
+    GPU model in the parity leg (unet_resnet.py:191-194 with eps injected)."""
+    return torch.randn(B, 32, generator=torch.Generator().manual_seed(77))
+
+
 def cpu_baseline(args, dev):
     """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py;
     kind "port") timed on this host: the same synthetic batch
     (B x 3 x S x S, rank-0 seed), 1 warmup + K timed full train steps (fwd,
-    CombinedLoss, bwd, clip, AdamW), fp32 (the reference semantics) and CPU
-    autocast bf16 (train.py's amp default on CPU).
+    loss, bwd, clip, AdamW), fp32 (the reference semantics) and CPU autocast
+    bf16 (train.py's amp default on CPU).  --model vae: UNetResNet with
+    CombinedLoss + 1e-3 * KL (free bits 1e-3) and a fixed latent draw.
 
-    The fp32 warmup step's pre-update logits are also the parity reference:
+    The fp32 warmup step's pre-update outputs are also the parity reference:
     the GPU model (fp32 parity mode, same weights, same batch) is compared
     with them (the "Dice parity vs CPU ref" of the metric name)."""
     from oracle import cpu_ref as R
-    from vaeunet_amd import UNet
-    from vaeunet_amd.init import seeded_init_
     threads, affinity = _cpu_threads()
     torch.set_num_threads(threads)
     B = args.cpu_batch
+    vae = args.model == "vae"
     x, t = synthetic(B, args.size, args.classes, 0, "cpu")
+    eps = _latent_eps(B) if vae else None
+
+    def train_step(model, opt):
+        if vae:
+            return R.vae_train_step(model, opt, x, t, eps)
+        return R.train_step(model, opt, x, t)
     legs, parity = {}, None
     for leg in ("fp32", "bf16"):
         if leg == "bf16" and args.cpu_no_bf16:
             continue
-        model = R.UNetRef(seeded_init_(UNet(3, args.classes), 0).state_dict())
+        model = _ref_model(args)
         opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
         ctx = torch.autocast("cpu", dtype=torch.bfloat16) if leg == "bf16" else _Null()
         t0 = time.perf_counter()
         with ctx:
-            ref_logits, ref_loss, _ = R.train_step(model, opt, x, t)  # warmup; pre-update outputs
+            ref_out, ref_loss, _ = train_step(model, opt)  # warmup; pre-update outputs
         warm = time.perf_counter() - t0
         if leg == "fp32":
-            parity = gpu_parity(args, x, t, ref_logits, ref_loss, dev)
+            parity = gpu_parity(args, x, t, ref_out, ref_loss, dev, eps)
         # bounded sample: a slow host gets fewer timed steps (stated in "sample")
         n = args.cpu_steps if warm * args.cpu_steps <= args.cpu_budget_s else max(1, int(args.cpu_budget_s // warm))
         t0 = time.perf_counter()
         with ctx:
             for _ in range(n):
-                R.train_step(model, opt, x, t)
+                train_step(model, opt)
         dt = time.perf_counter() - t0
         legs[leg] = {"value": round(B * n / dt, 4), "steps": n, "s_per_step": round(dt / n, 3)}
     f = legs["fp32"]
+    what = ("UNetResNet(3,1) VAE train steps (fwd+CombinedLoss+1e-3*KL+bwd+clip+AdamW)" if vae else
+            f"UNet(3,{args.classes}) train steps (fwd+CombinedLoss+bwd+clip+AdamW)")
     out = {"value": f["value"], "unit": "images/sec", "cores": threads, "kind": "port",
            "cpu_model": _cpu_model(), "affinity_cores": affinity,
-           "sample": (f"1 warmup + {f['steps']} timed fp32 train steps (fwd+CombinedLoss+bwd+clip+AdamW) of "
-                      f"UNet(3,{args.classes}) on {B}x3x{args.size}x{args.size} (oracle/cpu_ref.py, torch CPU, "
-                      f"{threads} threads)"),
+           "sample": (f"1 warmup + {f['steps']} timed fp32 {what} on {B}x3x{args.size}x{args.size} "
+                      f"(oracle/cpu_ref.py, torch CPU, {threads} threads)"),
            "legs": legs}
     return out, parity
 
@@ -152,43 +178,67 @@ class _Null:
         return False
 
 
-def gpu_parity(args, x, t, ref_logits, ref_loss, dev):
-    """GPU UNet (fp32 parity mode: no autocast) vs the CPU oracle, same weights,
-    same batch: Dice of the argmax class maps, the reference's own dice_score
-    semantics (utils/metrics.py:8-35: both tensors thresholded at 0.5), argmax
-    agreement with the reference margin of EVERY flipped pixel, max |dlogit|
-    and |dloss|."""
-    from vaeunet_amd import UNet
+def gpu_parity(args, x, t, ref_out, ref_loss, dev, eps=None):
+    """GPU model (fp32 parity mode: no autocast) vs the CPU oracle, same weights,
+    same batch (and, for the VAE, the same latent draw): Dice of the class maps
+    (argmax for 2 classes, logit > 0 for 1), the reference's own dice_score
+    semantics (utils/metrics.py:8-35: both tensors thresholded at 0.5), class
+    agreement with the reference margin of EVERY flipped pixel, max |dlogit|,
+    |dloss| (and mu / logvar for the VAE)."""
     from vaeunet_amd.init import seeded_init_
-    from vaeunet_amd.loss import CombinedLoss
+    from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
     from vaeunet_amd.metrics import dice_score
     from oracle import cpu_ref as R
-    model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
-    model.train()
+    vae = args.model == "vae"
+    if vae:
+        from vaeunet_amd import UNetResNet
+        model = seeded_init_(UNetResNet(3, 1, pretrained=False), 0)
+        model.eps_override = eps
+        ref_logits, ref_mu, ref_lv = ref_out
+    else:
+        from vaeunet_amd import UNet
+        model = seeded_init_(UNet(3, args.classes), 0)
+        ref_logits = ref_out
+    model = model.to(dev).to(memory_format=torch.channels_last).train()
     xg = x.to(dev).contiguous(memory_format=torch.channels_last)
     tg = t.to(dev).contiguous(memory_format=torch.channels_last)
+    extra = {}
     with torch.no_grad():
-        lg = model(xg)
-        loss = CombinedLoss()(lg, tg)
+        if vae:
+            lg, mu, lv = model(xg)
+            loss = CombinedLoss()(lg, tg) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+            for k, a, b in (("mu", mu, ref_mu), ("logvar", lv, ref_lv)):
+                extra[f"{k}_max_rel_err"] = float((a.float().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-12))
+        else:
+            lg = model(xg)
+            loss = CombinedLoss()(lg, tg)
         ds_gpu = float(dice_score(lg, ref_logits.float().to(dev).contiguous(memory_format=torch.channels_last)))
     lg = lg.float().cpu()
     ref = ref_logits.float()
     ds_ref = float(R.dice_score(lg.contiguous(), ref.contiguous()))
-    cg, cr = lg.argmax(1), ref.argmax(1)
-    fg, fr = (cg == 1), (cr == 1)
+    if lg.shape[1] == 1:
+        fg, fr = lg[:, 0] > 0, ref[:, 0] > 0
+        flips = fg != fr
+        margins = ref[:, 0].abs()[flips]
+    else:
+        cg, cr = lg.argmax(1), ref.argmax(1)
+        fg, fr = (cg == 1), (cr == 1)
+        flips = cg != cr
+        margins = (ref[:, 0] - ref[:, 1]).abs()[flips]
     den = int(fg.sum() + fr.sum())
     dice = 1.0 if den == 0 else 2.0 * int((fg & fr).sum()) / den
-    flips = cg != cr
-    margins = (ref[:, 0] - ref[:, 1]).abs()[flips]
-    return {"dice_class_map": round(dice, 6), "dice_score_ref_semantics": round(ds_gpu, 7),
-            "dice_score_ref_semantics_cpu": round(ds_ref, 7),
-            "argmax_agree": round(float((~flips).float().mean()), 8), "argmax_flips": int(flips.sum()),
-            "flipped_ref_margins": [float(f"{v:.3e}") for v in margins.tolist()[:32]],
-            "max_flipped_ref_margin": float(margins.max()) if margins.numel() else 0.0,
-            "max_abs_logit_diff": float((lg - ref).abs().max()),
-            "logit_scale": float(ref.abs().max()),
-            "loss_abs_diff": abs(float(loss) - float(ref_loss)),
-            "sample": f"{x.shape[0]}x3x{args.size}x{args.size}, fp32 GPU vs oracle/cpu_ref.py fp32, same weights/input"}
+    out = {"dice_class_map": round(dice, 6), "dice_score_ref_semantics": round(ds_gpu, 7),
+           "dice_score_ref_semantics_cpu": round(ds_ref, 7),
+           "argmax_agree": round(float((~flips).float().mean()), 8), "argmax_flips": int(flips.sum()),
+           "flipped_ref_margins": [float(f"{v:.3e}") for v in margins.tolist()[:32]],
+           "max_flipped_ref_margin": float(margins.max()) if margins.numel() else 0.0,
+           "max_abs_logit_diff": float((lg - ref).abs().max()),
+           "logit_scale": float(ref.abs().max()),
+           "loss_abs_diff": abs(float(loss) - float(ref_loss))}
+    out.update(extra)
+    out["sample"] = (f"{x.shape[0]}x3x{args.size}x{args.size}, fp32 GPU vs oracle/cpu_ref.py fp32, same weights/input"
+                     + (", same latent eps; class = logit > 0" if vae else ""))
+    return out
 
 
 def main():
@@ -213,7 +263,6 @@ def main():
         from vaeunet_amd import UNetResNet
         from vaeunet_amd.loss import kl_with_free_bits
         args.classes = 1
-        args.no_cpu_baseline = True
         model = seeded_init_(UNetResNet(3, 1, pretrained=False), 0).to(dev).to(memory_format=torch.channels_last)
     else:
         model = seeded_init_(UNet(3, args.classes), 0).to(dev).to(memory_format=torch.channels_last)
@@ -304,8 +353,8 @@ def main():
         n = sum(v[2] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
         achieved = fl / (tm * 1e-3) / 1e12 if tm > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(),
-                "traffic_unit": "HBM bytes per launch (profiles/pmc_traffic.json)",
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(args.model),
+                "traffic_unit": f"HBM bytes per launch ({os.path.relpath(PMC_TRAFFIC[args.model], ROOT)})",
                 "kernel": "gemm_fwd_kernel+gemm_wgrad_kernel (3x3 conv fwd/dgrad/wgrad, inc.0 excluded)",
                 "launches_per_step": n // 2,
                 "per_kind": {k: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1),

@@ -119,7 +119,11 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     tiles) with 128x64 4-wave v2 tiles instead of split-K / v3;
  *   VU_TUNE_V5: 1 (default) serves the short-K 1x1 / ConvTranspose GEMMs
  *     with the persistent v5 kernel (gemm_fwd5.hip), 0 routes them to v2,
- *     k >= 2 caps its grid at k blocks (tests: several tiles per block). */
+ *     k >= 2 caps its grid at k blocks (tests: several tiles per block);
+ *   VU_TUNE_V6: 1 (default) serves 64 -> 64 3x3 convs (and their input
+ *     gradients) with >= 2 tiles of 16x32 pixels per CU with the
+ *     resident-weight persistent kernel (gemm_fwd6.hip), 0 routes them to
+ *     v3/v4, k >= 2 serves any grid with the grid capped at k (tests). */
 #define VU_TUNE_V4_MIN_BLOCKS 0
 #define VU_TUNE_FP8_GRID 4
 #define VU_TUNE_STREAM 5
@@ -127,6 +131,7 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 #define VU_TUNE_V4_SPLIT_CHUNKS 8
 #define VU_TUNE_V2_SMALL 9
 #define VU_TUNE_V5 10
+#define VU_TUNE_V6 11
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */

@@ -302,3 +302,31 @@ def train_step(model, opt, x, target, clip=1.0):
     total = clip_grad_norm(list(model.p.values()), clip)
     opt.step()
     return logits.detach(), loss.detach(), total
+
+
+class UNetResNetRef:
+    """Parameter container mirroring the reference UNetResNet's state_dict
+    (unet_resnet.py:103-279); `eps` fixes reparameterize's draw (:191-194)."""
+
+    def __init__(self, state, latent_injection="all"):
+        self.p = {k: v.clone().float().requires_grad_(True) for k, v in state.items()
+                  if "running" not in k and "num_batches" not in k}
+        self.bufs = {k: v.clone() for k, v in state.items()
+                     if "running" in k or "num_batches" in k}
+        self.latent_injection = latent_injection
+
+    def forward(self, x, eps=None, train=True):
+        return unet_resnet_forward(x, self.p, self.bufs, eps, train, self.latent_injection)
+
+
+def vae_train_step(model, opt, x, target, eps, beta=1e-3, free_bits=1e-3, clip=1.0):
+    """train.py:381-411 for the resnet path: CombinedLoss + beta * KL with free
+    bits (utils/loss.py:148-170), clip, AdamW."""
+    logits, mu, logvar = model.forward(x, eps, True)
+    loss = combined_loss(logits, target) + beta * kl_with_free_bits(mu, logvar, free_bits)
+    for q in model.p.values():
+        q.grad = None
+    loss.backward()
+    total = clip_grad_norm(list(model.p.values()), clip)
+    opt.step()
+    return (logits.detach(), mu.detach(), logvar.detach()), loss.detach(), total

@@ -386,6 +386,47 @@ def test_gemm_v5_fwd_stats_accumulate(case):
         _tune((TUNE_V5, 1))
 
 
+TUNE_V6 = 11
+V6_CASES = [
+    # (N, H, W, grid cap): resident-weight 64 -> 64 3x3 kernel (gemm_fwd6.hip),
+    # tiles of 16x32 pixels walked persistently (cap < tiles: several per block)
+    (1, 16, 32, 2),     # one tile, image border on every side
+    (2, 32, 64, 3),     # 8 tiles over 3 blocks (uneven walk)
+    (1, 48, 96, 5),     # 9 tiles
+    (3, 64, 32, 256),   # 12 tiles, one per block
+]
+
+
+@pytest.mark.parametrize("case", V6_CASES)
+def test_conv3x3_c64_resident(case):
+    """64 -> 64 3x3 conv forward (bias + BN partials of 64-pixel wave tiles)
+    and input gradient on the v6 kernel vs torch fp32 of the bf16-rounded
+    operands (unet_parts.py:43 and its backward)."""
+    K, E = _k()
+    N, H, W, cap = case
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(N, 64, H, W, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(64, 64, 3, 3, generator=g) / 24.0
+    b = torch.randn(64, generator=g)
+    wq = w.to(torch.bfloat16).float()
+    d = _code("bf16")
+    xs = _act(x, "bf16")
+    wf = E.w3x3_fwd(w.to(DEV), d)
+    _tune((TUNE_V6, cap))
+    try:
+        out = K.empty_act(N, 64, H, W, torch.bfloat16, DEV)
+        assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wf, 64, out, K.gather3x3)) == 64
+        st = K.gemm_fwd(K.gather3x3([xs]), wf, 64, out, d, bias=b.to(DEV), stats=True)
+        _close(out, F.conv2d(x, wq, b, padding=1), "bf16", what="v6 fwd")
+        _stats_check(st, out.float().cpu())
+        dy = torch.randn(N, 64, H, W, generator=g).to(torch.bfloat16).float()
+        dx = K.empty_act(N, 64, H, W, torch.bfloat16, DEV)
+        K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), 64, dx, d, kind="dgrad")
+        _close(dx, torch.nn.grad.conv2d_input((N, 64, H, W), wq, dy, padding=1), "bf16", what="v6 dgrad")
+    finally:
+        _tune((TUNE_V6, 1))
+
+
 @pytest.mark.parametrize("ci,co,h,cap", [(512, 256, 32, 0), (256, 128, 64, 6), (1024, 512, 32, 0)])
 def test_gemm_v5_convT(ci, co, h, cap):
     """ConvTranspose2d 2x2/s2 of the deeper decoder levels on v5: forward with

@@ -44,6 +44,13 @@ def _shape(name, args):
             M = w.p.N * w.p.H * w.p.W
             b = M * (w.p.C + w.q.C) * 2
             return f"wgrad R{w.q.R} {w.q.H}x{w.q.W} ni{w.ni} nj{w.nj} s{w.splits}", b, 2 * M * w.ni * w.nj
+        # BatchNorm streams: (x, xs, y, ys, P, C, ...) -> bytes per launch (bf16/fp32 by dtype)
+        nbytes = {"vu_bn_apply": 2, "vu_bn_bwd_reduce": 2, "vu_bn_bwd_apply": 3}
+        if name in nbytes:
+            iv = [int(getattr(a, "value", a) or 0) for a in (args[4], args[5], args[-2])]
+            P, Cc, dt = iv
+            esz = 2 if dt == _lib.BF16 else 4
+            return f"P{P} C{Cc}", nbytes[name] * P * Cc * esz, 0
     except Exception:  # noqa: BLE001
         pass
     return "", 0, 0

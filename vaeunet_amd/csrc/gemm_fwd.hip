@@ -337,6 +337,8 @@ int gemm_stream_bm(const VuGemmFwd& p, int dtype);     // gemm_stream.hip (short
 int gemm_stream_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd5.hip (persistent short-K GEMM)
 int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd6.hip (64 -> 64 3x3, resident weights)
+int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st);
 
 static bool use_v2(int dtype) {
   static int mode = -1;
@@ -373,7 +375,9 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
     if (bm) return bm;
   }
   if (use_v4(dtype)) {
-    int bm = gemm_fwd_v4_bm(*args, dtype);
+    int bm = gemm_fwd_v6_bm(*args, dtype);
+    if (bm) return bm;
+    bm = gemm_fwd_v4_bm(*args, dtype);
     if (bm) return bm;
   }
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return 128;
@@ -389,6 +393,7 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
 
 extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype) && (conv_image_bm(*args, dtype) || gemm_stream_bm(*args, dtype))) return 0;
+  if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return 0;
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_workspace(*args, dtype);
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_workspace(*args, dtype);
   return 0;
@@ -404,6 +409,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return conv_image_launch(*args, st);
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
+  if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return gemm_fwd_v6_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);

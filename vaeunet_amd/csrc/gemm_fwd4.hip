@@ -672,6 +672,7 @@ int conv_fp8_tune(int key, int value);     // conv_fp8.hip
 int gemm_stream_tune(int key, int value);  // gemm_stream.hip
 int gemm_fwd_v2_tune(int key, int value);  // gemm_fwd2.hip
 int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
+int gemm_fwd_v6_tune(int key, int value);  // gemm_fwd6.hip
 
 extern "C" int vu_gemm_set_tuning(int key, int value) {
   if (key == VU_TUNE_V4_MIN_BLOCKS) {
@@ -687,7 +688,7 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
     return 0;
   }
   if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0 || gemm_fwd_v2_tune(key, value) == 0 ||
-      gemm_fwd_v5_tune(key, value) == 0)
+      gemm_fwd_v5_tune(key, value) == 0 || gemm_fwd_v6_tune(key, value) == 0)
     return 0;
   return (int)hipErrorInvalidValue;
 }

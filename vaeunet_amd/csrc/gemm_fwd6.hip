@@ -1,0 +1,317 @@
+// 3x3 / stride-1 / pad-1 convolution with 64 input and 64 output channels
+// ("v6", bf16): the second conv of the 512^2-level DoubleConvs (inc, up4:
+// unet_parts.py:43) and the input gradient of every 64 -> 64 conv (the same
+// shape with flipped weights).
+//
+// Why a separate kernel: with K = 576 a tile of these layers is 9-18 K-steps
+// long, so the halo / ping-pong kernels (one tile per block) spend a large
+// part of every tile in its prologue (first halo), its weight stream and its
+// LDS-staged epilogue: 740-820 TFLOP/s in the bench step against
+// 1,100-1,500 on the deeper layers.  Here the whole weight matrix (64 x 576
+// bf16 = 72 KiB) is loaded into LDS ONCE per block and stays resident, and a
+// persistent block walks its tiles as one stream of (tile, 32-channel chunk)
+// groups:
+//
+//   * tile = 16 x 32 pixels x 64 channels; wave w owns image rows 2w, 2w+1
+//     (4 pixel fragments x 4 channel fragments of v_mfma_f32_16x16x32_bf16,
+//     64 accumulator registers);
+//   * the only DMA stream is the halo: while a group computes from one
+//     18 x 34-pixel chunk buffer, the next group's chunk (the second chunk of
+//     this tile or the first of the next tile) lands in the other one
+//     (global_load_lds_dwordx4), so the pipeline never drains at a tile seam;
+//   * MFMA operands are (weights, pixels) with the weight rows read in a
+//     permuted order, so a lane's accumulators hold 16 consecutive output
+//     channels of one pixel, stored straight from registers (no LDS staging,
+//     no barrier; 64 contiguous bytes per pixel and store), with the BatchNorm partial
+//     statistics of each wave's 64 pixels from DPP row sums (same contract as
+//     the other kernels: per-tile sum + centered M2 of the rounded values);
+//   * LDS images are conflict-free for every fragment read: weight rows XOR
+//     their 16-byte pieces with wswz(row); halo pixel P keeps its piece k at
+//     position (k + 2 * ((P >> 2) & 1)) & 3, which spreads the 16 lanes of
+//     every ds_read_b128 lane group over distinct banks for any tap shift.
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+static __device__ __attribute__((aligned(16))) uint32_t v6_zero_page[16];
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int TH = 16, TW = 32;
+constexpr int HWD = TW + 2;                  // halo row (pixels)
+constexpr int HP = (TH + 2) * HWD;           // 612 halo pixels
+constexpr int HPIECES = HP * 4;              // 16-byte pieces of one 32-channel chunk
+constexpr int NHR = (HPIECES + 511) / 512;   // DMA rounds per chunk (5)
+constexpr int HBUF = NHR * 512 * 16;         // chunk buffer, padded to whole DMA rounds
+constexpr int WROW = 576 * 2;                // one output channel's weights (bytes)
+constexpr int WBYTES = 64 * WROW;            // 72 KiB, resident
+constexpr int WROUNDS = WBYTES / 16 / 512;   // 9
+constexpr int LDS_BYTES = WBYTES + 2 * HBUF;
+static_assert(LDS_BYTES <= 163840, "LDS");
+static_assert(WROUNDS * 512 * 16 == WBYTES, "weight DMA rounds");
+
+template <int N>
+VU_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// a workgroup barrier that neither drains the memory counters nor lets the
+// compiler move LDS reads, DMA issues or MFMAs across it
+VU_DEV void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// weight-row piece swizzle: with the permuted fragment rows below (lane row
+// rr of fragment j = channel 16*(rr>>2) + 4j + (rr&3)) every ds_read_b128
+// lane group touches 16 distinct 4-bank groups (checked for all j, tap, c)
+VU_DEV int wswz(int n) { return (n + (n >> 2)) & 7; }
+
+template <int R>
+VU_DEV float ror_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xf, 0xf, false));
+}
+VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
+
+template <bool STATS>
+__global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  char* const wl = smem;
+  char* const hl = smem + WBYTES;
+
+  const VuGather& g = p.a;
+  const int H = g.H, W = g.W;
+  const int txn = W / TW, per_img = txn * (H / TH);
+  const int T = g.N * per_img;
+  const int G = gridDim.x;  // <= T (host)
+  const int lb = xcd_remap(blockIdx.x, G);
+  const int ngroups = 2 * ((T - lb + G - 1) / G);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l16 = lane & 15, kg = lane >> 4;
+  const bf16_t* const src = reinterpret_cast<const bf16_t*>(g.src[0]);
+  const int64_t st = g.stride[0];
+  const void* const zp = (const void*)v6_zero_page;
+  // bias of this lane's channels, loaded up front: a load in the epilogue
+  // would wait for the in-flight halo DMA (vmcnt is in order)
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    bv[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 16 * kg + 4 * j) : f32x4{0, 0, 0, 0};
+
+  // ---- resident weights: row n (output channel) = 576 bf16; 16-byte piece
+  //      pc of row n lives at piece pc ^ wswz(n) ----
+  {
+    const bf16_t* bm = reinterpret_cast<const bf16_t*>(p.b);
+#pragma unroll
+    for (int i = 0; i < WROUNDS; ++i) {
+      const int s = i * 512 + tid;
+      const int n = s / 72, pc = s - (s / 72) * 72;
+      const void* gp = (const void*)(bm + (int64_t)n * p.ldb + (pc ^ wswz(n)) * 8);
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(wl + (i * 512 + wid * 64) * 16), 16, 0, 0);
+    }
+  }
+  // ---- halo of (tile t, chunk c) into buffer b ----
+  auto halo = [&](int t, int c, int b) {
+    const int img = t / per_img, r = t - (t / per_img) * per_img;
+    const int ty = r / txn, tx = r - (r / txn) * txn;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    const bf16_t* s0 = src + (int64_t)img * H * W * st + c * 32;
+    char* dst = hl + b * HBUF;
+#pragma unroll
+    for (int i = 0; i < NHR; ++i) {
+      if (i * 512 + wid * 64 >= HPIECES) continue;  // wave-uniform
+      const int s = i * 512 + tid;
+      const int P = s >> 2, pos = s & 3;
+      const int hy = P / HWD, hx = P - (P / HWD) * HWD;
+      const int y = y0 + hy, x = x0 + hx;
+      const int k = (pos - ((P >> 1) & 2)) & 3;  // the global piece stored at position pos
+      const bool ok = s < HPIECES && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const void* gp = ok ? (const void*)(s0 + (int64_t)(y * W + x) * st + k * 8) : zp;
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(dst + (i * 512 + wid * 64) * 16), 16, 0, 0);
+    }
+  };
+
+  halo(lb, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  raw_barrier();
+
+  // B fragment j, lane row l16 = output channel n_j = 16*(l16>>2) + 4j + (l16&3),
+  // so that a lane's accumulators hold 16 consecutive channels (16*kg ..):
+  // K piece (tap, c, kg) of row n_j sits at piece tap*8 + ((c*4 + kg) ^ wswz(n_j))
+  int boff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = 16 * (l16 >> 2) + 4 * j + (l16 & 3);
+    boff[j] = n * WROW + ((kg ^ wswz(n)) << 4);
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+
+  int t = lb, c = 0, b = 0;
+  for (int gi = 0; gi < ngroups; ++gi) {
+    // the other buffer was released by every wave at the previous barrier
+    if (gi + 1 < ngroups) halo(c == 0 ? t : t + G, c ^ 1, b ^ 1);
+    const char* hb = hl + b * HBUF;
+    const int cx = c << 6;  // (c*4) XORed into the piece index: 4 pieces = 64 bytes
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ty = tap / 3, tx = tap - (tap / 3) * 3;
+      u32x4 bf[4], af[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(wl + (boff[j] ^ cx) + tap * 128);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int P = (2 * wid + (i >> 1) + ty) * HWD + (i & 1) * 16 + tx + l16;
+        af[i] = *reinterpret_cast<const u32x4*>(hb + P * 64 + (((kg + ((P >> 1) & 2)) & 3) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+                                                              __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
+    }
+    if (c == 1) {
+      // ---- epilogue of tile t from registers: acc[i][j][r] = pixel fragment
+      //      i (row 2*wid + i/2, column (i&1)*16 + l16), channel 16kg + 4j + r ----
+      const int img = t / per_img, r0 = t - (t / per_img) * per_img;
+      const int ty = r0 / txn, tx = r0 - (r0 / txn) * txn;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] += bv[j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r]);
+      if (STATS) {
+        // per-wave (sum, centered M2) of its 64 pixels; lane (kg, l16) keeps
+        // channel 16*kg + l16 = lane: one store per statistic
+        float ms = 0.f, mq = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float sv = (acc[0][j][r] + acc[1][j][r]) + (acc[2][j][r] + acc[3][j][r]);
+            sv = row16_sum(sv);
+            const float mean = sv * (1.f / 64);
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float d = acc[i][j][r] - mean;
+              q += d * d;
+            }
+            q = row16_sum(q);
+            if (l16 == j * 4 + r) {
+              ms = sv;
+              mq = q;
+            }
+          }
+        const int64_t so = (int64_t)(t * 8 + wid) * p.ncol + lane;
+        p.stat_sum[so] = ms;
+        p.stat_m2[so] = mq;
+      }
+      // stores: a lane holds channels 16kg .. 16kg+15 of its pixel (two 16-byte
+      // pieces); a permlane16 + permlane32 swap regroups them so that store h
+      // of lane kg writes channels 32h + 8kg .. +7: 64 contiguous bytes per
+      // pixel and instruction
+      bf16_t* const obase = reinterpret_cast<bf16_t*>(p.out) + p.out_coff + 8 * kg +
+                            (((int64_t)img * H + ty * TH + 2 * wid) * W + tx * TW + l16) * p.out_stride;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        u32x4 cv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 a = acc[i][2 * h], e = acc[i][2 * h + 1];
+          cv[h] = u32x4{(uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16), (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16),
+                        (uint32_t)f2bf(e[0]) | ((uint32_t)f2bf(e[1]) << 16), (uint32_t)f2bf(e[2]) | ((uint32_t)f2bf(e[3]) << 16)};
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const auto r1 = __builtin_amdgcn_permlane16_swap(cv[0][w], cv[1][w], false, false);
+          const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
+          cv[0][w] = r2[0];
+          cv[1][w] = r2[1];
+        }
+        bf16_t* o = obase + ((i >> 1) * (int64_t)W + (i & 1) * 16) * p.out_stride;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          *reinterpret_cast<u32x4*>(o + 32 * h) = cv[h];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+      // the next group's halo was issued before this tile's stores
+      if (STATS) wait_vm<10>(); else wait_vm<8>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();
+    b ^= 1;
+    if (c == 1) t += G;
+    c ^= 1;
+  }
+}
+
+int cu_count6() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 2 tiles per CU), k >= 2 on with the grid capped at k
+
+}  // namespace
+
+// Statistics row tile (64) when v6 serves this problem, else 0.
+int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype) {
+  if (g_v6 == 0 || dtype != VU_BF16 || p.out_mode != 0 || p.accumulate) return 0;
+  const VuGather& g = p.a;
+  if (g.R != 3 || g.S != 3 || g.sy != 1 || g.sx != 1 || g.dy != 1 || g.dx != 1 || g.oy != -1 || g.ox != -1 ||
+      g.Hs != g.H || g.Ws != g.W)
+    return 0;
+  if (g.nsrc != 1 || g.C != 64 || g.cend[0] != 64 || p.ncol != 64) return 0;
+  if (g.H % TH != 0 || g.W % TW != 0) return 0;
+  if (g.stride[0] % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0 || p.ldb < 576)
+    return 0;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  if (M >= ((int64_t)1 << 31)) return 0;
+  const int64_t T = M / (TH * TW);
+  if (g_v6 == 1 && T < 2 * (int64_t)cu_count6()) return 0;  // needs a tile stream per block
+  return 64;
+}
+
+int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
+  const int64_t T = (int64_t)p.a.N * p.a.H * p.a.W / (TH * TW);
+  int64_t grid = T < cu_count6() ? T : cu_count6();
+  if (g_v6 >= 2 && grid > g_v6) grid = g_v6;
+if (p.stat_sum)
+    hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
+  return (int)hipGetLastError();
+}
+
+int gemm_fwd_v6_tune(int key, int value) {
+  if (key == VU_TUNE_V6) {
+    g_v6 = value < 0 ? 0 : value;
+    return 0;
+  }
+  return -1;
+}
