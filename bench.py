@@ -35,7 +35,7 @@ PMC_TRAFFIC = {"unet": os.path.join(ROOT, "profiles", "pmc_traffic.json"),
 
 def pmc_traffic(model):
     """HBM bytes per launch of the 3x3 conv kernels from the committed rocprofv3
-    PMC passes over this model's bench (tools/gpu_r2_final.sh ->
+    PMC passes over this model's bench (tools/gpu_evidence.sh ->
     tools/pmc_traffic.py), or None."""
     try:
         with open(PMC_TRAFFIC[model]) as f:

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round evidence on one GPU box: both bench lines (UNet = the metric, with
+# cpu_baseline + parity + roofline; VAE-U-Net = config 3), rocprofv3 kernel
+# stats of each bench, and the HBM-traffic PMC passes of each (FETCH_SIZE and
+# WRITE_SIZE in separate runs: MI355X_MICROARCH.md HBM section).
+# usage: bash tools/gpu_evidence.sh <tag>   -> gpurun_out/<tag>/
+set -o pipefail
+export TMPDIR=/tmp
+tag=${1:-evidence}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$tag
+mkdir -p $O
+cd $R
+timeout -k 10 700 python -u bench.py > $O/bench_unet.log 2>&1 || { echo BENCH_FAIL; tail -20 $O/bench_unet.log; exit 1; }
+timeout -k 10 700 python -u bench.py --model vae > $O/bench_vae.log 2>&1 || { echo VAE_FAIL; tail -20 $O/bench_vae.log; exit 1; }
+cd /tmp
+for m in unet vae; do
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$m -o p -- python -u $R/bench.py --model $m --steps 10 --warmup 3 --no-cpu-baseline --no-roofline > $O/prof_$m.log 2>&1 || { echo PROF_FAIL $m; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$m -o f -- python -u $R/bench.py --model $m --steps 1 --warmup 1 --no-cpu-baseline --no-roofline > $O/pmc_fetch_$m.log 2>&1 || { echo FETCH_FAIL $m; exit 1; }
+  timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$m -o w -- python -u $R/bench.py --model $m --steps 1 --warmup 1 --no-cpu-baseline --no-roofline > $O/pmc_write_$m.log 2>&1 || { echo WRITE_FAIL $m; exit 1; }
+done
+cd $R
+python tools/pmc_traffic.py $O/pmc_fetch_unet $O/pmc_write_unet $O/pmc_traffic.json &&
+python tools/pmc_traffic.py $O/pmc_fetch_vae $O/pmc_write_vae $O/pmc_traffic_vae.json &&
+for m in unet vae; do find $O/prof_$m -name "*kernel_stats.csv" -exec cp {} $O/${m}_kernel_stats.csv \; ; done &&
+rm -rf $O/pmc_fetch_* $O/pmc_write_* &&
+tail -1 $O/bench_unet.log | cut -c1-400 && tail -1 $O/bench_vae.log | cut -c1-400

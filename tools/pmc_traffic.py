@@ -2,7 +2,7 @@
 (MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KB; on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced stream -> x2; WRITE_SIZE
 is exact for 16-byte stores).  Reads the counter_collection CSVs of two
-separate passes (`--pmc FETCH_SIZE`, `--pmc WRITE_SIZE`, tools/gpu_pmc.sh) and
+separate passes (`--pmc FETCH_SIZE`, `--pmc WRITE_SIZE`, tools/gpu_evidence.sh) and
 writes profiles/pmc_traffic.json, which bench.py reports as roofline.traffic.
 
 usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> [out.json]

@@ -189,11 +189,7 @@ struct ChanMap {
 // Streaming kernels issue UNR independent 16-byte rows per thread before
 // using any of them (a grid-stride loop with one load in flight per thread
 // leaves HBM at ~60% of its bandwidth).
-#ifndef VU_RED_UNR
-#define VU_RED_UNR 4
-#endif
 constexpr int UNR = 4;
-constexpr int RUNR = VU_RED_UNR;  // rows in flight per thread in the reductions
 
 template <typename T>
 __global__ void bn_apply_kernel(const T* x, int64_t xs, T* y, int64_t ys, int64_t P, int C,
@@ -228,10 +224,7 @@ __global__ void bn_apply_kernel(const T* x, int64_t xs, T* y, int64_t ys, int64_
 // ---- per-channel partial reductions ----
 // MODE 0: s0 = sum x (over an optional pixel window)
 // MODE 1: s0 = sum dz, s1 = sum dz*xhat; dz = dy*(z>0 if relu), xhat=(x-mean)*invstd
-#ifndef VU_RED_MAXBLK
-#define VU_RED_MAXBLK 1024
-#endif
-constexpr int RED_MAXBLK = VU_RED_MAXBLK;
+constexpr int RED_MAXBLK = 1024;
 
 struct RedArgs {
   const void* a; int64_t as;   // x (mode 0) or dy (mode 1)
@@ -263,11 +256,11 @@ __global__ void chan_partial_kernel(RedArgs r) {
       sc[i] = r.scale[c + i]; sf[i] = r.shift[c + i]; mu[i] = r.mean[c + i]; is[i] = r.invstd[c + i];
     }
   }
-  const int64_t step = (int64_t)gridDim.x * cm.R * RUNR;
-  for (int64_t p0 = (int64_t)blockIdx.x * cm.R * RUNR + cm.row; p0 < r.P; p0 += step) {
-    Vec8<T> va[RUNR], vb[RUNR];
+  const int64_t step = (int64_t)gridDim.x * cm.R * UNR;
+  for (int64_t p0 = (int64_t)blockIdx.x * cm.R * UNR + cm.row; p0 < r.P; p0 += step) {
+    Vec8<T> va[UNR], vb[UNR];
 #pragma unroll
-    for (int u = 0; u < RUNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       const int64_t p = p0 + (int64_t)u * cm.R;
       if (p < r.P) {
         va[u].load(reinterpret_cast<const T*>(r.a) + (MODE == 0 ? win_pix(r, p) : p) * r.as + c);
@@ -275,7 +268,7 @@ __global__ void chan_partial_kernel(RedArgs r) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < RUNR; ++u) {
+    for (int u = 0; u < UNR; ++u) {
       if (p0 + (int64_t)u * cm.R >= r.P) continue;
       if (MODE == 0) {
 #pragma unroll
