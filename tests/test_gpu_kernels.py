@@ -427,6 +427,35 @@ def test_conv3x3_c64_resident(case):
         _tune((TUNE_V6, 1))
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 96, 160), (64, 13, 13)])
+def test_conv_stem_7x7s2(N, H, W):
+    """ResNet34 stem (7x7, stride 2, pad 3, 8 packed channels -> 64) on the
+    stem kernel (conv_stem.hip): bias + BN partials vs torch fp32 of the
+    bf16-rounded operands; odd sizes exercise every border tap."""
+    K, E = _k()
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(N, 8, H, W, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(64, 8, 7, 7, generator=g) / 20.0
+    b = torch.randn(64, generator=g)
+    wq = w.to(torch.bfloat16).float()
+    d = _code("bf16")
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    if (N * Ho * Wo) % 64:
+        pytest.skip("whole 64-pixel tiles only")
+    xs = _act(x, "bf16")
+    wf = E.w3x3_fwd(w.to(DEV), d)
+    out = K.empty_act(N, 64, Ho, Wo, torch.bfloat16, DEV)
+    gth = K.gather([xs], N, Ho, Wo, R=7, S=7, sy=2, sx=2, oy=-3, ox=-3)
+    import ctypes as C
+    from vaeunet_amd import _lib
+    a = _lib.VuGemmFwd()
+    a.a, a.b, a.ldb, a.ncol, a.out, a.out_stride, a.out_mode = gth, wf.data_ptr(), wf.shape[-1], 64, out.data_ptr(), K.pstride(out), 0
+    assert K.query("vu_gemm_fwd_row_tile", C.byref(a), 1) == 64
+    st = K.gemm_fwd(gth, wf, 64, out, d, bias=b.to(DEV), stats=True)
+    _close(out, F.conv2d(x, wq, b, stride=2, padding=3), "bf16", what="stem fwd")
+    _stats_check(st, out.float().cpu())
+
+
 @pytest.mark.parametrize("ci,co,h,cap", [(512, 256, 32, 0), (256, 128, 64, 6), (1024, 512, 32, 0)])
 def test_gemm_v5_convT(ci, co, h, cap):
     """ConvTranspose2d 2x2/s2 of the deeper decoder levels on v5: forward with

@@ -332,6 +332,8 @@ int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v4_launch(const VuGemmFwd& p, hipStream_t st);
 int64_t gemm_fwd_v4_workspace(const VuGemmFwd& p, int dtype);
 int conv_image_bm(const VuGemmFwd& p, int dtype);      // conv_image.hip (3-channel image conv)
+int conv_stem_bm(const VuGemmFwd& p, int dtype);       // conv_stem.hip (ResNet34 7x7/s2 stem)
+int conv_stem_launch(const VuGemmFwd& p, hipStream_t st);
 int conv_image_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_stream_bm(const VuGemmFwd& p, int dtype);     // gemm_stream.hip (short-K 1x1 streams)
 int gemm_stream_launch(const VuGemmFwd& p, hipStream_t st);
@@ -371,6 +373,8 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype)) {
     int bm = conv_image_bm(*args, dtype);
     if (bm) return bm;
+    bm = conv_stem_bm(*args, dtype);
+    if (bm) return bm;
     bm = gemm_stream_bm(*args, dtype);
     if (bm) return bm;
   }
@@ -392,7 +396,8 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
 }
 
 extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype) {
-  if (use_v2(dtype) && (conv_image_bm(*args, dtype) || gemm_stream_bm(*args, dtype))) return 0;
+  if (use_v2(dtype) && (conv_image_bm(*args, dtype) || conv_stem_bm(*args, dtype) || gemm_stream_bm(*args, dtype)))
+    return 0;
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return 0;
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_workspace(*args, dtype);
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_workspace(*args, dtype);
@@ -408,6 +413,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if ((args->ldb % epc) != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return conv_image_launch(*args, st);
+  if (use_v2(dtype) && conv_stem_bm(*args, dtype)) return conv_stem_launch(*args, st);
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return gemm_fwd_v6_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
