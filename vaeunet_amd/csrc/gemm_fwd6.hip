@@ -156,6 +156,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
 
+  // the previous tile's packed output, stored one piece per tap during the
+  // next group's MFMAs (a burst of stores at the group end idled the MFMA pipe)
+  u32x4 pend[8];
+  bf16_t* pdst = nullptr;
+  bool have_pend = false;
+  auto store_pend = [&](int q) {  // piece q = 2 * fragment + half
+    bf16_t* o = pdst + ((q >> 2) * (int64_t)W + ((q >> 1) & 1) * 16) * p.out_stride + 32 * (q & 1);
+    *reinterpret_cast<u32x4*>(o) = pend[q];
+  };
+
   int t = lb, c = 0, b = 0;
   for (int gi = 0; gi < ngroups; ++gi) {
     // the other buffer was released by every wave at the previous barrier
@@ -165,6 +175,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ty = tap / 3, tx = tap - (tap / 3) * 3;
+      if (tap < 8 && have_pend) store_pend(tap);
       u32x4 bf[4], af[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(wl + (boff[j] ^ cx) + tap * 128);
@@ -225,9 +236,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
       // stores: a lane holds channels 16kg .. 16kg+15 of its pixel (two 16-byte
       // pieces); a permlane16 + permlane32 swap regroups them so that store h
       // of lane kg writes channels 32h + 8kg .. +7: 64 contiguous bytes per
-      // pixel and instruction
-      bf16_t* const obase = reinterpret_cast<bf16_t*>(p.out) + p.out_coff + 8 * kg +
-                            (((int64_t)img * H + ty * TH + 2 * wid) * W + tx * TW + l16) * p.out_stride;
+      // pixel and instruction.  Issued during the next group (store_pend).
+      pdst = reinterpret_cast<bf16_t*>(p.out) + p.out_coff + 8 * kg +
+             (((int64_t)img * H + ty * TH + 2 * wid) * W + tx * TW + l16) * p.out_stride;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         u32x4 cv[2];
@@ -244,25 +255,33 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
           cv[0][w] = r2[0];
           cv[1][w] = r2[1];
         }
-        bf16_t* o = obase + ((i >> 1) * (int64_t)W + (i & 1) * 16) * p.out_stride;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          *reinterpret_cast<u32x4*>(o + 32 * h) = cv[h];
+        pend[2 * i] = cv[0];
+        pend[2 * i + 1] = cv[1];
       }
+      have_pend = true;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-      // the next group's halo was issued before this tile's stores
-      if (STATS) wait_vm<10>(); else wait_vm<8>();
+      // the next group's halo was issued before this tile's statistics stores
+      if (STATS) wait_vm<2>(); else wait_vm<0>();
     } else {
-      wait_vm<0>();
+      // the next group's halo was issued before the previous tile's 8 stores
+      if (have_pend) {
+        have_pend = false;
+        wait_vm<8>();
+      } else {
+        wait_vm<0>();
+      }
     }
     raw_barrier();
     b ^= 1;
     if (c == 1) t += G;
     c ^= 1;
   }
+  if (have_pend)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) store_pend(q);
 }
 
 int cu_count6() {
