@@ -286,18 +286,24 @@ def bn_coef(bn, st, C_):
     return K.bn_eval(C_, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
 
 
-def bn_bwd(dy, x, coef, bn, relu, M, dx=None):
-    """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
-    batch statistics; eval mode (running statistics, constants) gives
-    dx = gamma*invstd*dz and the same dgamma/dbeta sums."""
+def bn_grad_sinks(bn):
     gw, accw = grad_sink(bn.weight)
     gb, accb = grad_sink(bn.bias)
     if gw is not None and gb is not None and accw != accb:
         raise RuntimeError("inconsistent BatchNorm grad state")
+    return gw, gb, accw or accb
+
+
+def bn_bwd(dy, x, coef, bn, relu, M, dx=None, k=None):
+    """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
+    batch statistics; eval mode (running statistics, constants) gives
+    dx = gamma*invstd*dz and the same dgamma/dbeta sums.  k: coefficients
+    (and dgamma/dbeta) already reduced by the producer of dy."""
+    gw, gb, acc = (None, None, False) if k is not None else bn_grad_sinks(bn)
     if dx is None:
         dx = torch.empty_like(x)
-    K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, accw or accb, dx, K.dcode(x.dtype),
-                  train=bn.training)
+    K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
+                  train=bn.training, k=k)
     return dx
 
 
@@ -305,25 +311,29 @@ def bn_bwd(dy, x, coef, bn, relu, M, dx=None):
 # DoubleConv  (unet_parts.py:32-49; DecoderBlock conv1/conv2 unet_resnet.py:59-69)
 #   conv3x3(no bias) -> BN -> ReLU -> conv3x3(no bias) -> BN -> ReLU
 # ----------------------------------------------------------------------------
-def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None):
+def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
+    """defer: leave BN + ReLU unapplied (returns a = None) when the consumer
+    is a MaxPool2d that applies it in the same pass (down_fwd)."""
     N, _, H, W = srcs[0].shape
     co = conv.out_channels
     y = M.act(N, co, H, W)
     st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad), co, y, M.d,
                     stats=bn.training)
     coef = bn_coef(bn, st, co)
+    if defer and K.pool_fusable(y):
+        return None, (y, coef)
     a = M.act(N, co, H, W)
     K.bn_apply(y, a, coef, True, M.d)
     return a, (y, coef)
 
 
 def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False,
-                     cin_pad=None):
+                     cin_pad=None, k=None):
     """cin_pad: compute the input gradient for cin_pad channels (zero weight
     rows past conv.in_channels) so that its column count stays a tile
     multiple; the caller reads the real channels only."""
     y, coef = saved
-    dy = bn_bwd(da, y, coef, bn, True, M)
+    dy = bn_bwd(da, y, coef, bn, True, M, k=k)
     wgrad3x3(dy, srcs, conv.weight, M, cvalid)
     M.notify([conv.weight, bn.weight, bn.bias])
     if not need_dsrc:
@@ -339,35 +349,65 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     return dsrc
 
 
-def double_conv_fwd(M, seq, srcs, cin_pad=None):
+def double_conv_fwd(M, seq, srcs, cin_pad=None, defer=False):
+    """defer: the output feeds a Down (down_fwd applies BN2 + ReLU fused with
+    its max-pool); a2 is then None and saved[3] = (y2, coef2)."""
     conv1, bn1, _, conv2, bn2, _ = seq
     a1, s1 = conv_bn_relu_fwd(M, srcs, conv1, bn1, cin_pad)
-    a2, s2 = conv_bn_relu_fwd(M, [a1], conv2, bn2)
+    a2, s2 = conv_bn_relu_fwd(M, [a1], conv2, bn2, defer=defer)
     return a2, (srcs, a1, s1, s2)
 
 
-def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None):
+def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None, k2=None):
+    """k2: BN2's backward coefficients already reduced by the producer of da2
+    (the fused max-pool backward of the Down that consumed this output)."""
     conv1, bn1, _, conv2, bn2, _ = seq
     srcs, a1, s1, s2 = saved
-    da1 = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True)
+    da1 = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True, k=k2)
     return conv_bn_relu_bwd(M, srcs, conv1, bn1, s1, da1, need_dsrc, cvalid)
 
 
 # ----------------------------------------------------------------------------
 # Down (unet_parts.py:51-63): MaxPool2d(2) -> DoubleConv
 # ----------------------------------------------------------------------------
-def down_fwd(M, mod, x):
+def down_fwd(M, mod, x, pend=None, defer=False):
+    """x: the input activation, or None with pend = (y, coef) of the producing
+    DoubleConv's unapplied BN2 -- then BN + ReLU and the 2x2 max-pool run as
+    one pass (vu_bn_apply_maxpool2) that also materialises x (the skip
+    connection).  defer: this Down's own output feeds another Down.
+    Returns (x, out, saved)."""
     seq = mod.maxpool_conv[1].double_conv
-    xp = K.maxpool_fwd(x, M.d)
-    out, sdc = double_conv_fwd(M, seq, [xp])
-    return out, (x, sdc)
+    if x is None:
+        y, coef = pend
+        N, C_, H, W = y.shape
+        x = M.act(N, C_, H, W)
+        xp = M.act(N, C_, H // 2, W // 2)
+        K.bn_apply_maxpool(y, x, xp, coef, True, M.d)
+    else:
+        xp = K.maxpool_fwd(x, M.d)
+    out, sdc = double_conv_fwd(M, seq, [xp], defer=defer)
+    return x, out, (x, sdc)
 
 
-def down_bwd(M, mod, saved, dout, add=None):
+def down_bwd(M, mod, saved, dout, add=None, k2=None, prev=None):
+    """Returns dx = d(loss)/d(this Down's input).  k2: this Down's own BN2
+    coefficients, already reduced by the next Down.  prev = (bn, (y, coef))
+    of the BatchNorm + ReLU that produced the input: its backward reduction
+    runs inside the max-pool backward (vu_maxpool2_bwd_bnreduce) and
+    (dx, k) is returned, k for that layer's bn_bwd."""
     x, sdc = saved
     seq = mod.maxpool_conv[1].double_conv
-    dxp = double_conv_bwd(M, seq, sdc, dout, True)
+    dxp = double_conv_bwd(M, seq, sdc, dout, True, k2=k2)
     dx = torch.empty_like(x)
+    if prev is not None:
+        bn, (y, coef) = prev
+        if K.pool_fusable(x) and K.pstride(y) % 8 == 0 and (add is None or K.pstride(add) % 8 == 0):
+            gw, gb, acc = bn_grad_sinks(bn)
+            k = K.maxpool_bwd_bnreduce(x, dxp, dx, add, y, coef, bn.weight, True, gw, gb, acc, M.d,
+                                       train=bn.training)
+            return dx, k
+        K.maxpool_bwd(x, dxp, dx, add, M.d)
+        return dx, None
     K.maxpool_bwd(x, dxp, dx, add, M.d)
     return dx
 

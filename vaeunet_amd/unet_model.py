@@ -38,11 +38,13 @@ class UNet(nn.Module):
     def _fwd(self, M, x):
         cp = (self.n_channels + 7) // 8 * 8
         xa = E.to_act(M, x, cp)
-        x1, s0 = E.double_conv_fwd(M, self.inc.double_conv, [xa], cin_pad=cp)
-        x2, s1 = E.down_fwd(M, self.down1, x1)
-        x3, s2 = E.down_fwd(M, self.down2, x2)
-        x4, s3 = E.down_fwd(M, self.down3, x3)
-        x5, s4 = E.down_fwd(M, self.down4, x4)
+        # each encoder DoubleConv's BN2 + ReLU runs fused with the next Down's
+        # max-pool (which also materialises the skip activation x_k)
+        x1, s0 = E.double_conv_fwd(M, self.inc.double_conv, [xa], cin_pad=cp, defer=True)
+        x1, x2, s1 = E.down_fwd(M, self.down1, x1, s0[3], defer=True)
+        x2, x3, s2 = E.down_fwd(M, self.down2, x2, s1[1][3], defer=True)
+        x3, x4, s3 = E.down_fwd(M, self.down3, x3, s2[1][3], defer=True)
+        x4, x5, s4 = E.down_fwd(M, self.down4, x4, s3[1][3])
         y, u1 = E.up_fwd(M, self.up1, x5, x4)
         y, u2 = E.up_fwd(M, self.up2, y, x3)
         y, u3 = E.up_fwd(M, self.up3, y, x2)
@@ -57,12 +59,15 @@ class UNet(nn.Module):
         dy, dx2 = E.up_bwd(M, self.up3, u3, dy)
         dy, dx3 = E.up_bwd(M, self.up2, u2, dy)
         dx5, dx4 = E.up_bwd(M, self.up1, u1, dy)
-        dx4 = E.down_bwd(M, self.down4, s4, dx5, add=dx4)
-        dx3 = E.down_bwd(M, self.down3, s3, dx4, add=dx3)
-        dx2 = E.down_bwd(M, self.down2, s2, dx3, add=dx2)
-        dx1 = E.down_bwd(M, self.down1, s1, dx2, add=dx1)
+        # each max-pool backward also reduces the BN2 backward of the
+        # DoubleConv whose output it pools (k: that layer's coefficients)
+        bn2 = lambda mod: mod.maxpool_conv[1].double_conv[4]  # noqa: E731
+        dx4, k = E.down_bwd(M, self.down4, s4, dx5, add=dx4, prev=(bn2(self.down3), s3[1][3]))
+        dx3, k = E.down_bwd(M, self.down3, s3, dx4, add=dx3, k2=k, prev=(bn2(self.down2), s2[1][3]))
+        dx2, k = E.down_bwd(M, self.down2, s2, dx3, add=dx2, k2=k, prev=(bn2(self.down1), s1[1][3]))
+        dx1, k = E.down_bwd(M, self.down1, s1, dx2, add=dx1, k2=k, prev=(self.inc.double_conv[4], s0[3]))
         return E.double_conv_bwd(M, self.inc.double_conv, s0, dx1, need_dx,
-                                 cvalid=self.n_channels)
+                                 cvalid=self.n_channels, k2=k)
 
     def forward(self, x):
         M = E.current_mode(x.device, self.grad_ready)

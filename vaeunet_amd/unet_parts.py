@@ -89,7 +89,7 @@ class Down(nn.Module):
         M = E.current_mode(x.device)
 
         def fwd(inp):
-            return E.down_fwd(M, self, E.to_act(M, inp[0]))
+            return E.down_fwd(M, self, E.to_act(M, inp[0]))[1:]
 
         def bwd(state, dout):
             return (E.from_act(E.down_bwd(M, self, state, act_grad(M, dout)), x),)
