@@ -266,21 +266,11 @@ int vu_maxpool2_bwd(const void* x, int64_t xs, const void* dy, int64_t dys,
                     const void* add, int64_t adds, int dtype, void* stream);
 /* MaxPool2d(2) fused with the BatchNorm(+ReLU) of the DoubleConv that feeds it
  * (Down, unet_parts.py:51-63; H, W even, C = 8 * 2^k <= 2048, 8-element
- * strides, else hipErrorInvalidValue).  Forward: a = relu(y*scale+shift) is
- * stored AND pooled in one pass (replaces vu_bn_apply + vu_maxpool2_fwd).
- * Backward: vu_maxpool2_bwd plus the vu_bn_bwd_reduce of the layer that
- * produced x, over the gradient it writes (coef / dgamma / dbeta exactly as
- * vu_bn_bwd_reduce; workspace vu_reduce_workspace_bytes(N*H*W, C)). */
+ * strides, else hipErrorInvalidValue): a = relu(y*scale+shift) is stored AND
+ * pooled in one pass (replaces vu_bn_apply + vu_maxpool2_fwd). */
 int vu_bn_apply_maxpool2(const void* y, int64_t ys, void* a, int64_t as, void* pool, int64_t ps,
                          int N, int H, int W, int C, const float* scale, const float* shift,
                          int relu, int dtype, void* stream);
-int vu_maxpool2_bwd_bnreduce(const void* x, int64_t xs, const void* dy, int64_t dys,
-                             int N, int H, int W, int C, void* dx, int64_t dxs,
-                             const void* add, int64_t adds, const void* y, int64_t ys,
-                             const float* scale, const float* shift, const float* mean,
-                             const float* invstd, const float* gamma, int relu, int train,
-                             float* dgamma, float* dbeta, int accumulate, float* coef,
-                             float* workspace, int dtype, void* stream);
 /* bilinear, align_corners=True, (Hi,Wi) -> (Ho,Wo) placed at (py,px) inside
  * a zero (Hp,Wp) canvas (F.pad of unet_parts.py:88-89 folded in). */
 int vu_upsample_fwd(const void* x, int64_t xs, int N, int Hi, int Wi, int C,

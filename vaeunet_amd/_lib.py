@@ -98,8 +98,6 @@ _SIGS = {
     "vu_maxpool2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _p]),
     "vu_maxpool2_bwd": (_i, [_p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _p, _l, _i, _p]),
     "vu_bn_apply_maxpool2": (_i, [_p, _l, _p, _l, _p, _l, _i, _i, _i, _i, _p, _p, _i, _i, _p]),
-    "vu_maxpool2_bwd_bnreduce": (_i, [_p, _l, _p, _l, _i, _i, _i, _i, _p, _l, _p, _l, _p, _l,
-                                      _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _p, _p, _i, _p]),
     "vu_upsample_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _i, _i, _i, _i, _i, _i, _p]),
     "vu_upsample_bwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _i, _i, _i, _i, _i, _i, _i,
                              _p]),

@@ -423,7 +423,7 @@ __global__ void bn_apply_scalar(const T* x, int64_t xs, T* y, int64_t ys, int64_
 
 // ---- BatchNorm(+ReLU) fused with MaxPool2d(2) (Down, unet_parts.py:51-63;
 //      the encoder DoubleConv outputs feed the pool and the skip) ----
-// Forward: a = relu(y*scale + shift) rounded to T is written (the skip
+// a = relu(y*scale + shift) rounded to T is written (the skip
 // connection and the max-pool backward read it) and the 2x2 max of the
 // rounded values goes to the pooled tensor in the same pass -- one read of
 // y instead of y, then a.  A thread owns 8 channels; a row is one pooled pixel
@@ -464,79 +464,6 @@ __global__ void bn_apply_maxpool_kernel(const T* y, int64_t ys, T* a, int64_t as
 #pragma unroll
     for (int e = 0; e < 8; ++e) o.set(e, best[e]);
     o.store(pool + q * ps + c);
-  }
-}
-
-// Backward: dx = maxpool2 backward (first-max ties, + the skip gradient
-// `add`), and in the same pass the BatchNorm(+ReLU) backward reduction of the
-// layer that produced x (sum dz, sum dz*xhat with dz = dx*(y*scale+shift>0),
-// xhat = (y-mean)*invstd) as [block][2][C] partials for bn_bwd_final -- the
-// separate reduction pass would re-read dx and y.
-template <typename T>
-__global__ void maxpool_bwd_bnred_kernel(const T* x, int64_t xs, const T* dy, int64_t dys, int N, int H, int W,
-                                         int C, T* dx, int64_t dxs, const T* add, int64_t adds, const T* yb,
-                                         int64_t ybs, const float* scale, const float* shift, const float* mean,
-                                         const float* invstd, int relu, float* part) {
-  __shared__ float shm[2][256 * 8];
-  ChanMap cm(C);
-  const int c = cm.cv * 8;
-  float sc[8], sf[8], mu[8], is[8], s0[8], s1[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = scale[c + e]; sf[e] = shift[c + e]; mu[e] = mean[c + e]; is[e] = invstd[c + e];
-    s0[e] = 0.f; s1[e] = 0.f;
-  }
-  const int Ho = H >> 1, Wo = W >> 1;
-  const int64_t Q = (int64_t)N * Ho * Wo;
-  for (int64_t q = (int64_t)blockIdx.x * cm.R + cm.row; q < Q; q += (int64_t)gridDim.x * cm.R) {
-    const int j = (int)(q % Wo);
-    const int64_t t = q / Wo;
-    const int i = (int)(t % Ho), n = (int)(t / Ho);
-    const int64_t p00 = ((int64_t)n * H + 2 * i) * W + 2 * j;
-    Vec8<T> vx[4], va[4], vy[4], g;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t pix = p00 + (k >> 1) * W + (k & 1);
-      vx[k].load(x + pix * xs + c);
-      vy[k].load(yb + pix * ybs + c);
-      if (add) va[k].load(add + pix * adds + c); else va[k].zero();
-    }
-    g.load(dy + q * dys + c);
-    int arg[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float best = -INFINITY;
-      arg[e] = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float f = vx[k].get(e);
-        if (f > best || isnan(f)) { best = f; arg[e] = k; }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      Vec8<T> o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o.set(e, va[k].get(e) + (arg[e] == k ? g.get(e) : 0.f));
-      o.store(dx + (p00 + (k >> 1) * W + (k & 1)) * dxs + c);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float yv = vy[k].get(e);
-        float dz = o.get(e);  // the stored (rounded) gradient, as the reduction pass reads it
-        if (relu && !(yv * sc[e] + sf[e] > 0.f)) dz = 0.f;
-        s0[e] += dz;
-        s1[e] += dz * ((yv - mu[e]) * is[e]);
-      }
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { shm[0][cm.row * C + c + e] = s0[e]; shm[1][cm.row * C + c + e] = s1[e]; }
-  __syncthreads();
-  for (int cc = threadIdx.x; cc < C; cc += 256) {
-    float a0 = 0.f, a1 = 0.f;
-    for (int r = 0; r < cm.R; ++r) { a0 += shm[0][r * C + cc]; a1 += shm[1][r * C + cc]; }
-    part[((int64_t)blockIdx.x * 2 + 0) * C + cc] = a0;
-    part[((int64_t)blockIdx.x * 2 + 1) * C + cc] = a1;
   }
 }
 
@@ -705,9 +632,9 @@ extern "C" int vu_chan_sum(const void* x, int64_t stride, int N, int H, int W, i
   return (int)hipGetLastError();
 }
 
-// MaxPool2d(2) fusions (even H, W; C = 8 * 2^k <= 2048; 8-element strides)
-static bool pool_fusable(int H, int W, int C, int64_t s0, int64_t s1, int64_t s2, int64_t s3 = 0, int64_t s4 = 0) {
-  return H % 2 == 0 && W % 2 == 0 && chanmap_ok(C, s0, s1, s2) && s3 % 8 == 0 && s4 % 8 == 0;
+// MaxPool2d(2) fusion (even H, W; C = 8 * 2^k <= 2048; 8-element strides)
+static bool pool_fusable(int H, int W, int C, int64_t s0, int64_t s1, int64_t s2) {
+  return H % 2 == 0 && W % 2 == 0 && chanmap_ok(C, s0, s1, s2);
 }
 
 extern "C" int vu_bn_apply_maxpool2(const void* y, int64_t ys, void* a, int64_t as, void* pool, int64_t ps, int N,
@@ -724,29 +651,5 @@ extern "C" int vu_bn_apply_maxpool2(const void* y, int64_t ys, void* a, int64_t 
   else
     hipLaunchKernelGGL(bn_apply_maxpool_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)y, ys,
                        (float*)a, as, (float*)pool, ps, N, H, W, C, scale, shift, relu);
-  return (int)hipGetLastError();
-}
-
-extern "C" int vu_maxpool2_bwd_bnreduce(const void* x, int64_t xs, const void* dy, int64_t dys, int N, int H, int W,
-                                        int C, void* dx, int64_t dxs, const void* add, int64_t adds, const void* y,
-                                        int64_t ys, const float* scale, const float* shift, const float* mean,
-                                        const float* invstd, const float* gamma, int relu, int train, float* dgamma,
-                                        float* dbeta, int accumulate, float* coef, float* workspace, int dtype,
-                                        void* stream) {
-  if (!pool_fusable(H, W, C, xs, dxs, ys, dys, add ? adds : 0)) return (int)hipErrorInvalidValue;
-  const int64_t Q = (int64_t)N * (H / 2) * (W / 2);
-  if (Q == 0) return (int)hipErrorInvalidValue;
-  const int nblk = (int)chan_grid(Q * 4, C, RED_MAXBLK);
-  hipStream_t st = (hipStream_t)stream;
-  if (dtype == VU_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_bnred_kernel<bf16_t>, dim3(nblk), dim3(256), 0, st, (const bf16_t*)x, xs,
-                       (const bf16_t*)dy, dys, N, H, W, C, (bf16_t*)dx, dxs, (const bf16_t*)add, adds,
-                       (const bf16_t*)y, ys, scale, shift, mean, invstd, relu, workspace);
-  else
-    hipLaunchKernelGGL(maxpool_bwd_bnred_kernel<float>, dim3(nblk), dim3(256), 0, st, (const float*)x, xs,
-                       (const float*)dy, dys, N, H, W, C, (float*)dx, dxs, (const float*)add, adds,
-                       (const float*)y, ys, scale, shift, mean, invstd, relu, workspace);
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, C,
-                     (int64_t)N * H * W, gamma, invstd, dgamma, dbeta, accumulate, coef, train);
   return (int)hipGetLastError();
 }

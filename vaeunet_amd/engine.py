@@ -294,16 +294,15 @@ def bn_grad_sinks(bn):
     return gw, gb, accw or accb
 
 
-def bn_bwd(dy, x, coef, bn, relu, M, dx=None, k=None):
+def bn_bwd(dy, x, coef, bn, relu, M, dx=None):
     """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
     batch statistics; eval mode (running statistics, constants) gives
-    dx = gamma*invstd*dz and the same dgamma/dbeta sums.  k: coefficients
-    (and dgamma/dbeta) already reduced by the producer of dy."""
-    gw, gb, acc = (None, None, False) if k is not None else bn_grad_sinks(bn)
+    dx = gamma*invstd*dz and the same dgamma/dbeta sums."""
+    gw, gb, acc = bn_grad_sinks(bn)
     if dx is None:
         dx = torch.empty_like(x)
     K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
-                  train=bn.training, k=k)
+                  train=bn.training)
     return dx
 
 
@@ -328,12 +327,12 @@ def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
 
 
 def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False,
-                     cin_pad=None, k=None):
+                     cin_pad=None):
     """cin_pad: compute the input gradient for cin_pad channels (zero weight
     rows past conv.in_channels) so that its column count stays a tile
     multiple; the caller reads the real channels only."""
     y, coef = saved
-    dy = bn_bwd(da, y, coef, bn, True, M, k=k)
+    dy = bn_bwd(da, y, coef, bn, True, M)
     wgrad3x3(dy, srcs, conv.weight, M, cvalid)
     M.notify([conv.weight, bn.weight, bn.bias])
     if not need_dsrc:
@@ -358,12 +357,10 @@ def double_conv_fwd(M, seq, srcs, cin_pad=None, defer=False):
     return a2, (srcs, a1, s1, s2)
 
 
-def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None, k2=None):
-    """k2: BN2's backward coefficients already reduced by the producer of da2
-    (the fused max-pool backward of the Down that consumed this output)."""
+def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None):
     conv1, bn1, _, conv2, bn2, _ = seq
     srcs, a1, s1, s2 = saved
-    da1 = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True, k=k2)
+    da1 = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True)
     return conv_bn_relu_bwd(M, srcs, conv1, bn1, s1, da1, need_dsrc, cvalid)
 
 
@@ -389,25 +386,15 @@ def down_fwd(M, mod, x, pend=None, defer=False):
     return x, out, (x, sdc)
 
 
-def down_bwd(M, mod, saved, dout, add=None, k2=None, prev=None):
-    """Returns dx = d(loss)/d(this Down's input).  k2: this Down's own BN2
-    coefficients, already reduced by the next Down.  prev = (bn, (y, coef))
-    of the BatchNorm + ReLU that produced the input: its backward reduction
-    runs inside the max-pool backward (vu_maxpool2_bwd_bnreduce) and
-    (dx, k) is returned, k for that layer's bn_bwd."""
+def down_bwd(M, mod, saved, dout, add=None):
+    """dx = d(loss)/d(this Down's input); add = the skip gradient, summed in
+    the max-pool backward.  (A max-pool backward carrying the producing BN's
+    backward reduction streams five tensors and measured slower than the two
+    passes it replaces: DESIGN.md §4.2.)"""
     x, sdc = saved
     seq = mod.maxpool_conv[1].double_conv
-    dxp = double_conv_bwd(M, seq, sdc, dout, True, k2=k2)
+    dxp = double_conv_bwd(M, seq, sdc, dout, True)
     dx = torch.empty_like(x)
-    if prev is not None:
-        bn, (y, coef) = prev
-        if K.pool_fusable(x) and K.pstride(y) % 8 == 0 and (add is None or K.pstride(add) % 8 == 0):
-            gw, gb, acc = bn_grad_sinks(bn)
-            k = K.maxpool_bwd_bnreduce(x, dxp, dx, add, y, coef, bn.weight, True, gw, gb, acc, M.d,
-                                       train=bn.training)
-            return dx, k
-        K.maxpool_bwd(x, dxp, dx, add, M.d)
-        return dx, None
     K.maxpool_bwd(x, dxp, dx, add, M.d)
     return dx
 

@@ -351,21 +351,19 @@ def bn_apply(x, y, coef, relu, dtype):
     return y
 
 
-def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True, k=None):
+def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
     """dx = BN(+ReLU) backward; writes/accumulates dgamma, dbeta.  train=False:
-    the statistics are constants (eval mode).  k: backward coefficients
-    already reduced by the producer of dy (maxpool_bwd_bnreduce)."""
+    the statistics are constants (eval mode)."""
     N, Cc, H, W = x.shape
     P = N * H * W
     dev = x.device
-    if k is None:
-        k = torch.empty((3, Cc), dtype=torch.float32, device=dev)
-        ws = torch.empty(query("vu_reduce_workspace_bytes", P, Cc) // 4 + 1, dtype=torch.float32,
-                         device=dev)
-        call("vu_bn_bwd_reduce", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
-             ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
-             1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype,
-             stream())
+    k = torch.empty((3, Cc), dtype=torch.float32, device=dev)
+    ws = torch.empty(query("vu_reduce_workspace_bytes", P, Cc) // 4 + 1, dtype=torch.float32,
+                     device=dev)
+    call("vu_bn_bwd_reduce", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
+         ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
+         1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype,
+         stream())
     call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
          ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
          stream())
@@ -418,8 +416,8 @@ def maxpool_bwd(x, dy, dx, add, dtype):
 
 
 def pool_fusable(y):
-    """MaxPool2d(2) + BatchNorm fusion applies (vu_bn_apply_maxpool2 /
-    vu_maxpool2_bwd_bnreduce): even H, W; C = 8 * 2^k <= 2048; NHWC strides."""
+    """MaxPool2d(2) + BatchNorm fusion applies (vu_bn_apply_maxpool2): even
+    H, W; C = 8 * 2^k <= 2048; NHWC strides."""
     N, Cc, H, W = y.shape
     v = Cc // 8
     return (H % 2 == 0 and W % 2 == 0 and Cc % 8 == 0 and 0 < v <= 256 and v & (v - 1) == 0
@@ -432,21 +430,6 @@ def bn_apply_maxpool(y, a, pool, coef, relu, dtype):
     call("vu_bn_apply_maxpool2", ptr(y), pstride(y), ptr(a), pstride(a), ptr(pool), pstride(pool), N, H, W, Cc,
          ptr(coef[0]), ptr(coef[1]), 1 if relu else 0, dtype, stream())
     return a, pool
-
-
-def maxpool_bwd_bnreduce(x, dy, dx, add, y, coef, gamma, relu, dgamma, dbeta, acc, dtype, train=True):
-    """dx = maxpool2 backward (+ add); returns the BatchNorm backward
-    coefficients [3, C] of the layer whose output is x (y its pre-BN input),
-    with dgamma / dbeta written (accumulated) as vu_bn_bwd_reduce does."""
-    N, Cc, H, W = x.shape
-    k = torch.empty((3, Cc), dtype=torch.float32, device=x.device)
-    ws = torch.empty(query("vu_reduce_workspace_bytes", N * H * W, Cc) // 4 + 1, dtype=torch.float32,
-                     device=x.device)
-    call("vu_maxpool2_bwd_bnreduce", ptr(x), pstride(x), ptr(dy), pstride(dy), N, H, W, Cc, ptr(dx), pstride(dx),
-         ptr(add), pstride(add) if add is not None else 0, ptr(y), pstride(y), ptr(coef[0]), ptr(coef[1]),
-         ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0, 1 if train else 0, ptr(dgamma), ptr(dbeta),
-         1 if acc else 0, ptr(k), ptr(ws), dtype, stream())
-    return k
 
 
 def upsample_fwd(x, out, Ho, Wo, py, px, dtype):

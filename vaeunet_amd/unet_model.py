@@ -59,15 +59,12 @@ class UNet(nn.Module):
         dy, dx2 = E.up_bwd(M, self.up3, u3, dy)
         dy, dx3 = E.up_bwd(M, self.up2, u2, dy)
         dx5, dx4 = E.up_bwd(M, self.up1, u1, dy)
-        # each max-pool backward also reduces the BN2 backward of the
-        # DoubleConv whose output it pools (k: that layer's coefficients)
-        bn2 = lambda mod: mod.maxpool_conv[1].double_conv[4]  # noqa: E731
-        dx4, k = E.down_bwd(M, self.down4, s4, dx5, add=dx4, prev=(bn2(self.down3), s3[1][3]))
-        dx3, k = E.down_bwd(M, self.down3, s3, dx4, add=dx3, k2=k, prev=(bn2(self.down2), s2[1][3]))
-        dx2, k = E.down_bwd(M, self.down2, s2, dx3, add=dx2, k2=k, prev=(bn2(self.down1), s1[1][3]))
-        dx1, k = E.down_bwd(M, self.down1, s1, dx2, add=dx1, k2=k, prev=(self.inc.double_conv[4], s0[3]))
+        dx4 = E.down_bwd(M, self.down4, s4, dx5, add=dx4)
+        dx3 = E.down_bwd(M, self.down3, s3, dx4, add=dx3)
+        dx2 = E.down_bwd(M, self.down2, s2, dx3, add=dx2)
+        dx1 = E.down_bwd(M, self.down1, s1, dx2, add=dx1)
         return E.double_conv_bwd(M, self.inc.double_conv, s0, dx1, need_dx,
-                                 cvalid=self.n_channels, k2=k)
+                                 cvalid=self.n_channels)
 
     def forward(self, x):
         M = E.current_mode(x.device, self.grad_ready)
