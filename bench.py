@@ -149,14 +149,16 @@ def cpu_baseline(args, dev):
         with ctx:
             ref_out, ref_loss, _ = train_step(model, opt)  # warmup; pre-update outputs
         warm = time.perf_counter() - t0
+        _progress(f"cpu_baseline {leg} warmup step: {warm:.1f} s")
         if leg == "fp32":
             parity = gpu_parity(args, x, t, ref_out, ref_loss, dev, eps)
         # bounded sample: a slow host gets fewer timed steps (stated in "sample")
         n = args.cpu_steps if warm * args.cpu_steps <= args.cpu_budget_s else max(1, int(args.cpu_budget_s // warm))
         t0 = time.perf_counter()
         with ctx:
-            for _ in range(n):
+            for i in range(n):
                 train_step(model, opt)
+                _progress(f"cpu_baseline {leg} step {i + 1}/{n}: {time.perf_counter() - t0:.1f} s")
         dt = time.perf_counter() - t0
         legs[leg] = {"value": round(B * n / dt, 4), "steps": n, "s_per_step": round(dt / n, 3)}
     f = legs["fp32"]
@@ -168,6 +170,11 @@ def cpu_baseline(args, dev):
                       f"(oracle/cpu_ref.py, torch CPU, {threads} threads)"),
            "legs": legs}
     return out, parity
+
+
+def _progress(msg):
+    """Progress of the long CPU legs on stderr (the JSON line stays the only stdout line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 class _Null:
