@@ -41,6 +41,8 @@ template <typename T> struct Vec8;
 template <> struct Vec8<bf16_t> {
   u32x4 v;
   VU_DEV void load(const bf16_t* p) { v = *reinterpret_cast<const u32x4*>(p); }
+  // streaming (last-use) load: non-temporal cache policy
+  VU_DEV void load_nt(const bf16_t* p) { v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)); }
   VU_DEV void store(bf16_t* p) const { *reinterpret_cast<u32x4*>(p) = v; }
   VU_DEV float get(int i) const {
     uint32_t w = v[i >> 1];
@@ -58,6 +60,10 @@ template <> struct Vec8<float> {
   VU_DEV void load(const float* p) {
     a = *reinterpret_cast<const f32x4*>(p);
     b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  VU_DEV void load_nt(const float* p) {
+    a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
   }
   VU_DEV void store(float* p) const {
     *reinterpret_cast<f32x4*>(p) = a;
