@@ -297,6 +297,58 @@ __global__ void slab_reduce_kernel(const float* slab, int splits, int ni, int nj
   *o = accumulate ? *o + s : s;
 }
 
+// Vectorised form (tot % 4 == 0): a thread owns 4 consecutive outputs
+// (16-byte slab loads), SL split lanes per output group, 4 independent
+// accumulators per lane.  The slabs were just written by the weight-gradient
+// kernel and sit in the L2s / Infinity Cache, so the reduce is bound by the
+// bytes it keeps in flight, not by HBM: 16-byte loads x 4 accumulators x
+// up to 16 split lanes keep ~8x more in flight than one float per lane.
+template <int SL>
+__global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* slab, int splits, int ni, int nj, int C,
+                                                          int cvalid, int64_t s_i, int64_t s_tap, int64_t s_c,
+                                                          float* out, int accumulate) {
+  constexpr int L = 256 / SL;  // float4 output groups per block
+  __shared__ f32x4 sh[SL][L];
+  const int l = threadIdx.x % L, q = threadIdx.x / L;
+  const int64_t tot4 = (int64_t)ni * nj / 4;
+  const int64_t idx4 = (int64_t)blockIdx.x * L + l;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(slab);
+  f32x4 a[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (idx4 < tot4) {
+    int k = q;
+    for (; k + 3 * SL < splits; k += 4 * SL)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += s4[(int64_t)(k + u * SL) * tot4 + idx4];
+    for (; k < splits; k += SL) a[0] += s4[(int64_t)k * tot4 + idx4];
+  }
+  sh[q][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (q != 0 || idx4 >= tot4) return;
+  f32x4 s = sh[0][l];
+#pragma unroll
+  for (int w = 1; w < SL; ++w) s += sh[w][l];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t idx = idx4 * 4 + e;
+    const int i = (int)(idx / nj), j = (int)(idx - (int64_t)i * nj);
+    const int tap = j / C, c = j - tap * C;
+    if (c >= cvalid) continue;
+    float* o = out + i * s_i + tap * s_tap + c * s_c;
+    *o = accumulate ? *o + s[e] : s[e];
+  }
+}
+
+template <int SL>
+void launch_slab4(const float* slab, int splits, int ni, int nj, int C, int cvalid, int64_t s_i, int64_t s_tap,
+                  int64_t s_c, float* out, int accumulate, hipStream_t st) {
+  constexpr int L = 256 / SL;
+  const int64_t tot4 = (int64_t)ni * nj / 4;
+  hipLaunchKernelGGL(slab_reduce4_kernel<SL>, dim3((unsigned)((tot4 + L - 1) / L)), dim3(256), 0, st, slab, splits,
+                     ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate);
+}
+
 }  // namespace
 
 int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj);
@@ -351,10 +403,25 @@ extern "C" int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream) {
   return dtype == VU_BF16 ? dispatch_wg<bf16_t>(*args, st) : dispatch_wg<float>(*args, st);
 }
 
+static bool slab4_on() {  // VU_SLAB4=0: the scalar reduce (A/B runs)
+  static int v = [] { const char* e = getenv("VU_SLAB4"); return e ? atoi(e) : 1; }();
+  return v != 0;
+}
+
 extern "C" int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C, int cvalid, int64_t s_i,
                               int64_t s_tap, int64_t s_c, float* out, int accumulate, void* stream) {
   int64_t tot = (int64_t)ni * nj;
   if (tot == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (tot % 4 == 0 && reinterpret_cast<uintptr_t>(slab) % 16 == 0 && slab4_on()) {
+    // split lanes: about 4 slab loads per lane, at most 16 lanes
+    if (splits >= 64) launch_slab4<16>(slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate, st);
+    else if (splits >= 32) launch_slab4<8>(slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate, st);
+    else if (splits >= 16) launch_slab4<4>(slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate, st);
+    else if (splits >= 8) launch_slab4<2>(slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate, st);
+    else launch_slab4<1>(slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate, st);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(256), 0,
                      (hipStream_t)stream, slab, splits, ni, nj, C, cvalid, s_i, s_tap, s_c, out, accumulate);
   return (int)hipGetLastError();
