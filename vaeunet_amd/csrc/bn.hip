@@ -507,9 +507,10 @@ inline unsigned chan_grid(int64_t P, int C, int maxblk) {
 
 // Non-temporal loads for the streams of a large tensor: those bytes cannot
 // stay in the 256 MB Infinity Cache until their next use anyway, and keeping
-// them out leaves it to the smaller tensors (measured: UNet +1.9 %, VAE -0.7 %
-// with nt on every BN stream).  Threshold in MB per streamed tensor
-// (VU_BN_NT_MB overrides, for A/B runs).
+// them out leaves it to the smaller tensors.  Same-box A/B
+// (profiles/r2_ab_bn_nt.log): UNet 483 -> 491 img/s for any threshold of
+// 0-128 MB; VAE 708 at -1 (never), 701-703 at 0 (always), 708 at 32 MB.
+// Threshold in MB per streamed tensor (VU_BN_NT_MB overrides, for A/B runs).
 inline bool bn_nt(int64_t P, int C, int esize) {
   static const int64_t mb = [] {
     const char* e = getenv("VU_BN_NT_MB");
