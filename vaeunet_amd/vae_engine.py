@@ -83,20 +83,28 @@ def conv_dgrad(M, dy, conv, dx, accumulate):
         return dx
     if s != 2:
         raise NotImplementedError("only stride 1 and 2 convolutions")
-    if not accumulate:
-        dx.zero_()
     Ho, Wo = dy.shape[2], dy.shape[3]
+    classes = []
     for py in (0, 1):
         for px in (0, 1):
             wmat, ry, rx = _parity_w(conv.weight, py, px, p, M.d)
             hp, wp = (H - py + 1) // 2, (W - px + 1) // 2
-            if wmat is None or hp <= 0 or wp <= 0:
+            if hp <= 0 or wp <= 0:
                 continue
-            oy = (py + p - max(ry)) // 2
-            ox = (px + p - max(rx)) // 2
-            g = K.gather([dy], N, hp, wp, R=len(ry), S=len(rx), oy=oy, ox=ox, Hs=Ho, Ws=Wo)
-            K.gemm_fwd(g, wmat, ci, dx, M.d, accumulate=True, kind="dgrad",
-                       strided=(H, W, py, px))
+            classes.append((py, px, wmat, ry, rx, hp, wp))
+    # the four parity classes write disjoint pixel sub-lattices that cover dx:
+    # with every class non-empty, each one overwrites its lattice (no zero fill)
+    covering = all(c[2] is not None for c in classes)
+    if not accumulate and not covering:
+        K.zero(dx)
+    for py, px, wmat, ry, rx, hp, wp in classes:
+        if wmat is None:
+            continue
+        oy = (py + p - max(ry)) // 2
+        ox = (px + p - max(rx)) // 2
+        g = K.gather([dy], N, hp, wp, R=len(ry), S=len(rx), oy=oy, ox=ox, Hs=Ho, Ws=Wo)
+        K.gemm_fwd(g, wmat, ci, dx, M.d, accumulate=accumulate or not covering, kind="dgrad",
+                   strided=(H, W, py, px))
     return dx
 
 
@@ -139,16 +147,18 @@ def basic_bwd(M, blk, saved, dout, need_dx=True):
     M.notify([blk.conv1.weight, blk.conv2.weight, blk.bn1.weight, blk.bn1.bias,
               blk.bn2.weight, blk.bn2.bias])
     dx = None
-    if need_dx:
-        dx = conv_dgrad(M, dy1, blk.conv1, torch.empty_like(x), False)
     if blk.downsample is not None:
+        if need_dx:
+            dx = conv_dgrad(M, dy1, blk.conv1, torch.empty_like(x), False)
         dyd = E.bn_bwd(g, yd, cd, blk.downsample[1], False, M)
         conv_wgrad(M, dyd, [x], blk.downsample[0])
         M.notify([blk.downsample[0].weight, blk.downsample[1].weight, blk.downsample[1].bias])
         if need_dx:
             conv_dgrad(M, dyd, blk.downsample[0], dx, True)
     elif need_dx:
-        K.copy(g, dx, accumulate=True)
+        # identity shortcut: dx = g + conv1's input gradient, accumulated by the
+        # GEMM epilogue into g itself (g is dead after bn2's backward)
+        dx = conv_dgrad(M, dy1, blk.conv1, g, True)
     return dx
 
 
