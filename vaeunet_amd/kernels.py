@@ -30,7 +30,9 @@ def empty_act(N, Cc, H, W, dtype, device):
 
 
 def zeros_act(N, Cc, H, W, dtype, device):
-    return torch.empty((N, Cc, H, W), dtype=dtype, device=device, memory_format=CL).zero_()
+    y = torch.empty((N, Cc, H, W), dtype=dtype, device=device, memory_format=CL)
+    zero(y)
+    return y
 
 
 def pstride(t):

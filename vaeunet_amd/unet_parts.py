@@ -48,7 +48,7 @@ class AttentionGate(nn.Module):
 
         def bwd(state, dout):
             st, ga = state
-            dg = torch.zeros_like(ga)
+            dg = M.zeros(*ga.shape)
             dx = E.attention_bwd(M, self, st, act_grad(M, dout), (dg, 0), True)
             return E.from_act(dg, g), E.from_act(dx, x)
         return run_block(self, fwd, bwd, (g, x))
