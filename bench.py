@@ -254,7 +254,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        # nccl = RCCL over xGMI; VU_DIST_BACKEND=gloo rehearses the N>1 path
+        # with several ranks sharing one GPU (RCCL refuses duplicate devices)
+        dist.init_process_group(os.environ.get("VU_DIST_BACKEND", "nccl"), init_method="env://")
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -301,7 +304,10 @@ def main():
             reducer.finish()
         clip(model.parameters(), 1.0)
         opt.step()
-        opt.zero_grad(set_to_none=reducer is None)
+        if reducer is not None:
+            reducer.zero_grad()  # one fill per ~25 MB bucket (the .grad views stay bound)
+        else:
+            opt.zero_grad(set_to_none=True)
         return loss
 
     graphed = None
