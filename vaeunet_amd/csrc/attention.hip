@@ -26,8 +26,24 @@ inline unsigned ew_grid(int64_t work) {
   return (unsigned)g;
 }
 
+// Sum over aligned groups of lpp lanes (lpp a power of two, uniform): DPP
+// lane permutations within 16-lane rows (xor 1, xor 2, half-row mirror,
+// row mirror: each step pairs every lane with one holding the other half of
+// its group), LDS-crossbar shuffles only across rows.  A ds_bpermute chain
+// costs one LDS round trip per step, and these per-pixel dot products run
+// one chain per pixel.
+template <int CTRL>
+VU_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
 VU_DEV float group_sum(float v, int lpp) {
-  for (int o = lpp >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (lpp >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  if (lpp >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  if (lpp >= 8) v += dpp_f<0x141>(v);  // row_half_mirror
+  if (lpp >= 16) v += dpp_f<0x140>(v); // row_mirror
+  if (lpp >= 32) v += __shfl_xor(v, 16, 64);
+  if (lpp >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 
@@ -228,6 +244,47 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
   const int sub = lane % lpp, slot = lane / lpp;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  if (C <= 512) {
+    // one 8-channel chunk per lane: its weights and the bias live in
+    // registers (the compiler cannot hoist per-pixel weight loads that may
+    // alias y), and PU pixel rows per lane are loaded before any is used
+    // (cold-cache 512^2 x 64 -> 2: 135 -> 107 us with the DPP group sums)
+    constexpr int PU = 4;
+    const int c = sub * 8;
+    float wr[4][8], bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bj[j] = (j < J && b) ? b[j] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wr[j][k] = j < J ? w[j * C + c + k] : 0.f;
+    }
+    for (int64_t pb = wave * ppw * PU; pb < P; pb += nwaves * ppw * PU) {
+      float f[PU][8];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int64_t p = pb + u * ppw + slot;
+        if (p < P) load8<T>(x + p * xs + c, f[u]);
+        else
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[u][k] = 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int64_t p = pb + u * ppw + slot;
+        float acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j] = 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[j] += f[u][k] * wr[j][k];
+          acc[j] = group_sum(acc[j], lpp);
+        }
+        if (sub == 0 && p < P)
+          for (int j = 0; j < J; ++j) y[p * ys + j] = acc[j] + bj[j];
+      }
+    }
+    return;
+  }
   for (int64_t pb = wave * ppw; pb < P; pb += nwaves * ppw) {
     int64_t p = pb + slot;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
