@@ -54,7 +54,7 @@ __global__ void maxpool_fwd_kernel(const T* x, int64_t xs, int N, int H, int W, 
   }
 }
 
-template <typename T, int VW>
+template <typename T, int VW, bool NT>
 __global__ void maxpool_bwd_kernel(const T* x, int64_t xs, const T* dy, int64_t dys, int N, int H, int W, int C,
                                    T* dx, int64_t dxs, const T* add, int64_t adds) {
   int Ho = H >> 1, Wo = W >> 1, V = C / VW;
@@ -68,46 +68,53 @@ __global__ void maxpool_bwd_kernel(const T* x, int64_t xs, const T* dy, int64_t 
     int n = (int)(t / Ho);
     float best[VW];
     int arg[VW];
-    float vals[4][VW];
+    float vals[4][VW], g[VW], o[4][VW];
+    // every load of the window (4 x, dy, 4 skip-gradient rows) is issued
+    // before any is used; all of them are last uses (NT: non-temporal)
+    if (VW == 8) {
+      Vec8<T> vx[4], vg, va[4];
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        const int64_t pix = ((int64_t)n * H + 2 * i + (ab >> 1)) * W + 2 * j + (ab & 1);
+        if (NT) vx[ab].load_nt(x + pix * xs + c); else vx[ab].load(x + pix * xs + c);
+        if (add) { if (NT) va[ab].load_nt(add + pix * adds + c); else va[ab].load(add + pix * adds + c); }
+      }
+      if (NT) vg.load_nt(dy + q * dys + c); else vg.load(dy + q * dys + c);
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          vals[ab][k] = vx[ab].get(k);
+          o[ab][k] = add ? va[ab].get(k) : 0.f;
+        }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = vg.get(k);
+    } else {
+#pragma unroll
+      for (int ab = 0; ab < 4; ++ab) {
+        const int64_t pix = ((int64_t)n * H + 2 * i + (ab >> 1)) * W + 2 * j + (ab & 1);
+        vals[ab][0] = ld1<T>(x + pix * xs + c);
+        o[ab][0] = add ? ld1<T>(add + pix * adds + c) : 0.f;
+      }
+      g[0] = ld1<T>(dy + q * dys + c);
+    }
 #pragma unroll
     for (int k = 0; k < VW; ++k) { best[k] = -INFINITY; arg[k] = 0; }
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int ab = 0; ab < 4; ++ab)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const T* src = x + (((int64_t)n * H + 2 * i + a) * W + 2 * j + b) * xs + c;
-        if (VW == 8) {
-          Vec8<T> v; v.load(src);
-#pragma unroll
-          for (int k = 0; k < VW; ++k) vals[a * 2 + b][k] = v.get(k);
-        } else vals[a * 2 + b][0] = ld1<T>(src);
-#pragma unroll
-        for (int k = 0; k < VW; ++k) {
-          float f = vals[a * 2 + b][k];
-          if (f > best[k] || isnan(f)) { best[k] = f; arg[k] = a * 2 + b; }
-        }
+      for (int k = 0; k < VW; ++k) {
+        float f = vals[ab][k];
+        if (f > best[k] || isnan(f)) { best[k] = f; arg[k] = ab; }
       }
-    float g[VW];
-    if (VW == 8) { Vec8<T> v; v.load(dy + q * dys + c); for (int k = 0; k < 8; ++k) g[k] = v.get(k); }
-    else g[0] = ld1<T>(dy + q * dys + c);
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int ab = 0; ab < 4; ++ab) {
+      const int64_t pix = ((int64_t)n * H + 2 * i + (ab >> 1)) * W + 2 * j + (ab & 1);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        int64_t pix = ((int64_t)n * H + 2 * i + a) * W + 2 * j + b;
-        float o[VW];
-        if (add) {
-          if (VW == 8) { Vec8<T> v; v.load(add + pix * adds + c); for (int k = 0; k < 8; ++k) o[k] = v.get(k); }
-          else o[0] = ld1<T>(add + pix * adds + c);
-        } else {
-#pragma unroll
-          for (int k = 0; k < VW; ++k) o[k] = 0.f;
-        }
-#pragma unroll
-        for (int k = 0; k < VW; ++k) if (arg[k] == a * 2 + b) o[k] += g[k];
-        if (VW == 8) { Vec8<T> v; for (int k = 0; k < 8; ++k) v.set(k, o[k]); v.store(dx + pix * dxs + c); }
-        else st1<T>(dx + pix * dxs + c, o[0]);
-      }
+      for (int k = 0; k < VW; ++k) if (arg[k] == ab) o[ab][k] += g[k];
+      if (VW == 8) { Vec8<T> v; for (int k = 0; k < 8; ++k) v.set(k, o[ab][k]); v.store(dx + pix * dxs + c); }
+      else st1<T>(dx + pix * dxs + c, o[ab][0]);
+    }
   }
 }
 
@@ -332,9 +339,16 @@ extern "C" int vu_maxpool2_bwd(const void* x, int64_t xs, const void* dy, int64_
   bool vec = C % 8 == 0 && xs % 8 == 0 && dys % 8 == 0 && dxs % 8 == 0 && (!add || adds % 8 == 0);
   DISPATCH_T(dtype, {
     if (work > 0) {
-      if (vec) hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
-                                  (const T*)x, xs, (const T*)dy, dys, N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
-      else hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1>), dim3(ew_grid(work)), dim3(256), 0, st,
+      // non-temporal loads once the input no longer fits beside the stream
+      // in the Infinity Cache (the BN streams' 32 MB rule, bn.hip)
+      const bool nt = (int64_t)N * H * W * C * (int64_t)sizeof(T) >= 32000000;
+      if (vec && nt)
+        hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8, true>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
+                           (const T*)x, xs, (const T*)dy, dys, N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
+      else if (vec)
+        hipLaunchKernelGGL((maxpool_bwd_kernel<T, 8, false>), dim3(ew_grid(work / 8)), dim3(256), 0, st,
+                           (const T*)x, xs, (const T*)dy, dys, N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
+      else hipLaunchKernelGGL((maxpool_bwd_kernel<T, 1, false>), dim3(ew_grid(work)), dim3(256), 0, st,
                               (const T*)x, xs, (const T*)dy, dys, N, H, W, C, (T*)dx, dxs, (const T*)add, adds);
     }
     if ((H & 1) || (W & 1))
