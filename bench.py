@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8, help="CPU baseline batch (BASELINE.md §4: 8)")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps per leg after 1 warmup")
-    ap.add_argument("--cpu-budget-s", type=float, default=90.0,
+    ap.add_argument("--cpu-budget-s", type=float, default=60.0,
                     help="cap on the timed CPU work per leg (fewer steps on a slow host)")
     ap.add_argument("--cpu-no-bf16", action="store_true", help="skip the CPU autocast-bf16 leg")
     ap.add_argument("--torch-optim", action="store_true",
@@ -91,11 +91,14 @@ def _cpu_model():
 
 
 def _cpu_threads():
-    """All cores this process may run on, capped by the box's OMP_NUM_THREADS
-    share when the launcher set one (the GPU box sets its per-GPU share)."""
+    """(affinity, share): every core this process may run on
+    (``len(os.sched_getaffinity(0))``, BASELINE.md §4 / SURVEY.md §8d: the
+    headline CPU baseline's thread count) and the per-GPU CPU share the box's
+    launcher sets in OMP_NUM_THREADS (reported as a second, labelled leg)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     omp = os.environ.get("OMP_NUM_THREADS")
-    return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
+    share = min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
+    return n, share
 
 
 def _ref_model(args):
@@ -119,16 +122,18 @@ def cpu_baseline(args, dev):
     """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py;
     kind "port") timed on this host: the same synthetic batch
     (B x 3 x S x S, rank-0 seed), 1 warmup + K timed full train steps (fwd,
-    loss, bwd, clip, AdamW), fp32 (the reference semantics) and CPU autocast
-    bf16 (train.py's amp default on CPU).  --model vae: UNetResNet with
-    CombinedLoss + 1e-3 * KL (free bits 1e-3) and a fixed latent draw.
+    loss, bwd, clip, AdamW).  Legs: fp32 on every core of the affinity mask
+    (the headline: reference semantics, threads = len(sched_getaffinity)),
+    CPU autocast bf16 on the same threads (train.py's amp default on CPU),
+    and fp32 on the per-GPU share (OMP_NUM_THREADS) when that differs.
+    --model vae: UNetResNet with CombinedLoss + 1e-3 * KL (free bits 1e-3)
+    and a fixed latent draw.
 
-    The fp32 warmup step's pre-update outputs are also the parity reference:
-    the GPU model (fp32 parity mode, same weights, same batch) is compared
-    with them (the "Dice parity vs CPU ref" of the metric name)."""
+    The first fp32 warmup step's pre-update outputs are also the parity
+    reference: the GPU model (fp32 parity mode, same weights, same batch) is
+    compared with them (the "Dice parity vs CPU ref" of the metric name)."""
     from oracle import cpu_ref as R
-    threads, affinity = _cpu_threads()
-    torch.set_num_threads(threads)
+    affinity, share = _cpu_threads()
     B = args.cpu_batch
     vae = args.model == "vae"
     x, t = synthetic(B, args.size, args.classes, 0, "cpu")
@@ -138,19 +143,23 @@ def cpu_baseline(args, dev):
         if vae:
             return R.vae_train_step(model, opt, x, t, eps)
         return R.train_step(model, opt, x, t)
+    plan = [("fp32", "fp32", affinity)]
+    if not args.cpu_no_bf16:
+        plan.append(("bf16", "bf16", affinity))
+    if share != affinity:
+        plan.append((f"fp32_{share}_threads", "fp32", share))
     legs, parity = {}, None
-    for leg in ("fp32", "bf16"):
-        if leg == "bf16" and args.cpu_no_bf16:
-            continue
+    for name, prec, threads in plan:
+        torch.set_num_threads(threads)
         model = _ref_model(args)
         opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
-        ctx = torch.autocast("cpu", dtype=torch.bfloat16) if leg == "bf16" else _Null()
+        ctx = torch.autocast("cpu", dtype=torch.bfloat16) if prec == "bf16" else _Null()
         t0 = time.perf_counter()
         with ctx:
             ref_out, ref_loss, _ = train_step(model, opt)  # warmup; pre-update outputs
         warm = time.perf_counter() - t0
-        _progress(f"cpu_baseline {leg} warmup step: {warm:.1f} s")
-        if leg == "fp32":
+        _progress(f"cpu_baseline {name} ({threads} threads) warmup step: {warm:.1f} s")
+        if parity is None and prec == "fp32":
             parity = gpu_parity(args, x, t, ref_out, ref_loss, dev, eps)
         # bounded sample: a slow host gets fewer timed steps (stated in "sample")
         n = args.cpu_steps if warm * args.cpu_steps <= args.cpu_budget_s else max(1, int(args.cpu_budget_s // warm))
@@ -158,17 +167,19 @@ def cpu_baseline(args, dev):
         with ctx:
             for i in range(n):
                 train_step(model, opt)
-                _progress(f"cpu_baseline {leg} step {i + 1}/{n}: {time.perf_counter() - t0:.1f} s")
+                _progress(f"cpu_baseline {name} step {i + 1}/{n}: {time.perf_counter() - t0:.1f} s")
         dt = time.perf_counter() - t0
-        legs[leg] = {"value": round(B * n / dt, 4), "steps": n, "s_per_step": round(dt / n, 3)}
+        legs[name] = {"value": round(B * n / dt, 4), "threads": threads, "steps": n,
+                      "s_per_step": round(dt / n, 3)}
     f = legs["fp32"]
     what = ("UNetResNet(3,1) VAE train steps (fwd+CombinedLoss+1e-3*KL+bwd+clip+AdamW)" if vae else
             f"UNet(3,{args.classes}) train steps (fwd+CombinedLoss+bwd+clip+AdamW)")
-    out = {"value": f["value"], "unit": "images/sec", "cores": threads, "kind": "port",
-           "cpu_model": _cpu_model(), "affinity_cores": affinity,
+    out = {"value": f["value"], "unit": "images/sec", "cores": affinity, "kind": "port",
+           "cpu_model": _cpu_model(), "affinity_cores": affinity, "per_gpu_share_threads": share,
            "sample": (f"1 warmup + {f['steps']} timed fp32 {what} on {B}x3x{args.size}x{args.size} "
-                      f"(oracle/cpu_ref.py, torch CPU, {threads} threads)"),
+                      f"(oracle/cpu_ref.py, torch CPU, {affinity} threads = len(sched_getaffinity))"),
            "legs": legs}
+    torch.set_num_threads(share)
     return out, parity
 
 
@@ -256,8 +267,12 @@ def main():
     if world > 1:
         # nccl = RCCL over xGMI; VU_DIST_BACKEND=gloo rehearses the N>1 path
         # with several ranks sharing one GPU (RCCL refuses duplicate devices)
-        dist.init_process_group(os.environ.get("VU_DIST_BACKEND", "nccl"), init_method="env://")
-        local = local % torch.cuda.device_count()
+        backend = os.environ.get("VU_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, init_method="env://")
+        if backend == "gloo":
+            local = local % torch.cuda.device_count()   # rehearsal: ranks share the card(s)
+        elif local >= torch.cuda.device_count():
+            raise SystemExit(f"bench: LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPUs")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -479,6 +479,17 @@ int vu_uncertainty(const float* seg, int samples, int64_t n, float* mean,
 int vu_gather_affine(const void* x, int B, int H, int W, int C, const int* map,
                      void* y, int Ho, int Wo, int dtype, void* stream);
 
+/* Patch-cache producer (IDRIDDataset.precompute_all_patches,
+ * utils/data_loading.py:370-397, and is_valid_patch :287-300): for the
+ * ny x nx windows of size P at `stride` over one scaled image img [C][H][W]
+ * fp32 and its mask [H][W] fp32, black[w] = #pixels with channel mean < 0.1
+ * (left-to-right fp32 sum / C) and lesion[w] = #mask pixels > 0.5 (int32,
+ * window w = row-major (y/stride, x/stride)).  Every window must lie inside
+ * the image (else hipErrorInvalidValue). */
+int vu_patch_stats(const float* img, int C, int H, int W, const float* mask,
+                   int P, int stride, int ny, int nx, int* black, int* lesion,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

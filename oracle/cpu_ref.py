@@ -26,6 +26,7 @@ Reference semantics restated (file:line):
   KLAnnealer / kl_with_free_bits .. utils/loss.py:114-145, 148-170
   dice_score ...................... utils/metrics.py:8-35
   train step ...................... train.py:381-411 (AdamW train.py:334)
+  patch-cache window statistics ... utils/data_loading.py:287-300, 370-397
 """
 import math
 
@@ -330,3 +331,28 @@ def vae_train_step(model, opt, x, target, eps, beta=1e-3, free_bits=1e-3, clip=1
     total = clip_grad_norm(list(model.p.values()), clip)
     opt.step()
     return (logits.detach(), mu.detach(), logvar.detach()), loss.detach(), total
+
+
+# ----------------------------------------------------------------------------
+# patch-cache producer (utils/data_loading.py:287-300 is_valid_patch,
+# 370-397 the window loop): per-window integer counts
+# ----------------------------------------------------------------------------
+def patch_window_stats(img, mask, patch, stride):
+    """img [C, H, W] float32, mask [1, H, W]; windows at stride over
+    range(0, H - patch + 1, stride) x range(0, W - patch + 1, stride) (row
+    major).  Returns (ny, nx, black, lesion): black = #pixels whose channel
+    mean (fp32 left-to-right sum, then / C, as torch's CPU mean over dim 0)
+    is < 0.1; lesion = #mask pixels > 0.5."""
+    import numpy as np
+    a = np.asarray(img, dtype=np.float32)
+    m = np.asarray(mask, dtype=np.float32)[0]
+    s = a[0].copy()
+    for k in range(1, a.shape[0]):
+        s = (s + a[k]).astype(np.float32)
+    is_black = (s / np.float32(a.shape[0])) < np.float32(0.1)
+    is_lesion = m > np.float32(0.5)
+    _, h, w = a.shape
+    ys, xs = list(range(0, h - patch + 1, stride)), list(range(0, w - patch + 1, stride))
+    black = np.array([int(is_black[y:y + patch, x:x + patch].sum()) for y in ys for x in xs], np.int64)
+    lesion = np.array([int(is_lesion[y:y + patch, x:x + patch].sum()) for y in ys for x in xs], np.int64)
+    return len(ys), len(xs), black, lesion

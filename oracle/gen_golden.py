@@ -367,6 +367,128 @@ def gen_inference():
     print("inference:", {k: v.shape for k, v in rec.items()})
 
 
+PATCH_CFG = {"patch": 64, "scale": 0.25, "seed": 1234, "lesion": "EX"}
+
+
+def _synthetic_idrid(root, seed=5):
+    """Small fundus-like JPEG images + TIF lesion masks in the reference's
+    directory layout (imgs/<split>/*.jpg, masks/<split>/EX/*_EX.tif): a bright
+    textured disc on a black background (border rejection), lesion blobs,
+    plus one image too small for the patch and one with a mismatched mask
+    (both skipped by the reference)."""
+    from PIL import Image
+    rng = np.random.Generator(np.random.PCG64(seed))
+    layout = {"train": 4, "val": 2, "test": 2}
+    for split, n in layout.items():
+        os.makedirs(os.path.join(root, "imgs", split), exist_ok=True)
+        os.makedirs(os.path.join(root, "masks", split, "EX"), exist_ok=True)
+        for i in range(n + 1):
+            H, W = (720, 1040) if i < n else ((200, 200) if split != "train" else (720, 1040))
+            yy, xx = np.mgrid[0:H, 0:W]
+            cy, cx = H / 2 + rng.uniform(-30, 30), W / 2 + rng.uniform(-60, 60)
+            r = min(H, W) * rng.uniform(0.42, 0.5)
+            disc = ((yy - cy) ** 2 + (xx - cx) ** 2) < r * r
+            base = np.stack([rng.uniform(120, 200), rng.uniform(40, 90), rng.uniform(10, 40)])
+            tex = rng.normal(0, 12, (H // 8 + 1, W // 8 + 1, 3)).repeat(8, 0).repeat(8, 1)[:H, :W]
+            img = np.clip(base[None, None, :] + tex, 0, 255) * disc[..., None]
+            # a few dark-but-not-black pixels around the 0.1 mean threshold
+            img[:, :40] = np.array([25, 26, 26])[None, None, :] * (rng.random((H, 40, 1)) < 0.5)
+            m = np.zeros((H, W), np.uint8)
+            for _ in range(int(rng.integers(2, 6))):
+                ly, lx = rng.integers(0, H), rng.integers(0, W)
+                rr = rng.uniform(6, 30)
+                m[((yy - ly) ** 2 + (xx - lx) ** 2) < rr * rr] = 255
+            name = f"IDRiD_{split}_{i:02d}"
+            Image.fromarray(img.astype(np.uint8)).save(os.path.join(root, "imgs", split, name + ".jpg"), quality=92)
+            if split == "train" and i == n:
+                m = m[:, :-8]    # mismatched mask size: skipped
+            Image.fromarray(m).save(os.path.join(root, "masks", split, "EX", f"{name}_EX.tif"))
+    return layout
+
+
+def _load_idrid_slicer():
+    """IDRIDDataset.is_valid_patch (287-300), precompute_all_patches (302-446)
+    and preprocess (580-601) plus load_image (18-28), compiled from
+    utils/data_loading.py's AST (the module imports albumentations and cv2 at
+    the top, both absent; none of these methods touches them) onto a bare
+    class: the reference's own slicing, border rejection, record format and
+    positive/negative balancing."""
+    import logging
+    import random
+    from pathlib import Path
+    from PIL import Image
+    path = os.path.join(REF, "utils", "data_loading.py")
+    tree = ast.parse(open(path).read())
+    fns = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "load_image"]
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "IDRIDDataset")
+    want = ("is_valid_patch", "precompute_all_patches", "preprocess")
+    body = [n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name in want]
+    slicer = ast.copy_location(ast.ClassDef(name="IDRIDSlicer", bases=[], keywords=[], body=body,
+                                            decorator_list=[]), cls)
+    mod = ast.fix_missing_locations(ast.Module(body=fns + [slicer], type_ignores=[]))
+    ns = {"torch": torch, "np": np, "Image": Image, "logging": logging, "os": os, "random": random,
+          "Path": Path, "tqdm": lambda it, **kw: it}
+    exec(compile(mod, path, "exec"), ns)
+    return ns["IDRIDSlicer"]
+
+
+def gen_patch_cache():
+    """Patch-cache producer fixture: the reference's own
+    precompute_all_patches run on synthetic images; stores the input FILES
+    (bytes) and, per split, the resulting patch index and every kept record's
+    coords / has_lesion / content checksums, and the files left on disk."""
+    import random
+    import tempfile
+    import zlib
+    from pathlib import Path
+    Slicer = _load_idrid_slicer()
+    rec = {}
+    with tempfile.TemporaryDirectory() as root:
+        layout = _synthetic_idrid(root)
+        files = []
+        for dp, _, fs in os.walk(root):
+            for f in sorted(fs):
+                files.append(os.path.relpath(os.path.join(dp, f), root))
+        files.sort()
+        rec["files"] = np.array(files)
+        for i, f in enumerate(files):
+            rec[f"file{i}"] = np.frombuffer(open(os.path.join(root, f), "rb").read(), np.uint8)
+        P, lt = PATCH_CFG["patch"], PATCH_CFG["lesion"]
+        for split in layout:
+            s = Slicer.__new__(Slicer)
+            s.split, s.scale, s.patch_size, s.lesion_type = split, PATCH_CFG["scale"], P, lt
+            s.is_full_image, s.skip_border_check, s.stride = False, False, P // 2
+            s.images_dir = Path(root) / "imgs" / split
+            s.masks_dir = Path(root) / "masks" / split
+            s.ids = sorted(os.path.splitext(f)[0] for f in os.listdir(s.images_dir) if f.endswith(".jpg"))
+            s.patches_dir = Path(root) / "patches" / split / lt
+            s.patches_dir.mkdir(parents=True, exist_ok=True)
+            random.seed(PATCH_CFG["seed"])
+            s.precompute_all_patches()
+            rec[f"{split}.ids"] = np.array(s.ids)
+            rec[f"{split}.index_names"] = np.array([os.path.basename(p) for _, p, _ in s.patch_indices])
+            rec[f"{split}.index_lesion"] = np.array([bool(h) for _, _, h in s.patch_indices])
+            coords, has, isum, msum, crc = [], [], [], [], []
+            for _, p, _ in s.patch_indices:
+                r = torch.load(p, weights_only=True)
+                coords.append(tuple(r["coords"]))
+                has.append(bool(r["has_lesion"]))
+                isum.append(float(r["image"].double().sum()))
+                msum.append(float(r["mask"].double().sum()))
+                crc.append(zlib.crc32(r["image"].numpy().tobytes()) ^ (zlib.crc32(r["mask"].numpy().tobytes()) << 1))
+            rec[f"{split}.coords"] = np.array(coords, np.int64).reshape(-1, 2)
+            rec[f"{split}.has_lesion"] = np.array(has)
+            rec[f"{split}.image_sum"] = np.array(isum)
+            rec[f"{split}.mask_sum"] = np.array(msum)
+            rec[f"{split}.crc"] = np.array(crc, np.int64)
+            rec[f"{split}.on_disk"] = np.array(sorted(os.listdir(s.patches_dir)))
+            print(f"patch_cache {split}: {len(s.patch_indices)} patches "
+                  f"({int(np.sum(rec[split + '.index_lesion']))} positive), {len(rec[split + '.on_disk'])} on disk")
+    for k, v in PATCH_CFG.items():
+        rec[f"cfg.{k}"] = np.array(v)
+    np.savez_compressed(os.path.join(OUT, "patch_cache.npz"), **rec)
+
+
 def gen_decoder_spatial():
     """DecoderBlock with the reference's spatial z [B, L, h, w] (not constant)."""
     DecoderBlock = _load_decoder_block()
@@ -377,7 +499,7 @@ def gen_decoder_spatial():
 if __name__ == "__main__":
     # python oracle/gen_golden.py [parts losses unet vae decoder_spatial]  (default: all)
     os.makedirs(OUT, exist_ok=True)
-    what = set(sys.argv[1:]) or {"parts", "losses", "unet", "vae", "decoder_spatial", "inference"}
+    what = set(sys.argv[1:]) or {"parts", "losses", "unet", "vae", "decoder_spatial", "inference", "patch_cache"}
     if "parts" in what:
         gen_parts()
     if "losses" in what:
@@ -393,3 +515,5 @@ if __name__ == "__main__":
             gen_vae(mode)
     if "inference" in what:
         gen_inference()
+    if "patch_cache" in what:
+        gen_patch_cache()

@@ -127,3 +127,38 @@ def infer_inputs():
         "patch_z": _rand(INFER_SEED + 6, (1, 32, 1, 1), -1.5, 1.5),
         "segs": _rand(INFER_SEED + 7, (5, 1, 12, 10), 0.0, 1.0),
     }
+
+
+# fp32 adjudication factor: the HIP fp32 path may differ from fp64 by at most
+# FP32_ERR_FACTOR x the fp32 oracle's own largest margin error (different
+# summation orders: implicit-GEMM K order, fp64-combined BN statistics vs
+# torch's CPU reductions), and a flipped pixel's fp64 margin must lie inside
+# that envelope.
+FP32_ERR_FACTOR = 4.0
+
+
+def class_margin(lg):
+    """Signed class margin: logit(1) - logit(0) for 2 classes, the logit for 1."""
+    return (lg[:, 1] - lg[:, 0]) if lg.shape[1] == 2 else lg[:, 0]
+
+
+def adjudicate_flips(tag, m_gpu, m32, m64):
+    """Class-map flips of an fp32 HIP run against the fp32 oracle, judged by
+    fp64: the HIP margin error vs fp64 must stay within FP32_ERR_FACTOR x the
+    fp32 oracle's own largest margin error, and so must the fp64 |margin| of
+    every flipped pixel.  Returns the flip count vs the fp32 oracle."""
+    e_ref = float((m32 - m64).abs().max())
+    e_gpu = float((m_gpu - m64).abs().max())
+    s_gpu, s32, s64 = m_gpu > 0, m32 > 0, m64 > 0
+    flips_ref = s_gpu != s32                 # what bench.py's parity block counts
+    flips_gpu64 = s_gpu != s64
+    flips_ref64 = s32 != s64
+    bound = FP32_ERR_FACTOR * e_ref
+    m64_at_flips = m64.abs()[flips_ref | flips_gpu64]
+    worst = float(m64_at_flips.max()) if m64_at_flips.numel() else 0.0
+    print(f"{tag}: fp32 margin error vs fp64: HIP {e_gpu:.3e}, oracle {e_ref:.3e}; flips HIP-vs-fp32-oracle "
+          f"{int(flips_ref.sum())}, HIP-vs-fp64 {int(flips_gpu64.sum())}, oracle-fp32-vs-fp64 "
+          f"{int(flips_ref64.sum())}; largest fp64 |margin| at a flip {worst:.3e} (bound {bound:.3e})")
+    assert e_gpu <= bound, (e_gpu, e_ref)
+    assert worst <= bound, (worst, bound)
+    return int(flips_ref.sum())

@@ -140,6 +140,7 @@ _SIGS = {
     "vu_blend_finish": (_i, [_p, _p, _l, _p]),
     "vu_uncertainty": (_i, [_p, _i, _l, _p, _p, _p, _p, _p, _p]),
     "vu_gather_affine": (_i, [_p, _i, _i, _i, _i, _p, _p, _i, _i, _i, _p]),
+    "vu_patch_stats": (_i, [_p, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p, _p]),
 }
 
 _lib = None

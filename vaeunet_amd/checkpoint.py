@@ -19,7 +19,7 @@ state layout, so optimizer states are interchangeable too.
 import torch
 
 
-def checkpoint_dict(model, optimizer=None, scheduler=None, grad_scaler=None, epoch=0, best_val_score=0.0,
+def checkpoint_dict(model, optimizer=None, scheduler=None, grad_scaler=None, epoch=0, best_val_score=float("-inf"),
                     global_step=0, params=None):
     """The train.py:542-565 checkpoint dictionary."""
     return {
@@ -34,7 +34,7 @@ def checkpoint_dict(model, optimizer=None, scheduler=None, grad_scaler=None, epo
     }
 
 
-def save_checkpoint(path, model, optimizer=None, scheduler=None, grad_scaler=None, epoch=0, best_val_score=0.0,
+def save_checkpoint(path, model, optimizer=None, scheduler=None, grad_scaler=None, epoch=0, best_val_score=float("-inf"),
                     global_step=0, params=None):
     ck = checkpoint_dict(model, optimizer, scheduler, grad_scaler, epoch, best_val_score, global_step, params)
     torch.save(ck, path)

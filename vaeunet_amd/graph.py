@@ -24,7 +24,11 @@ capture (rebuild the object to change them).  Single process: the data-
 parallel reducer's collectives are not captured (``bench.py`` replays only
 at world size 1).
 """
+import gc
+import weakref
+
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 from . import engine as E
@@ -41,20 +45,28 @@ class GraphedTrainStep:
         self.fb = forward_backward
         self.opt = optimizer
         self.max_norm = max_norm
-        params = [p for g in optimizer.param_groups for p in g["params"] if p.requires_grad]
-        self.params = params
+        every = [p for g in optimizer.param_groups for p in g["params"] if p.requires_grad]
         # eager warm-up: builds the weight images, optimizer state and every
         # workspace the step touches
         for _ in range(max(1, warmup)):
             self.fb()
             if max_norm is not None:
-                clip_grad_norm_(params, max_norm)
+                clip_grad_norm_([p for p in every if p.grad is not None], max_norm)
             optimizer.step()
             optimizer.zero_grad(set_to_none=True)
+        # only the parameters the step gives a gradient (those AdamW holds state
+        # for): an unused one (UNetResNet's z_initial when use_bottleneck is
+        # False) keeps .grad None, so torch's AdamW would leave it untouched too
+        params = [p for p in every if len(optimizer.state.get(p, {})) > 0]
+        if not params:
+            raise RuntimeError("GraphedTrainStep: no parameter received a gradient in the warm-up")
+        self.params = params
+        keep = set(id(p) for p in params)
         dev = params[0].device
         # persistent zero gradients (the backward accumulates into them)
         for p in params:
             p.grad = torch.zeros_like(p)
+        self.grads = [p.grad for p in params]
         self.clip_tab = _Table([(p.grad, p.grad, None, None, 0.0, 1.0) for p in params], dev)
         self.norm = torch.empty(2, dtype=torch.float32, device=dev)
         self.ws = torch.empty(max(1, self.clip_tab.nchunks), dtype=torch.float64, device=dev)
@@ -62,7 +74,7 @@ class GraphedTrainStep:
         for group in optimizer.param_groups:
             rows, step0 = [], 0.0
             for p in group["params"]:
-                if not p.requires_grad:
+                if id(p) not in keep:
                     continue
                 st = optimizer.state[p]
                 rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], 0.0, 1.0))
@@ -71,16 +83,27 @@ class GraphedTrainStep:
                 step = torch.full((1,), step0, dtype=torch.float32, device=dev)
                 self.groups.append((group, _Table(rows, dev), step))
         # images, then capture
+        self._synced = True
+        # weak: no optimizer <-> graph cycle, so a dropped GraphedTrainStep (and
+        # its CUDAGraph) is freed at once, never by a cyclic GC pass that could
+        # run while another graph is being captured
+        optimizer._vu_graph = weakref.ref(self)
+        self.moments = [t for _, tab, _ in self.groups for r in tab.keep for t in (r[2], r[3])]
         self.refresh = E.StaticRefresh(params)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         E._STATIC_REFRESH = self.refresh
+        gc_was = gc.isenabled()
+        gc.collect()
+        gc.disable()   # no collector pass (and no foreign graph destructor) mid-capture
         try:
             with torch.cuda.graph(self.graph):
                 self.loss = self.fb()
                 self._tail()
         finally:
             E._STATIC_REFRESH = None
+            if gc_was:
+                gc.enable()
         torch.cuda.synchronize()
 
     def _tail(self):
@@ -96,8 +119,17 @@ class GraphedTrainStep:
                       float(b1), float(b2), float(group["eps"]), _lib.ptr(step), 1, s)
 
     def step(self):
-        """Replay one training step; returns the (static) loss tensor."""
+        """Replay one training step; returns the (static) loss tensor.
+
+        The replay updates the parameters and moments in place behind
+        autograd's back: their version counters are bumped as torch's in-place
+        ops do, so an eager forward after it (validation, inference helpers)
+        rebuilds its derived weight images instead of reusing the ones the
+        replay started from."""
         self.graph.replay()
+        increment_version(self.params)
+        increment_version(self.moments)
+        self._synced = False
         return self.loss
 
     @property
@@ -107,9 +139,24 @@ class GraphedTrainStep:
 
     def sync_optimizer_state(self):
         """Write the device step counts back into the optimizer's state (for
-        checkpoints: train.py:542-565 saves optimizer.state_dict())."""
-        for group, _, step in self.groups:
+        checkpoints: train.py:542-565 saves optimizer.state_dict(), and before
+        any eager ``optimizer.step()`` after replays).  One host sync."""
+        for group, tab, step in self.groups:
             v = float(step.item())
-            for p in group["params"]:
-                if p.requires_grad:
-                    self.opt.state[p]["step"] = torch.tensor(v, dtype=torch.float32)
+            for r in tab.keep:
+                self.opt.state[r[0]]["step"] = torch.tensor(v, dtype=torch.float32)
+        self._synced = True
+
+    def load_optimizer_steps(self):
+        """The optimizer's (host) step counts -> the device counters the replays
+        read: after an eager ``optimizer.step()`` between replays (called by
+        FusedAdamW.step itself)."""
+        for group, tab, step in self.groups:
+            step.fill_(float(self.opt.state[tab.keep[0][0]]["step"]))
+        # the eager step consumed the captured gradient buffers without clearing
+        # them (and zero_grad may have unbound them): clear and rebind
+        with torch.no_grad():
+            for p, g in zip(self.params, self.grads):
+                g.zero_()
+                p.grad = g
+        self._synced = True

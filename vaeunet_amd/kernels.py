@@ -178,7 +178,9 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     a.ksplit = 0
     a.workspace = None
     ws = None
-    if g.R == 3 and dtype == _lib.BF16:
+    if dtype == _lib.BF16:
+        # any bf16 shape may be given split-K by the C-side selector (it returns 0
+        # when none is needed), not only the 3x3 ones
         nb = query("vu_gemm_fwd_workspace_bytes", C.byref(a), dtype)
         if nb > 0:
             ws = torch.empty(nb // 4, dtype=torch.float32, device=out.device)

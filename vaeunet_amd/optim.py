@@ -153,6 +153,10 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        ref = getattr(self, "_vu_graph", None)  # weakref to a GraphedTrainStep replaying this optimizer
+        graph = ref() if ref is not None else None
+        if graph is not None and not graph._synced:
+            graph.sync_optimizer_state()  # its replays advanced the step count on the device
         for group in self.param_groups:
             beta1, beta2 = group["betas"]
             lr = float(group["lr"])
@@ -192,4 +196,6 @@ class FusedAdamW(torch.optim.Optimizer):
             # version counters like torch's in-place ops do (derived caches,
             # e.g. the engine's bf16 weight layouts, key on them)
             increment_version([r[k] for r in rows for k in (0, 2, 3)])
+        if graph is not None:
+            graph.load_optimizer_steps()  # later replays continue from this step
         return loss
