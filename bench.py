@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-no-bf16", action="store_true", help="skip the CPU autocast-bf16 leg")
     ap.add_argument("--torch-optim", action="store_true",
                     help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
+    ap.add_argument("--overlap", action="store_true",
+                    help="weight gradients on a side stream (engine.OVERLAP_WGRAD; measured slower, A/B only)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (vaeunet_amd.graph); auto = on "
                          "at world size 1 with the fused optimizer")
@@ -90,15 +92,51 @@ def _cpu_model():
     return None
 
 
+def _cgroup_cpus():
+    """CPUs the cgroup CPU quota grants this process (cpu.max / CFS quota), or None."""
+    import math
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, math.ceil(q / p))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def _cpu_threads():
-    """(affinity, share): every core this process may run on
-    (``len(os.sched_getaffinity(0))``, BASELINE.md §4 / SURVEY.md §8d: the
-    headline CPU baseline's thread count) and the per-GPU CPU share the box's
-    launcher sets in OMP_NUM_THREADS (reported as a second, labelled leg)."""
+    """(threads, affinity, quota): the cores this process can actually run on
+    -- ``len(os.sched_getaffinity(0))``, capped by the cgroup
+    CPU quota when one is set.  On the GPU box the affinity mask lists all 256
+    host cores but cpu.max grants 16 CPUs; 256 threads then run a CPU conv 12x
+    SLOWER than 16 (profiles/r3_cpu_probe.log), so the quota is the count that
+    gives the host its best time."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    omp = os.environ.get("OMP_NUM_THREADS")
-    share = min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
-    return n, share
+    quota = _cgroup_cpus()
+    return (min(n, quota) if quota else n), n, quota
+
+
+def _thread_probe(threads, affinity):
+    """One CPU 3x3 conv (8x64x256^2) at the chosen thread count and at the full
+    affinity count: the evidence for the choice, measured in the same run."""
+    import torch.nn.functional as F
+    x = torch.randn(8, 64, 256, 256).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(64, 64, 3, 3).contiguous(memory_format=torch.channels_last)
+    out = {}
+    for t in sorted({threads, affinity}):
+        torch.set_num_threads(t)
+        F.conv2d(x, w, padding=1)
+        t0 = time.perf_counter()
+        F.conv2d(x, w, padding=1)
+        out[str(t)] = round((time.perf_counter() - t0) * 1e3, 1)
+    return {"what": "ms of one 8x64x256^2 3x3 conv (torch CPU) per thread count", "ms": out}
 
 
 def _ref_model(args):
@@ -133,7 +171,9 @@ def cpu_baseline(args, dev):
     reference: the GPU model (fp32 parity mode, same weights, same batch) is
     compared with them (the "Dice parity vs CPU ref" of the metric name)."""
     from oracle import cpu_ref as R
-    affinity, share = _cpu_threads()
+    threads, affinity, quota = _cpu_threads()
+    probe = _thread_probe(threads, affinity)
+    _progress(f"cpu_baseline thread probe: {probe['ms']}")
     B = args.cpu_batch
     vae = args.model == "vae"
     x, t = synthetic(B, args.size, args.classes, 0, "cpu")
@@ -143,11 +183,9 @@ def cpu_baseline(args, dev):
         if vae:
             return R.vae_train_step(model, opt, x, t, eps)
         return R.train_step(model, opt, x, t)
-    plan = [("fp32", "fp32", affinity)]
+    plan = [("fp32", "fp32", threads)]
     if not args.cpu_no_bf16:
-        plan.append(("bf16", "bf16", affinity))
-    if share != affinity:
-        plan.append((f"fp32_{share}_threads", "fp32", share))
+        plan.append(("bf16", "bf16", threads))
     legs, parity = {}, None
     for name, prec, threads in plan:
         torch.set_num_threads(threads)
@@ -155,7 +193,8 @@ def cpu_baseline(args, dev):
         opt = R.AdamW(model.p.values(), lr=1e-4, weight_decay=1e-5)
         ctx = torch.autocast("cpu", dtype=torch.bfloat16) if prec == "bf16" else _Null()
         t0 = time.perf_counter()
-        with ctx:
+        _progress(f"cpu_baseline {name} ({threads} threads): warmup step")
+        with ctx, _Heartbeat(f"cpu_baseline {name} warmup"):
             ref_out, ref_loss, _ = train_step(model, opt)  # warmup; pre-update outputs
         warm = time.perf_counter() - t0
         _progress(f"cpu_baseline {name} ({threads} threads) warmup step: {warm:.1f} s")
@@ -164,7 +203,7 @@ def cpu_baseline(args, dev):
         # bounded sample: a slow host gets fewer timed steps (stated in "sample")
         n = args.cpu_steps if warm * args.cpu_steps <= args.cpu_budget_s else max(1, int(args.cpu_budget_s // warm))
         t0 = time.perf_counter()
-        with ctx:
+        with ctx, _Heartbeat(f"cpu_baseline {name} timed steps"):
             for i in range(n):
                 train_step(model, opt)
                 _progress(f"cpu_baseline {name} step {i + 1}/{n}: {time.perf_counter() - t0:.1f} s")
@@ -174,18 +213,44 @@ def cpu_baseline(args, dev):
     f = legs["fp32"]
     what = ("UNetResNet(3,1) VAE train steps (fwd+CombinedLoss+1e-3*KL+bwd+clip+AdamW)" if vae else
             f"UNet(3,{args.classes}) train steps (fwd+CombinedLoss+bwd+clip+AdamW)")
-    out = {"value": f["value"], "unit": "images/sec", "cores": affinity, "kind": "port",
-           "cpu_model": _cpu_model(), "affinity_cores": affinity, "per_gpu_share_threads": share,
+    out = {"value": f["value"], "unit": "images/sec", "cores": threads, "kind": "port",
+           "cpu_model": _cpu_model(), "affinity_cores": affinity, "cgroup_cpu_quota": quota,
+           "cores_basis": ("len(sched_getaffinity) capped by the cgroup cpu.max quota" if quota and quota < affinity
+                           else "len(sched_getaffinity)"),
+           "thread_probe": probe,
            "sample": (f"1 warmup + {f['steps']} timed fp32 {what} on {B}x3x{args.size}x{args.size} "
-                      f"(oracle/cpu_ref.py, torch CPU, {affinity} threads = len(sched_getaffinity))"),
+                      f"(oracle/cpu_ref.py, torch CPU, {threads} threads)"),
            "legs": legs}
-    torch.set_num_threads(share)
     return out, parity
 
 
 def _progress(msg):
     """Progress of the long CPU legs on stderr (the JSON line stays the only stdout line)."""
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+class _Heartbeat:
+    """A stderr line every `every` seconds while a long CPU leg runs (a single
+    CPU step can outlast the GPU runner's silence limit)."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+        self.what, self.every = what, every
+        self.stop = threading.Event()
+        self.t0 = time.perf_counter()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(self.every):
+            _progress(f"{self.what}: {time.perf_counter() - self.t0:.0f} s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+        return False
 
 
 class _Null:
@@ -276,8 +341,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from vaeunet_amd import UNet, kernels as K
+    from vaeunet_amd import UNet, kernels as K, engine as E
     from vaeunet_amd.init import seeded_init_
+    if args.overlap:
+        E.OVERLAP_WGRAD = True
     from vaeunet_amd.loss import CombinedLoss
     from vaeunet_amd import parallel
 
@@ -403,7 +470,8 @@ def main():
                                         "+clip+AdamW), random-init weights"),
                            "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
                            "global_batch": args.batch * world, "parallelism": f"dp{world}",
-                           "execution": "hipgraph-replay" if graphed is not None else "eager"},
+                           "execution": "hipgraph-replay" if graphed is not None else "eager",
+                           "wgrad_side_stream": bool(E.OVERLAP_WGRAD)},
                 "loss": round(float(loss.item()), 6),
                 "roofline": roof, "cpu_baseline": cpu, "parity": parity}
         print(json.dumps(line), flush=True)

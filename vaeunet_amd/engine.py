@@ -22,6 +22,63 @@ from . import kernels as K
 from ._lib import BF16, F32
 
 
+# Weight gradients on a side HIP stream: in every backward the weight-gradient
+# GEMM of a layer (and its slab reduce / bias sums) depends only on that
+# layer's output gradient and input activation, not on the input-gradient chain
+# (dgrad -> BatchNorm backward -> next dgrad) the main stream walks, so it is
+# forked onto a second stream and joined once at the end of the block's
+# backward.  The GPU then fills CUs left idle by small grids and kernel tails,
+# and co-schedules memory-bound BatchNorm passes with MFMA-bound GEMMs where
+# registers and LDS allow (a captured HIP graph keeps the fork/join as
+# parallel branches).  Measured SLOWER on MI355X (same-box A/B,
+# profiles/r3_ab_wgrad_overlap.log: UNet 500.4 -> 491.5, VAE 722.2 -> 687.3
+# img/s): the 3x3 GEMMs hold 230-256 VGPRs x 8 waves, so nothing co-resides
+# with them and the extra graph edges cost more than the tails they fill.
+# Off by default; module-level switch for A/B runs (bench.py --overlap).
+OVERLAP_WGRAD = False
+
+
+class SideStream:
+    """One side stream per device; ``run`` forks it from the current stream,
+    enqueues ``fn`` on it and keeps the tensors the side work reads alive
+    until ``join`` (the caching allocator would otherwise hand their blocks
+    to the main stream while the side stream still reads them)."""
+
+    _per_device = {}
+
+    def __init__(self, device):
+        self.stream = torch.cuda.Stream(device=device)
+        self.keep = []
+        self.pending = False
+
+    @classmethod
+    def get(cls, device):
+        key = torch.device(device).index
+        if key not in cls._per_device:
+            cls._per_device[key] = cls(device)
+        return cls._per_device[key]
+
+    def run(self, fn, keep):
+        self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
+        with torch.cuda.stream(self.stream):
+            r = fn()
+        self.keep.extend(keep)
+        self.pending = True
+        return r
+
+    def join(self):
+        if self.pending:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+            self.keep = []
+            self.pending = False
+
+
+def join_side():
+    """Join every device's side stream into its current stream (end of a backward)."""
+    for side in SideStream._per_device.values():
+        side.join()
+
+
 class Mode:
     """Per-call execution mode: storage dtype and training flag."""
 
@@ -30,6 +87,18 @@ class Mode:
         self.tdtype = torch.bfloat16 if dtype_code == BF16 else torch.float32
         self.device = device
         self.grad_ready = grad_ready
+        self.ov = SideStream.get(device) if OVERLAP_WGRAD else None
+
+    def side(self, fn, *keep):
+        """Run ``fn`` (weight-gradient launches) on the side stream, reading
+        the tensors ``keep``; inline when overlap is off."""
+        if self.ov is None:
+            return fn()
+        return self.ov.run(fn, keep)
+
+    def join(self):
+        if self.ov is not None:
+            self.ov.join()
 
     def act(self, N, Cc, H, W):
         return K.empty_act(N, Cc, H, W, self.tdtype, self.device)
@@ -38,8 +107,16 @@ class Mode:
         return K.zeros_act(N, Cc, H, W, self.tdtype, self.device)
 
     def notify(self, params):
-        if self.grad_ready is not None:
-            self.grad_ready([p for p in params if p is not None and p.grad is not None])
+        """Tell the DP reducer these gradients are final.  Its collectives wait
+        on the stream current at the call, so with overlap on the call is made
+        on the side stream, behind the weight-gradient launches."""
+        if self.grad_ready is None:
+            return
+        ready = lambda: self.grad_ready([p for p in params if p is not None and p.grad is not None])  # noqa: E731
+        if self.ov is None or torch.cuda.current_stream(self.ov.stream.device) == self.ov.stream:
+            ready()
+        else:
+            self.ov.run(ready, ())
 
 
 _FP16_WARNED = False
@@ -333,8 +410,11 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     multiple; the caller reads the real channels only."""
     y, coef = saved
     dy = bn_bwd(da, y, coef, bn, True, M)
-    wgrad3x3(dy, srcs, conv.weight, M, cvalid)
-    M.notify([conv.weight, bn.weight, bn.bias])
+
+    def wg():
+        wgrad3x3(dy, srcs, conv.weight, M, cvalid)
+        M.notify([conv.weight, bn.weight, bn.bias])
+    M.side(wg, dy, *srcs)
     if not need_dsrc:
         return None
     N, _, H, W = y.shape
@@ -469,12 +549,15 @@ def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
            K.ptr(gbp), 1 if accp else 0, K.ptr(ws), M.d, K.stream())
     dug = bn_bwd(ds, ug, cg, bng, False, M)
     dux = bn_bwd(ds, ux, cx, bnx, False, M)
-    wgrad1x1(dug, [g], wg.weight, M)
-    bias_grad(dug, wg.bias, M)
-    wgrad1x1(dux, [x], wx.weight, M)
-    bias_grad(dux, wx.bias, M)
-    M.notify([wg.weight, wg.bias, wx.weight, wx.bias, wp.weight, wp.bias, bng.weight, bng.bias,
-              bnx.weight, bnx.bias, bnp.weight, bnp.bias])
+
+    def wgs():
+        wgrad1x1(dug, [g], wg.weight, M)
+        bias_grad(dug, wg.bias, M)
+        wgrad1x1(dux, [x], wx.weight, M)
+        bias_grad(dux, wx.bias, M)
+        M.notify([wg.weight, wg.bias, wx.weight, wx.bias, wp.weight, wp.bias, bng.weight, bng.bias,
+                  bnx.weight, bnx.bias, bnp.weight, bnp.bias])
+    M.side(wgs, dug, dux, g, x)
     # input gradients of the two 1x1 convs
     if dg_out is not None:
         dst, coff = dg_out
@@ -539,12 +622,14 @@ def up_bwd(M, mod, saved, dout):
             K.upsample_bwd(du, duf, uh, uw, py, px, False, M.d)
             du, py, px = duf, 0, 0
             H, W = uh, uw
-        g, acc = grad_sink(mod.up.weight)
-        if g is not None:
-            K.gemm_wgrad(K.gather1x1([x1]), K.gather_convT(du, N, h, w, py, px), x1.shape[1], 4 * cu,
-                         g, convT_layout(g), M.d, acc)
-        bias_grad(du, mod.up.bias, M, window=(py, px, uh, uw))
-        M.notify([mod.up.weight, mod.up.bias])
+        def wgt(du=du, H=H, W=W, py=py, px=px):
+            g, acc = grad_sink(mod.up.weight)
+            if g is not None:
+                K.gemm_wgrad(K.gather1x1([x1]), K.gather_convT(du, N, h, w, py, px), x1.shape[1], 4 * cu,
+                             g, convT_layout(g), M.d, acc)
+            bias_grad(du, mod.up.bias, M, window=(py, px, uh, uw))
+            M.notify([mod.up.weight, mod.up.bias])
+        M.side(wgt, du, x1, dcat)
         dx1 = torch.empty_like(x1)
         K.gemm_fwd(K.gather_convT(du, N, h, w, py, px), wT_dgrad(mod.up.weight, M.d), x1.shape[1],
                    dx1, M.d)

@@ -34,6 +34,7 @@ class BlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *douts):
         grads = ctx.runner.bwd(ctx.state, douts if len(douts) > 1 else douts[0])
+        E.join_side()   # weight gradients forked onto the side stream are complete after this point
         ctx.state = None
         return (None, None) + tuple(grads) + (None,) * ctx.n_params
 

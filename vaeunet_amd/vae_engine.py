@@ -44,13 +44,16 @@ def conv_fwd(M, srcs, conv, stats, cin_pad=None):
 
 
 def conv_wgrad(M, dy, srcs, conv, cvalid=None):
-    gw, acc = E.grad_sink(conv.weight)
-    if gw is not None:
-        g, _, _ = conv_gather(srcs, conv)
-        K.gemm_wgrad(K.gather1x1([dy]), g, dy.shape[1], g.R * g.S * g.C, gw, E.conv_layout(gw), M.d,
-                     acc, cvalid=cvalid)
-    if conv.bias is not None:
-        E.bias_grad(dy, conv.bias, M)
+    """Weight (and bias) gradient, forked onto the side stream (engine.OVERLAP_WGRAD)."""
+    def wg():
+        gw, acc = E.grad_sink(conv.weight)
+        if gw is not None:
+            g, _, _ = conv_gather(srcs, conv)
+            K.gemm_wgrad(K.gather1x1([dy]), g, dy.shape[1], g.R * g.S * g.C, gw, E.conv_layout(gw), M.d,
+                         acc, cvalid=cvalid)
+        if conv.bias is not None:
+            E.bias_grad(dy, conv.bias, M)
+    M.side(wg, dy, *srcs)
 
 
 def _parity_w(w, py, px, p, d):
