@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-no-bf16", action="store_true", help="skip the CPU autocast-bf16 leg")
     ap.add_argument("--torch-optim", action="store_true",
                     help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
+    ap.add_argument("--engine-flag", action="append", default=[], metavar="NAME=0|1",
+                    help="set a vaeunet_amd.engine module switch (A/B runs), e.g. FUSE_BN_BWD_REDUCE=0")
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a side stream (engine.OVERLAP_WGRAD; measured slower, A/B only)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
@@ -345,6 +347,11 @@ def main():
     from vaeunet_amd.init import seeded_init_
     if args.overlap:
         E.OVERLAP_WGRAD = True
+    for kv in args.engine_flag:
+        name, val = kv.split("=")
+        if not hasattr(E, name):
+            raise SystemExit(f"bench: no engine switch {name}")
+        setattr(E, name, bool(int(val)))
     from vaeunet_amd.loss import CombinedLoss
     from vaeunet_amd import parallel
 
@@ -471,7 +478,8 @@ def main():
                            "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
                            "global_batch": args.batch * world, "parallelism": f"dp{world}",
                            "execution": "hipgraph-replay" if graphed is not None else "eager",
-                           "wgrad_side_stream": bool(E.OVERLAP_WGRAD)},
+                           "wgrad_side_stream": bool(E.OVERLAP_WGRAD),
+                           "bn_bwd_reduce_in_dgrad_epilogue": bool(E.FUSE_BN_BWD_REDUCE)},
                 "loss": round(float(loss.item()), 6),
                 "roofline": roof, "cpu_baseline": cpu, "parity": parity}
         print(json.dumps(line), flush=True)

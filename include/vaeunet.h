@@ -73,6 +73,25 @@ typedef struct VuGemmFwd {
   int32_t accumulate;  /* out += result (gradient accumulation) */
   int32_t ksplit;      /* set by the library (split-K ways); callers pass 0 */
   float* workspace;    /* fp32 split-K slabs, vu_gemm_fwd_workspace_bytes() */
+  /* Optional BatchNorm-backward partial sums of the OUTPUT (an input gradient
+   * that feeds the backward of a train-mode BatchNorm(+ReLU) over bnb_x, the
+   * BN's pre-normalisation input, same shape as the output, bnb_xstride
+   * elements per pixel): for output row tile r of vu_gemm_fwd_bnb_tile()
+   * pixels and channel c (ncol = C, out_coff 0, no accumulate),
+   *   bnb_part[(2r + 0) * ncol + c] = sum dz,
+   *   bnb_part[(2r + 1) * ncol + c] = sum dz * (x - bnb_mean[c]) * bnb_invstd[c],
+   *   dz = stored output * (x * bnb_scale[c] + bnb_shift[c] > 0 if bnb_relu)
+   * -- what vu_bn_bwd_reduce's first stage computes, finished by
+   * vu_bn_bwd_finish.  bnb_part = NULL: not requested. */
+  const void* bnb_x;
+  int64_t bnb_xstride;
+  const float* bnb_scale;
+  const float* bnb_shift;
+  const float* bnb_mean;
+  const float* bnb_invstd;
+  float* bnb_part;
+  int32_t bnb_relu;
+  int32_t bnb_pad_;
 } VuGemmFwd;
 
 /* Weight-gradient GEMM: out[s][i][j] = sum_{m in split s} P[m][i] * Q[m][j]
@@ -89,6 +108,11 @@ typedef struct VuGemmWgrad {
 /* ---- GEMM family ------------------------------------------------------ */
 int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream);
 int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype);  /* BM used */
+/* Pixels per BatchNorm-backward partial row tile when the kernel the
+ * dispatcher picks for this problem can emit bnb_part (bf16, 3x3 stride-1
+ * kernels: the resident-weight 64 -> 64 kernel and the ping-pong kernel incl.
+ * its split-K finish), else 0 (the caller then runs vu_bn_bwd_reduce). */
+int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype);
 /* bytes of args->workspace the dispatcher needs for this problem (0 = none):
  * the split-K slabs of the 3x3 kernel when its grid is under one block per CU */
 int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype);
@@ -132,6 +156,17 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 #define VU_TUNE_V2_SMALL 9
 #define VU_TUNE_V5 10
 #define VU_TUNE_V6 11
+/*   VU_TUNE_GEN: highest kernel generation the GEMM dispatchers may pick
+ *     (1 = generic only ... 4 = all, the default);
+ *   VU_TUNE_SLAB4: 0 = scalar split-K slab reduce (default 1 = vectorised);
+ *   VU_TUNE_V2_CFG: tile configuration of short-K v2 GEMMs (0 default, 1, 2);
+ *   VU_TUNE_BN_NT_MB: streamed-tensor size (MB) from which the BatchNorm
+ *     passes use non-temporal loads (default 32; -1 = never).
+ * The library reads no environment variables: these are the only knobs. */
+#define VU_TUNE_GEN 12
+#define VU_TUNE_SLAB4 13
+#define VU_TUNE_V2_CFG 14
+#define VU_TUNE_BN_NT_MB 15
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */
@@ -233,6 +268,13 @@ int vu_bn_bwd_reduce(const void* dy, int64_t dy_stride, const void* x,
                      int train, float* dgamma, float* dbeta, int accumulate,
                      float* coef, float* workspace, int dtype, void* stream);
 /* dx = k1*dz + k2*(x-mean) + k3 (+ add) */
+/* Second stage of vu_bn_bwd_reduce over partials a GEMM epilogue wrote
+ * (VuGemmFwd.bnb_part, nblk row tiles): dgamma, dbeta and the apply
+ * coefficients coef [3][C], exactly as vu_bn_bwd_reduce. */
+int vu_bn_bwd_finish(const float* part, int nblk, int64_t P, int C,
+                     const float* gamma, const float* invstd, int train,
+                     float* dgamma, float* dbeta, int accumulate, float* coef,
+                     void* stream);
 int vu_bn_bwd_apply(const void* dy, int64_t dy_stride, const void* x,
                     int64_t x_stride, int64_t P, int C, const float* scale,
                     const float* shift, const float* mean, const float* coef,

@@ -39,7 +39,10 @@ class VuGemmFwd(C.Structure):
                 ("out_coff", C.c_int32), ("oH", C.c_int32), ("oW", C.c_int32),
                 ("opy", C.c_int32), ("opx", C.c_int32), ("cout", C.c_int32),
                 ("bias", _p), ("stat_sum", _p), ("stat_m2", _p), ("accumulate", C.c_int32),
-                ("ksplit", C.c_int32), ("workspace", _p)]
+                ("ksplit", C.c_int32), ("workspace", _p),
+                ("bnb_x", _p), ("bnb_xstride", _l), ("bnb_scale", _p), ("bnb_shift", _p),
+                ("bnb_mean", _p), ("bnb_invstd", _p), ("bnb_part", _p), ("bnb_relu", C.c_int32),
+                ("bnb_pad_", C.c_int32)]
 
 
 class VuGemmWgrad(C.Structure):
@@ -70,6 +73,8 @@ _SIGS = {
     "vu_gemm_fwd": (_i, [C.POINTER(VuGemmFwd), _i, _p]),
     "vu_gemm_fwd_row_tile": (_l, [C.POINTER(VuGemmFwd), _i]),
     "vu_gemm_fwd_workspace_bytes": (_l, [C.POINTER(VuGemmFwd), _i]),
+    "vu_gemm_fwd_bnb_tile": (_l, [C.POINTER(VuGemmFwd), _i]),
+    "vu_bn_bwd_finish": (_i, [_p, _i, _l, _i, _p, _p, _i, _p, _p, _i, _p, _p]),
     "vu_gemm_wgrad": (_i, [C.POINTER(VuGemmWgrad), _i, _p]),
     "vu_gemm_wgrad_tile": (_i, [C.POINTER(VuGemmWgrad), _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vu_gemm_set_tuning": (_i, [_i, _i]),

@@ -510,12 +510,10 @@ inline unsigned chan_grid(int64_t P, int C, int maxblk) {
 // them out leaves it to the smaller tensors.  Same-box A/B
 // (profiles/r2_ab_bn_nt.log): UNet 483 -> 491 img/s for any threshold of
 // 0-128 MB; VAE 708 at -1 (never), 701-703 at 0 (always), 708 at 32 MB.
-// Threshold in MB per streamed tensor (VU_BN_NT_MB overrides, for A/B runs).
+// Threshold in MB per streamed tensor (VU_TUNE_BN_NT_MB, for A/B runs; -1 = never).
+int g_bn_nt_mb = 32;
 inline bool bn_nt(int64_t P, int C, int esize) {
-  static const int64_t mb = [] {
-    const char* e = getenv("VU_BN_NT_MB");
-    return (int64_t)(e ? atoi(e) : 32);
-  }();
+  const int64_t mb = g_bn_nt_mb;
   return mb >= 0 && P * C * esize >= mb * 1000000;
 }
 
@@ -550,6 +548,14 @@ int launch_partial(const RedArgs& r, hipStream_t st, int& nblk) {
 }
 
 }  // namespace
+
+int bn_tune(int key, int value) {
+  if (key == VU_TUNE_BN_NT_MB) {
+    g_bn_nt_mb = value;
+    return 0;
+  }
+  return -1;
+}
 
 extern "C" int64_t vu_reduce_workspace_bytes(int64_t P, int C) {
   (void)P;
@@ -628,6 +634,15 @@ extern "C" int vu_bn_bwd_reduce(const void* dy, int64_t dys, const void* x, int6
   if (rc) return rc;
   hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, C, P,
                      gamma, invstd, dgamma, dbeta, accumulate, coef, train);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_bn_bwd_finish(const float* part, int nblk, int64_t P, int C, const float* gamma,
+                                const float* invstd, int train, float* dgamma, float* dbeta, int accumulate,
+                                float* coef, void* stream) {
+  if (nblk < 1 || C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, (hipStream_t)stream, part, nblk,
+                     C, P, gamma, invstd, dgamma, dbeta, accumulate, coef, train);
   return (int)hipGetLastError();
 }
 

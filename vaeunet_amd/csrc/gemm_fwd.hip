@@ -341,33 +341,18 @@ int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd5.hip (persist
 int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd6.hip (64 -> 64 3x3, resident weights)
 int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v6_bnb_tile(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v4_bnb_tile(const VuGemmFwd& p, int dtype);
 
-static bool use_v2(int dtype) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("VU_GEMM_V2");
-    mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return mode == 1 && dtype == VU_BF16;
-}
+// Highest kernel generation the dispatchers may pick (vu_gemm_set_tuning
+// VU_TUNE_GEN; tests and A/B runs only -- no environment lookups in the
+// library): 1 = generic kernels only, 2 = + LDS-DMA tiles / 1x1 streams,
+// 3 = + halo kernels, 4 (default) = + ping-pong / resident-weight kernels.
+int g_tune_gen = 4;
 
-static bool use_v3(int dtype) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("VU_GEMM_V3");
-    mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return mode == 1 && use_v2(dtype);
-}
-
-static bool use_v4(int dtype) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("VU_GEMM_V4");
-    mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return mode == 1 && use_v3(dtype);
-}
+static bool use_v2(int dtype) { return g_tune_gen >= 2 && dtype == VU_BF16; }
+static bool use_v3(int dtype) { return g_tune_gen >= 3 && use_v2(dtype); }
+static bool use_v4(int dtype) { return g_tune_gen >= 4 && use_v3(dtype); }
 
 extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype)) {
@@ -404,8 +389,19 @@ extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype)
   return 0;
 }
 
+// The BatchNorm-backward partial tile of the kernel the dispatcher below picks
+// (it must mirror the dispatch order), 0 when that kernel cannot emit them.
+extern "C" int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype) {
+  if (use_v2(dtype) && (conv_image_bm(*args, dtype) || conv_stem_bm(*args, dtype) || gemm_stream_bm(*args, dtype)))
+    return 0;
+  if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return gemm_fwd_v6_bnb_tile(*args, dtype);
+  if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_bnb_tile(*args, dtype);
+  return 0;
+}
+
 extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   const VuGather& g = args->a;
+  if (args->bnb_part && vu_gemm_fwd_bnb_tile(args, dtype) == 0) return (int)hipErrorInvalidValue;
   int epc = dtype == VU_BF16 ? 8 : 4;
   if (g.C % epc != 0 || g.nsrc < 1 || g.nsrc > 3) return (int)hipErrorInvalidValue;
   for (int t = 0; t < g.nsrc; ++t)

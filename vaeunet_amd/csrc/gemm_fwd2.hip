@@ -309,15 +309,12 @@ int launch_ns(const VuGemmFwd& p, hipStream_t st) {
 // Tile configuration for short-K problems (<= 2 K steps of 64), where a
 // block's life is dominated by its load latency and epilogue: 0 = 256-row
 // tiles, 1 = 128-row tiles (8 waves), 2 = 128-row tiles (4 waves).
+}  // namespace
+int g_v2_cfg = 0;  // VU_TUNE_V2_CFG (A/B runs): the configuration short-K problems get
+namespace {
 int v2_cfg(const VuGemmFwd& p) {
-  static int mode = -1, all = 0;
-  if (mode < 0) {
-    const char* e = getenv("VU_V2_CFG");
-    mode = e ? atoi(e) : 0;
-    all = getenv("VU_V2_CFG_ALL") != nullptr;
-  }
   const int nk = (p.a.R * p.a.S * p.a.C + 63) / 64;
-  return nk <= 2 || all ? mode : 0;
+  return nk <= 2 ? g_v2_cfg : 0;
 }
 
 }  // namespace

@@ -80,7 +80,7 @@ VU_DEV float ror_add(float v) {
 }
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
-template <int BN, bool SPLIT>
+template <int BN, bool SPLIT, bool BNB>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -360,6 +360,31 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       pk[i][j][0] = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
       pk[i][j][1] = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
     }
+  // BatchNorm-backward partials (bnb_part) are taken in the staged-row layout
+  // below: a lane holds channels (lane & 7) * 8 .. +7 of the wave's 64 for
+  // pixels q * 8 + (lane >> 3) of each 32-pixel row h.  The BN input x of
+  // those 16 pixels is loaded now (all 16 loads in flight at once) and
+  // consumed row by row.
+  constexpr bool bnb = BNB;
+  const int bc = n0 + wn * 64 + (lane & 7) * 8;
+  float bsc[8], bsf[8], bmu[8], bis[8], bs0[8], bs1[8];
+  u32x4 bx[2][4];  // rows h (even/odd): row h + 1 is loaded while row h is used
+  const bf16_t* xr = nullptr;
+  if (bnb) {
+    xr = reinterpret_cast<const bf16_t*>(ep->bnb_x) + bc +
+         (((int64_t)img * H + y0 + wm * 4) * W + x0 + (lane >> 3)) * ep->bnb_xstride;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bx[0][q] = *reinterpret_cast<const u32x4*>(xr + (int64_t)q * 8 * ep->bnb_xstride);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = ep->bnb_scale[bc + e];
+      bsf[e] = ep->bnb_shift[bc + e];
+      bmu[e] = ep->bnb_mean[bc + e];
+      bis[e] = ep->bnb_invstd[bc + e];
+      bs0[e] = 0.f;
+      bs1[e] = 0.f;
+    }
+  }
   // the main-loop buffers are free once every wave is past its last fragment read
   __syncthreads();
   // fragments 2h and 2h+1 are the 32 pixels of tile row wm*4 + h
@@ -380,6 +405,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     for (int q = 0; q < 4; ++q) {
       const int e = q * 64 + lane;
       v[q] = *reinterpret_cast<const u32x4*>(stg + (e >> 3) * SPITCH + (e & 7) * 16);
+    }
+    if (bnb && h + 1 < 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bx[(h + 1) & 1][q] =
+            *reinterpret_cast<const u32x4*>(xr + ((int64_t)(h + 1) * W + q * 8) * ep->bnb_xstride);
     }
     bf16_t* const orow = orow0 + h * orow_y;
     if (ep->accumulate) {
@@ -403,6 +434,40 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     for (int q = 0; q < 4; ++q) {
       const int e = q * 64 + lane;
       *reinterpret_cast<u32x4*>(orow + (e >> 3) * ep->out_stride + (e & 7) * 8) = v[q];
+    }
+    if (bnb) {
+      // dz = stored output, masked by the forward ReLU; sums as vu_bn_bwd_reduce
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            const int e = 2 * w + hf;
+            const float xv = __uint_as_float(hf ? (bx[h & 1][q][w] & 0xffff0000u) : (bx[h & 1][q][w] << 16));
+            float dz = __uint_as_float(hf ? (v[q][w] & 0xffff0000u) : (v[q][w] << 16));
+            if (ep->bnb_relu && !(xv * bsc[e] + bsf[e] > 0.f)) dz = 0.f;
+            bs0[e] += dz;
+            bs1[e] += dz * ((xv - bmu[e]) * bis[e]);
+          }
+    }
+  }
+  if (bnb) {
+    // lanes sharing (lane & 7) hold the same 8 channels: fold over lane bits 3-5
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        bs0[e] += __shfl_xor(bs0[e], o, 64);
+        bs1[e] += __shfl_xor(bs1[e], o, 64);
+      }
+    }
+    if (lane < 8) {
+      float* pr = ep->bnb_part + (int64_t)(mt * WM + wm) * 2 * ep->ncol + bc;
+      *reinterpret_cast<f32x4*>(pr) = f32x4{bs0[0], bs0[1], bs0[2], bs0[3]};
+      *reinterpret_cast<f32x4*>(pr + 4) = f32x4{bs0[4], bs0[5], bs0[6], bs0[7]};
+      *reinterpret_cast<f32x4*>(pr + ep->ncol) = f32x4{bs1[0], bs1[1], bs1[2], bs1[3]};
+      *reinterpret_cast<f32x4*>(pr + ep->ncol + 4) = f32x4{bs1[4], bs1[5], bs1[6], bs1[7]};
     }
   }
 }
@@ -477,6 +542,41 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
       for (int e = 0; e < 8; ++e) o.set(e, old.get(e) + v[q][e]);
     }
     o.store(dst);
+  }
+  if (p.bnb_part) {
+    // BatchNorm-backward partials of this 128-row tile (see VuGemmFwd.bnb_part)
+    float s0[8], s1[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t m = (int64_t)rb * 128 + rs + 32 * q;
+      Vec8<bf16_t> xq;
+      xq.load(reinterpret_cast<const bf16_t*>(p.bnb_x) + m * p.bnb_xstride + c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xv = xq.get(e);
+        float dz = v[q][e];
+        if (p.bnb_relu && !(xv * p.bnb_scale[c0 + e] + p.bnb_shift[c0 + e] > 0.f)) dz = 0.f;
+        s0[e] += dz;
+        s1[e] += dz * ((xv - p.bnb_mean[c0 + e]) * p.bnb_invstd[c0 + e]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[rs][cg * 8 + e] = k ? s1[e] : s0[e];
+      __syncthreads();
+      if (rs == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float sm = 0.f;
+          for (int r = 0; r < 32; ++r) sm += red[r][cg * 8 + e];
+          p.bnb_part[((int64_t)rb * 2 + k) * p.ncol + c0 + e] = sm;
+        }
+      }
+      __syncthreads();
+    }
   }
   if (!p.stat_sum) return;
   // two-pass (sum, centered M2) of the 128 rows of each column
@@ -604,14 +704,17 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
   if (ks <= 1) {
     VuGemmFwd q = p;
     q.ksplit = 1;
-    hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+    if (p.bnb_part)
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+    else
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     return (int)hipGetLastError();
   }
   const dim3 grid((unsigned)(tiles * ks));
   if (!p.workspace) return (int)hipErrorInvalidValue;
   VuGemmFwd q = p;
   q.ksplit = ks;
-  hipLaunchKernelGGL((conv3x3_pp_kernel<BN, true>), grid, dim3(512), 0, st, q);
+  hipLaunchKernelGGL((conv3x3_pp_kernel<BN, true, false>), grid, dim3(512), 0, st, q);
   const int64_t M = (int64_t)g.N * g.H * g.W;
   hipLaunchKernelGGL(splitk_finish_kernel, dim3((unsigned)((M / 128) * (p.ncol / 64))), dim3(256), 0, st, q);
   return (int)hipGetLastError();
@@ -639,6 +742,15 @@ bool operands_ok(const VuGemmFwd& p, int dtype) {
 // statistics come per 128 pixels (one wave tile, or one finish-kernel tile).
 int gemm_fwd_v4_bm(const VuGemmFwd& p, int dtype) {
   return operands_ok(p, dtype) && plan(p).bn ? 128 : 0;
+}
+
+// BatchNorm-backward partial row tile (128: one wave tile, or one finish
+// tile) when the ping-pong kernel serves the problem and its output is a
+// whole plain tensor (no accumulate, no channel offset), else 0.
+int gemm_fwd_v4_bnb_tile(const VuGemmFwd& p, int dtype) {
+  if (!gemm_fwd_v4_bm(p, dtype) || p.accumulate || p.out_coff != 0) return 0;
+  if (p.bnb_xstride % 8 != 0) return 0;
+  return 128;
 }
 
 // fp32 split-K slab bytes the ping-pong kernel needs for this problem (0 = none)
@@ -673,6 +785,10 @@ int gemm_stream_tune(int key, int value);  // gemm_stream.hip
 int gemm_fwd_v2_tune(int key, int value);  // gemm_fwd2.hip
 int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
 int gemm_fwd_v6_tune(int key, int value);  // gemm_fwd6.hip
+int bn_tune(int key, int value);           // bn.hip
+extern int g_tune_gen;                     // gemm_fwd.hip
+extern int g_tune_slab4;                   // gemm_wgrad.hip
+extern int g_v2_cfg;                       // gemm_fwd2.hip
 
 extern "C" int vu_gemm_set_tuning(int key, int value) {
   if (key == VU_TUNE_V4_MIN_BLOCKS) {
@@ -687,8 +803,22 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
     g_split_min_chunks = value;
     return 0;
   }
+  if (key == VU_TUNE_GEN) {
+    if (value < 1 || value > 4) return (int)hipErrorInvalidValue;
+    g_tune_gen = value;
+    return 0;
+  }
+  if (key == VU_TUNE_SLAB4) {
+    g_tune_slab4 = value;
+    return 0;
+  }
+  if (key == VU_TUNE_V2_CFG) {
+    if (value < 0 || value > 2) return (int)hipErrorInvalidValue;
+    g_v2_cfg = value;
+    return 0;
+  }
   if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0 || gemm_fwd_v2_tune(key, value) == 0 ||
-      gemm_fwd_v5_tune(key, value) == 0 || gemm_fwd_v6_tune(key, value) == 0)
+      gemm_fwd_v5_tune(key, value) == 0 || gemm_fwd_v6_tune(key, value) == 0 || bn_tune(key, value) == 0)
     return 0;
   return (int)hipErrorInvalidValue;
 }

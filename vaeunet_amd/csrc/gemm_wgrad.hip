@@ -356,23 +356,9 @@ int gemm_wgrad_v2_launch(const VuGemmWgrad& p, hipStream_t st);
 int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj);
 int gemm_wgrad_v3_launch(const VuGemmWgrad& p, hipStream_t st);
 
-static bool use_v2w(int dtype) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("VU_GEMM_V2");
-    mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return mode == 1 && dtype == VU_BF16;
-}
-
-static bool use_v3w(int dtype) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("VU_GEMM_V3");
-    mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return mode == 1 && use_v2w(dtype);
-}
+extern int g_tune_gen;  // gemm_fwd.hip (VU_TUNE_GEN)
+static bool use_v2w(int dtype) { return g_tune_gen >= 2 && dtype == VU_BF16; }
+static bool use_v3w(int dtype) { return g_tune_gen >= 3 && use_v2w(dtype); }
 
 // Output tile the dispatcher will use (host split-K heuristic).  Returns the
 // kernel generation: 3 = halo kernel (splits must be whole 128-pixel tiles),
@@ -403,10 +389,8 @@ extern "C" int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream) {
   return dtype == VU_BF16 ? dispatch_wg<bf16_t>(*args, st) : dispatch_wg<float>(*args, st);
 }
 
-static bool slab4_on() {  // VU_SLAB4=0: the scalar reduce (A/B runs)
-  static int v = [] { const char* e = getenv("VU_SLAB4"); return e ? atoi(e) : 1; }();
-  return v != 0;
-}
+int g_tune_slab4 = 1;  // VU_TUNE_SLAB4 = 0: the scalar slab reduce (A/B runs)
+static bool slab4_on() { return g_tune_slab4 != 0; }
 
 extern "C" int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C, int cvalid, int64_t s_i,
                               int64_t s_tap, int64_t s_c, float* out, int accumulate, void* stream) {

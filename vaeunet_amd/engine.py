@@ -37,6 +37,12 @@ from ._lib import BF16, F32
 # Off by default; module-level switch for A/B runs (bench.py --overlap).
 OVERLAP_WGRAD = False
 
+# The first stage of a BatchNorm backward reduction (sum dz, sum dz * xhat)
+# emitted by the epilogue of the input-gradient GEMM that produces dz's
+# source (DoubleConv conv2 -> BN1; bf16 3x3 kernels that support it), instead
+# of a separate pass over dy and x.  Module-level switch for A/B runs.
+FUSE_BN_BWD_REDUCE = True
+
 
 class SideStream:
     """One side stream per device; ``run`` forks it from the current stream,
@@ -340,10 +346,20 @@ def wgrad1x1(dy, srcs, w, M):
     K.gemm_wgrad(K.gather1x1([dy]), K.gather1x1(srcs), dy.shape[1], cin, g, conv_layout(g), M.d, acc)
 
 
-def bias_grad(dy, b, M, window=None):
+def bias_grad(dy, b, M, window=None, bn=None):
+    """d(loss)/d(conv bias) = per-channel sum of dy.  When the conv feeds a
+    TRAIN-mode BatchNorm (``bn``), BN(x + b) does not depend on b (the batch
+    mean absorbs it), so the gradient is exactly zero: it is written as zeros
+    instead of summing a zero-mean map (autograd's sum leaves only rounding
+    noise there).  Eval-mode BN and plain consumers get the real sum."""
     g, acc = grad_sink(b)
-    if g is not None:
-        K.chan_sum(dy, g, acc, M.d, window)
+    if g is None:
+        return
+    if bn is not None and bn.training:
+        if not acc:
+            K.call("vu_zero", K.ptr(g), 0, 1, g.numel(), K.dcode(g.dtype), K.stream())
+        return
+    K.chan_sum(dy, g, acc, M.d, window)
 
 
 # ----------------------------------------------------------------------------
@@ -371,15 +387,20 @@ def bn_grad_sinks(bn):
     return gw, gb, accw or accb
 
 
-def bn_bwd(dy, x, coef, bn, relu, M, dx=None):
+def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None):
     """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
     batch statistics; eval mode (running statistics, constants) gives
-    dx = gamma*invstd*dz and the same dgamma/dbeta sums."""
+    dx = gamma*invstd*dz and the same dgamma/dbeta sums.  part: the first
+    reduction stage, already emitted by the GEMM that produced dy."""
     gw, gb, acc = bn_grad_sinks(bn)
     if dx is None:
         dx = torch.empty_like(x)
-    K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
-                  train=bn.training)
+    if part is not None and part.x is x:
+        K.bn_backward_part(part, dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
+                           train=bn.training)
+    else:
+        K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
+                      train=bn.training)
     return dx
 
 
@@ -404,12 +425,17 @@ def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
 
 
 def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False,
-                     cin_pad=None):
+                     cin_pad=None, da_part=None, feeds=None):
     """cin_pad: compute the input gradient for cin_pad channels (zero weight
     rows past conv.in_channels) so that its column count stays a tile
-    multiple; the caller reads the real channels only."""
+    multiple; the caller reads the real channels only.
+    da_part: BatchNorm-backward partials of ``da`` from the GEMM that made it.
+    feeds=(saved, bn) of the BN(+ReLU) the input gradient feeds (the previous
+    conv's): its first backward reduction stage then rides this input-gradient
+    GEMM's epilogue, returned as (dsrc, part) -- part None when the kernel
+    cannot."""
     y, coef = saved
-    dy = bn_bwd(da, y, coef, bn, True, M)
+    dy = bn_bwd(da, y, coef, bn, True, M, part=da_part)
 
     def wg():
         wgrad3x3(dy, srcs, conv.weight, M, cvalid)
@@ -423,8 +449,14 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     cin = cin_pad or conv.in_channels
     if dsrc is None:
         dsrc = M.act(N, cin, H, W)
-    K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d, cin), cin, dsrc, M.d, accumulate=dsrc_acc,
-               kind="dgrad")
+    bnb = None
+    if feeds is not None and FUSE_BN_BWD_REDUCE:
+        (fy, fcoef), fbn = feeds
+        bnb = (fy, fcoef, True)
+    part = K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d, cin), cin, dsrc, M.d, accumulate=dsrc_acc,
+                      kind="dgrad", bnb=bnb)
+    if feeds is not None:
+        return dsrc, part
     return dsrc
 
 
@@ -440,8 +472,9 @@ def double_conv_fwd(M, seq, srcs, cin_pad=None, defer=False):
 def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None):
     conv1, bn1, _, conv2, bn2, _ = seq
     srcs, a1, s1, s2 = saved
-    da1 = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True)
-    return conv_bn_relu_bwd(M, srcs, conv1, bn1, s1, da1, need_dsrc, cvalid)
+    # conv2's input gradient also emits BN1's first backward reduction stage
+    da1, part = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True, feeds=(s1, bn1))
+    return conv_bn_relu_bwd(M, srcs, conv1, bn1, s1, da1, need_dsrc, cvalid, da_part=part)
 
 
 # ----------------------------------------------------------------------------
@@ -552,9 +585,9 @@ def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
 
     def wgs():
         wgrad1x1(dug, [g], wg.weight, M)
-        bias_grad(dug, wg.bias, M)
+        bias_grad(dug, wg.bias, M, bn=bng)
         wgrad1x1(dux, [x], wx.weight, M)
-        bias_grad(dux, wx.bias, M)
+        bias_grad(dux, wx.bias, M, bn=bnx)
         M.notify([wg.weight, wg.bias, wx.weight, wx.bias, wp.weight, wp.bias, bng.weight, bng.bias,
                   bnx.weight, bnx.bias, bnp.weight, bnp.bias])
     M.side(wgs, dug, dux, g, x)

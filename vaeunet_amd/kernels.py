@@ -7,7 +7,6 @@ channel concat of unet_parts.py:94 is addressed without a copy).  Every
 function launches on the current HIP stream and never synchronises.
 """
 import ctypes as C
-import os
 
 import torch
 
@@ -140,10 +139,21 @@ class Stats:
         self.psum, self.pm2, self.tiles, self.tile_rows, self.rows = psum, pm2, tiles, tile_rows, rows
 
 
+class BnbPart:
+    """BatchNorm-backward partial sums [nblk][2][C] a GEMM epilogue wrote for
+    the BN over ``x`` that its output feeds (VuGemmFwd.bnb_part)."""
+
+    def __init__(self, part, nblk, x):
+        self.part, self.nblk, self.x = part, nblk, x
+
+
 def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
-             convT=None, kind="fwd", strided=None):
+             convT=None, kind="fwd", strided=None, bnb=None):
     """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
     the pixel-shuffle epilogue, strided=(oH,oW,opy,opx) the stride-2 sub-lattice one.
+    bnb=(x, coef, relu): also emit the BatchNorm-backward partials of the output
+    for the train/eval BN over x (coef = bn_finalize's scale, shift, mean,
+    invstd) when the selected kernel can (returns a BnbPart then, else None).
     Returns Stats if requested."""
     a = VuGemmFwd()
     a.a = g
@@ -177,6 +187,22 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
         a.stat_sum = a.stat_m2 = None
     a.ksplit = 0
     a.workspace = None
+    part = None
+    if bnb is not None and dtype == _lib.BF16 and not accumulate and out_coff == 0 and bias is None \
+            and out.shape[1] == ncol:
+        bx, bcoef, brelu = bnb
+        a.bnb_xstride = pstride(bx)
+        tile = query("vu_gemm_fwd_bnb_tile", C.byref(a), dtype)
+        rows = g.N * g.H * g.W
+        if tile > 0 and rows % tile == 0:
+            nblk = rows // tile
+            pbuf = torch.empty((nblk, 2, ncol), dtype=torch.float32, device=out.device)
+            a.bnb_x = bx.data_ptr()
+            a.bnb_scale, a.bnb_shift = bcoef[0].data_ptr(), bcoef[1].data_ptr()
+            a.bnb_mean, a.bnb_invstd = bcoef[2].data_ptr(), bcoef[3].data_ptr()
+            a.bnb_part = pbuf.data_ptr()
+            a.bnb_relu = 1 if brelu else 0
+            part = BnbPart(pbuf, nblk, bx)
     ws = None
     if dtype == _lib.BF16:
         # any bf16 shape may be given split-K by the C-side selector (it returns 0
@@ -189,10 +215,12 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     _timed(_gemm_tag(g, kind),
            2 * M * ncol * g.R * g.S * g.C,
            lambda: call("vu_gemm_fwd", C.byref(a), dtype, stream()))
+    if bnb is not None:
+        return part
     return st
 
 
-SPLIT_PIX = int(os.environ.get("VU_WGRAD_SPLIT_PIX", "4096"))
+SPLIT_PIX = 4096
 SPLIT_MAX = 1024
 
 
@@ -368,6 +396,20 @@ def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=T
          ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
          1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype,
          stream())
+    call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
+         ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
+         stream())
+    return dx
+
+
+def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
+    """bn_backward with the first reduction stage done by the producing GEMM's
+    epilogue (a BnbPart): the fp64 finish, then the apply pass."""
+    N, Cc, H, W = x.shape
+    P = N * H * W
+    k = torch.empty((3, Cc), dtype=torch.float32, device=x.device)
+    call("vu_bn_bwd_finish", ptr(part.part), part.nblk, P, Cc, ptr(gamma), ptr(coef[3]), 1 if train else 0,
+         ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), stream())
     call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
          ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
          stream())

@@ -43,8 +43,9 @@ def conv_fwd(M, srcs, conv, stats, cin_pad=None):
     return y, st
 
 
-def conv_wgrad(M, dy, srcs, conv, cvalid=None):
-    """Weight (and bias) gradient, forked onto the side stream (engine.OVERLAP_WGRAD)."""
+def conv_wgrad(M, dy, srcs, conv, cvalid=None, bn=None):
+    """Weight (and bias) gradient, forked onto the side stream (engine.OVERLAP_WGRAD);
+    bn: the BatchNorm the conv feeds (a train-mode one zeroes the bias gradient)."""
     def wg():
         gw, acc = E.grad_sink(conv.weight)
         if gw is not None:
@@ -52,7 +53,7 @@ def conv_wgrad(M, dy, srcs, conv, cvalid=None):
             K.gemm_wgrad(K.gather1x1([dy]), g, dy.shape[1], g.R * g.S * g.C, gw, E.conv_layout(gw), M.d,
                          acc, cvalid=cvalid)
         if conv.bias is not None:
-            E.bias_grad(dy, conv.bias, M)
+            E.bias_grad(dy, conv.bias, M, bn=bn)
     M.side(wg, dy, *srcs)
 
 
@@ -73,17 +74,21 @@ def _parity_w(w, py, px, p, d):
     return E._cached(w, ("wpar", d, py, px), build), ry, rx
 
 
-def conv_dgrad(M, dy, conv, dx, accumulate):
-    """dx (N, Cin, H, W) (+)= conv input gradient of dy."""
+def conv_dgrad(M, dy, conv, dx, accumulate, bnb=None):
+    """dx (N, Cin, H, W) (+)= conv input gradient of dy.  bnb=(x, coef, relu):
+    also the BN-backward partials of dx for the BN over x (stride 1; returns
+    (dx, part), part None when the kernel cannot)."""
     k, s, p = _geom(conv)
     N, ci, H, W = dx.shape
     if s == 1:
         if 2 * p != k - 1:
             raise NotImplementedError("stride-1 conv input gradient needs 'same' padding")
         g = K.gather([dy], N, H, W, R=k, S=k, oy=p - (k - 1), ox=p - (k - 1))
-        K.gemm_fwd(g, E.w3x3_dgrad(conv.weight, M.d), ci, dx, M.d, accumulate=accumulate,
-                   kind="dgrad")
-        return dx
+        part = K.gemm_fwd(g, E.w3x3_dgrad(conv.weight, M.d), ci, dx, M.d, accumulate=accumulate,
+                          kind="dgrad", bnb=bnb if E.FUSE_BN_BWD_REDUCE else None)
+        return (dx, part) if bnb is not None else dx
+    if bnb is not None:
+        raise NotImplementedError("BN-backward partials from a strided input gradient")
     if s != 2:
         raise NotImplementedError("only stride 1 and 2 convolutions")
     Ho, Wo = dy.shape[2], dy.shape[3]
@@ -144,8 +149,10 @@ def basic_bwd(M, blk, saved, dout, need_dx=True):
            K.ptr(g), K.pstride(g), M.d, K.stream())
     dy2 = E.bn_bwd(g, y2, c2, blk.bn2, False, M)
     conv_wgrad(M, dy2, [a1], blk.conv2)
-    da1 = conv_dgrad(M, dy2, blk.conv2, torch.empty_like(a1), False)
-    dy1 = E.bn_bwd(da1, y1, c1, blk.bn1, True, M)
+    # conv2 is 3x3 stride 1: its input gradient also emits bn1's first
+    # backward reduction stage
+    da1, part = conv_dgrad(M, dy2, blk.conv2, torch.empty_like(a1), False, bnb=(y1, c1, True))
+    dy1 = E.bn_bwd(da1, y1, c1, blk.bn1, True, M, part=part)
     conv_wgrad(M, dy1, [x], blk.conv1)
     M.notify([blk.conv1.weight, blk.conv2.weight, blk.bn1.weight, blk.bn1.bias,
               blk.bn2.weight, blk.bn2.bias])
@@ -245,7 +252,7 @@ def cbr1x1_bwd(M, seq, saved, da):
     conv, bn = seq[0], seq[1]
     x, y, c = saved
     dy = E.bn_bwd(da, y, c, bn, True, M)
-    conv_wgrad(M, dy, [x], conv)
+    conv_wgrad(M, dy, [x], conv, bn=bn)
     M.notify([conv.weight, conv.bias, bn.weight, bn.bias])
     dx = torch.empty_like(x)
     K.gemm_fwd(K.gather1x1([dy]), E.w1x1_dgrad(conv.weight, M.d), x.shape[1], dx, M.d,
@@ -316,10 +323,11 @@ def decoder_bwd(M, blk, saved, dout, z=None):
     """-> (dx, dskip or None, dz or None): dz is [B, L] fp32 for a vector z,
     an NHWC map like ``z`` for a spatial one."""
     x, skip, xu, srcs, satt, szp, a1, s1, s2, cpad = saved
-    da1 = E.conv_bn_relu_bwd(M, [a1], blk.conv2[0], blk.conv2[1], s2, dout, True)
+    da1, part = E.conv_bn_relu_bwd(M, [a1], blk.conv2[0], blk.conv2[1], s2, dout, True,
+                                   feeds=(s1, blk.conv1[1]))
     conv1 = blk.conv1[0]
     dsrc = E.conv_bn_relu_bwd(M, srcs, conv1, blk.conv1[1], s1, da1, True,
-                              cvalid=conv1.in_channels if cpad else None, cin_pad=cpad)
+                              cvalid=conv1.in_channels if cpad else None, cin_pad=cpad, da_part=part)
     cx = xu.shape[1]
     off = cx
     dskip = dz = None
