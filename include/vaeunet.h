@@ -270,11 +270,13 @@ int vu_bn_bwd_reduce(const void* dy, int64_t dy_stride, const void* x,
 /* dx = k1*dz + k2*(x-mean) + k3 (+ add) */
 /* Second stage of vu_bn_bwd_reduce over partials a GEMM epilogue wrote
  * (VuGemmFwd.bnb_part, nblk row tiles): dgamma, dbeta and the apply
- * coefficients coef [3][C], exactly as vu_bn_bwd_reduce. */
+ * coefficients coef [3][C], exactly as vu_bn_bwd_reduce.  workspace:
+ * vu_bn_bwd_finish_workspace_bytes(nblk, C) bytes (fp32 row folds). */
+int64_t vu_bn_bwd_finish_workspace_bytes(int nblk, int C);
 int vu_bn_bwd_finish(const float* part, int nblk, int64_t P, int C,
                      const float* gamma, const float* invstd, int train,
                      float* dgamma, float* dbeta, int accumulate, float* coef,
-                     void* stream);
+                     float* workspace, void* stream);
 int vu_bn_bwd_apply(const void* dy, int64_t dy_stride, const void* x,
                     int64_t x_stride, int64_t P, int C, const float* scale,
                     const float* shift, const float* mean, const float* coef,

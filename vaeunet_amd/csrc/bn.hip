@@ -637,12 +637,59 @@ extern "C" int vu_bn_bwd_reduce(const void* dy, int64_t dys, const void* x, int6
   return (int)hipGetLastError();
 }
 
+// GEMM-epilogue partials come per 64-128-pixel row tile (16k-32k rows at
+// 512^2): folded first by a grid of (channel group, row range) blocks into at
+// most FOLD_MAXS rows (fp64 sums rounded once to fp32), then the fixed-order
+// colsum32 of bn_bwd_final.  A single colsum32 pass over 32k rows runs on
+// C/32 blocks: 2 blocks for 64 channels, 3-4x the time of both passes here.
+constexpr int FOLD_MAXS = 256, FOLD_DIRECT = 1024;
+static int fold_blocks(int nblk) {
+  int S = (nblk + 63) / 64;
+  return S > FOLD_MAXS ? FOLD_MAXS : (S < 1 ? 1 : S);
+}
+
+namespace {
+__global__ void bnb_fold_kernel(const float* part, int nblk, int C, int S, float* ws) {
+  __shared__ double sh[2][4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  const int per = (nblk + S - 1) / S;
+  const int r0 = blockIdx.y * per, r1 = min(nblk, r0 + per);
+  double s0 = 0.0, s1 = 0.0;
+  const int cc = ok ? c : 0;
+  for (int r = r0 + rl; r < r1; r += 4) {
+    s0 += (double)part[((int64_t)r * 2 + 0) * C + cc];
+    s1 += (double)part[((int64_t)r * 2 + 1) * C + cc];
+  }
+  sh[0][rl][cl] = s0;
+  sh[1][rl][cl] = s1;
+  __syncthreads();
+  if (rl == 0 && ok) {
+    ws[((int64_t)blockIdx.y * 2 + 0) * C + c] = (float)(((sh[0][0][cl] + sh[0][1][cl]) + sh[0][2][cl]) + sh[0][3][cl]);
+    ws[((int64_t)blockIdx.y * 2 + 1) * C + c] = (float)(((sh[1][0][cl] + sh[1][1][cl]) + sh[1][2][cl]) + sh[1][3][cl]);
+  }
+}
+}  // namespace
+
+extern "C" int64_t vu_bn_bwd_finish_workspace_bytes(int nblk, int C) {
+  return nblk <= FOLD_DIRECT ? 0 : (int64_t)fold_blocks(nblk) * 2 * C * (int64_t)sizeof(float);
+}
+
 extern "C" int vu_bn_bwd_finish(const float* part, int nblk, int64_t P, int C, const float* gamma,
                                 const float* invstd, int train, float* dgamma, float* dbeta, int accumulate,
-                                float* coef, void* stream) {
+                                float* coef, float* workspace, void* stream) {
   if (nblk < 1 || C < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, (hipStream_t)stream, part, nblk,
-                     C, P, gamma, invstd, dgamma, dbeta, accumulate, coef, train);
+  hipStream_t st = (hipStream_t)stream;
+  if (nblk > FOLD_DIRECT) {
+    if (!workspace) return (int)hipErrorInvalidValue;
+    const int S = fold_blocks(nblk);
+    hipLaunchKernelGGL(bnb_fold_kernel, dim3((C + 63) / 64, S), dim3(256), 0, st, part, nblk, C, S, workspace);
+    part = workspace;
+    nblk = S;
+  }
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, part, nblk, C, P, gamma,
+                     invstd, dgamma, dbeta, accumulate, coef, train);
   return (int)hipGetLastError();
 }
 

@@ -47,8 +47,7 @@ constexpr int HBUF = NHR * 512 * 16;         // chunk buffer, padded to whole DM
 constexpr int WROW = 576 * 2;                // one output channel's weights (bytes)
 constexpr int WBYTES = 64 * WROW;            // 72 KiB, resident
 constexpr int WROUNDS = WBYTES / 16 / 512;   // 9
-constexpr int PARAM_BYTES = 4 * 64 * 4;       // BN-backward scale / shift / mean / invstd (BNB)
-constexpr int LDS_BYTES = WBYTES + 2 * HBUF + PARAM_BYTES;
+constexpr int LDS_BYTES = WBYTES + 2 * HBUF;
 static_assert(LDS_BYTES <= 163840, "LDS");
 static_assert(WROUNDS * 512 * 16 == WBYTES, "weight DMA rounds");
 
@@ -78,18 +77,11 @@ VU_DEV float ror_add(float v) {
 }
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
-// BNB: also emit the BatchNorm-backward partial sums of the output
-// (VuGemmFwd.bnb_part) per wave tile of 64 pixels.  The BN input x of the
-// tile's pixels is loaded at the start of the tile's second group (its
-// latency hidden behind that group's MFMAs, in the registers the pending
-// stores occupy during the first group) and combined with the rounded
-// accumulators in the epilogue; the per-channel BN coefficients sit in LDS.
-template <bool STATS, bool BNB>
+template <bool STATS>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   char* const wl = smem;
   char* const hl = smem + WBYTES;
-  float* const prm = reinterpret_cast<float*>(smem + WBYTES + 2 * HBUF);  // [4][64]
 
   const VuGather& g = p.a;
   const int H = g.H, W = g.W;
@@ -106,17 +98,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   const void* const zp = (const void*)v6_zero_page;
   // bias of this lane's channels, loaded up front: a load in the epilogue
   // would wait for the in-flight halo DMA (vmcnt is in order)
-  // (BNB launches carry no bias: an input gradient; the launcher checks)
   f32x4 bv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    bv[j] = (!BNB && p.bias) ? *reinterpret_cast<const f32x4*>(p.bias + 16 * kg + 4 * j) : f32x4{0, 0, 0, 0};
+    bv[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + 16 * kg + 4 * j) : f32x4{0, 0, 0, 0};
 
-  if (BNB && tid < 256) {
-    const float* srcp = (tid >> 6) == 0 ? p.bnb_scale : (tid >> 6) == 1 ? p.bnb_shift : (tid >> 6) == 2 ? p.bnb_mean
-                                                                                                        : p.bnb_invstd;
-    prm[tid] = srcp[tid & 63];
-  }
   // ---- resident weights: row n (output channel) = 576 bf16; 16-byte piece
   //      pc of row n lives at piece pc ^ wswz(n) ----
   {
@@ -151,7 +137,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   };
 
   halo(lb, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // weights, halo, BN table
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   raw_barrier();
 
   // B fragment j, lane row l16 = output channel n_j = 16*(l16>>2) + 4j + (l16&3),
@@ -226,16 +212,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     // ---- group (t, chunk 1): the other buffer takes chunk 0 of the next tile ----
     const int img = t / per_img, r0 = t - (t / per_img) * per_img;
     const int ty = r0 / txn, tx = r0 - (r0 / txn) * txn;
-    const int64_t pix0 = ((int64_t)img * H + ty * TH + 2 * wid) * W + tx * TW + l16;
-    u32x4 xb[4][2];  // BN input x of this lane's 4 pixels x 16 channels (BNB)
-    if (BNB) {
-      const bf16_t* xr = reinterpret_cast<const bf16_t*>(p.bnb_x) + 16 * kg + pix0 * p.bnb_xstride;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          xb[i][h] = *reinterpret_cast<const u32x4*>(xr + ((i >> 1) * (int64_t)W + (i & 1) * 16) * p.bnb_xstride + 8 * h);
-    }
     if (ti + 1 < ntile_blk) halo(t + G, 0, b ^ 1);
     taps(b, 1, false);
     // ---- epilogue of tile t from registers: acc[i][j][r] = pixel fragment
@@ -277,42 +253,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
       p.stat_sum[so] = ms;
       p.stat_m2[so] = mq;
     }
-    if (BNB) {
-      // BN-backward partials (sum dz, sum dz * xhat) of the wave's 64 pixels,
-      // dz = the rounded output masked by the forward ReLU; lane (kg, l16)
-      // keeps channel 16*kg + l16 = lane, as the statistics above
-      float m0 = 0.f, m1 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(prm + 0 * 64 + 16 * kg + 4 * j);
-        const f32x4 sf = *reinterpret_cast<const f32x4*>(prm + 1 * 64 + 16 * kg + 4 * j);
-        const f32x4 mu = *reinterpret_cast<const f32x4*>(prm + 2 * 64 + 16 * kg + 4 * j);
-        const f32x4 is = *reinterpret_cast<const f32x4*>(prm + 3 * 64 + 16 * kg + 4 * j);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int e = 4 * j + r;  // channel 16kg + e: piece e/8, word (e%8)/2, half e%2
-          float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t wv = xb[i][e >> 3][(e & 7) >> 1];
-            const float xv = __uint_as_float((e & 1) ? (wv & 0xffff0000u) : (wv << 16));
-            float dz = acc[i][j][r];
-            if (p.bnb_relu && !(xv * sc[r] + sf[r] > 0.f)) dz = 0.f;
-            s0 += dz;
-            s1 += dz * ((xv - mu[r]) * is[r]);
-          }
-          s0 = row16_sum(s0);
-          s1 = row16_sum(s1);
-          if (l16 == e) {
-            m0 = s0;
-            m1 = s1;
-          }
-        }
-      }
-      float* pr = p.bnb_part + (int64_t)(t * 8 + wid) * 2 * p.ncol + lane;
-      pr[0] = m0;
-      pr[p.ncol] = m1;
-    }
     // stores: a lane holds channels 16kg .. 16kg+15 of its pixel (two 16-byte
     // pieces); a permlane16 + permlane32 swap regroups them so that store h
     // of lane kg writes channels 32h + 8kg .. +7: 64 contiguous bytes per
@@ -343,9 +283,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-    // the next group's halo was issued before this tile's statistics /
-    // partial-sum stores (2 per lane)
-    if (STATS || BNB) wait_vm<2>(); else wait_vm<0>();
+    // the next group's halo was issued before this tile's statistics stores
+    if (STATS) wait_vm<2>(); else wait_vm<0>();
     raw_barrier();
     b ^= 1;
     t += G;
@@ -387,24 +326,26 @@ int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype) {
   return 64;
 }
 
-// BatchNorm-backward partial row tile (64 pixels: one wave tile) when v6
-// serves the problem (its output is a whole plain tensor: no offset), else 0.
+// BatchNorm-backward partials are not emitted here (0): at 512^2 with 64
+// channels this kernel already moves ~3.7 TB/s, and reading the BN input in
+// its epilogue (+268 MB per launch) plus the partial sums cost more than the
+// separate reduction pass they replace (measured: +100 us per launch against
+// the 97 us pass; profiles/r3_prof_bnb_fusion.txt).
 int gemm_fwd_v6_bnb_tile(const VuGemmFwd& p, int dtype) {
-  if (!gemm_fwd_v6_bm(p, dtype) || p.out_coff != 0 || p.stat_sum || p.bnb_xstride % 8 != 0) return 0;
-  return 64;
+  (void)p;
+  (void)dtype;
+  return 0;
 }
 
 int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
   const int64_t T = (int64_t)p.a.N * p.a.H * p.a.W / (TH * TW);
   int64_t grid = T < cu_count6() ? T : cu_count6();
   if (g_v6 >= 2 && grid > g_v6) grid = g_v6;
-  if (p.bnb_part && (p.stat_sum || p.bias)) return (int)hipErrorInvalidValue;
+  if (p.bnb_part) return (int)hipErrorInvalidValue;
   if (p.stat_sum)
-    hipLaunchKernelGGL((conv3x3_c64_kernel<true, false>), dim3((unsigned)grid), dim3(512), 0, st, p);
-  else if (p.bnb_part)
-    hipLaunchKernelGGL((conv3x3_c64_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
   else
-    hipLaunchKernelGGL((conv3x3_c64_kernel<false, false>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 

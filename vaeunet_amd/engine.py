@@ -39,9 +39,14 @@ OVERLAP_WGRAD = False
 
 # The first stage of a BatchNorm backward reduction (sum dz, sum dz * xhat)
 # emitted by the epilogue of the input-gradient GEMM that produces dz's
-# source (DoubleConv conv2 -> BN1; bf16 3x3 kernels that support it), instead
-# of a separate pass over dy and x.  Module-level switch for A/B runs.
-FUSE_BN_BWD_REDUCE = True
+# source (DoubleConv conv2 -> BN1; the ping-pong kernel and its split-K
+# finish), instead of a separate pass over dy and x.  Measured neutral
+# (same-box A/B, profiles/r3_ab_bn_bwd_fusion.log: UNet +0.35 %, VAE -0.4 %;
+# per kernel, profiles/r3_prof_bnb_fusion.txt: the 22 -> 16 reduction passes
+# save 172 us/step, the epilogues that replace them cost 124 us/step and the
+# partial folds 18): the epilogue's BN-input loads and sums run serialised
+# at one block per CU.  Off by default; module-level switch for A/B runs.
+FUSE_BN_BWD_REDUCE = False
 
 
 class SideStream:

@@ -408,8 +408,10 @@ def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dty
     N, Cc, H, W = x.shape
     P = N * H * W
     k = torch.empty((3, Cc), dtype=torch.float32, device=x.device)
+    nb = query("vu_bn_bwd_finish_workspace_bytes", part.nblk, Cc)
+    ws = workspace_f32(nb, x.device) if nb > 0 else None
     call("vu_bn_bwd_finish", ptr(part.part), part.nblk, P, Cc, ptr(gamma), ptr(coef[3]), 1 if train else 0,
-         ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), stream())
+         ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), stream())
     call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
          ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
          stream())
