@@ -400,10 +400,13 @@ def main():
         return loss
 
     graphed = None
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and not args.torch_optim)
+    # the step replays as one HIP graph with the fused optimizer; at N > 1 the
+    # bucketed RCCL all-reduces are captured with it (gloo rehearsals run eagerly)
+    capturable = not args.torch_optim and (world == 1 or dist.get_backend() == "nccl")
+    use_graph = args.graph == "on" or (args.graph == "auto" and capturable)
     if use_graph:
-        if world > 1 or args.torch_optim:
-            raise SystemExit("--graph on needs world size 1 and the fused optimizer")
+        if not capturable:
+            raise SystemExit("--graph on needs the fused optimizer and (at N > 1) the nccl backend")
         from vaeunet_amd.graph import GraphedTrainStep
 
         def fwd_bwd():
@@ -416,7 +419,7 @@ def main():
             loss.backward()
             return loss
         # warm-up steps run eagerly inside (weights, optimizer state), then one capture
-        graphed = GraphedTrainStep(fwd_bwd, opt, max_norm=1.0, warmup=max(1, args.warmup))
+        graphed = GraphedTrainStep(fwd_bwd, opt, max_norm=1.0, warmup=max(1, args.warmup), reducer=reducer)
     eager_step = step
     if graphed is not None:
         step = graphed.step

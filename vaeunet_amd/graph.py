@@ -20,9 +20,14 @@ AdamW once (``torch.cuda.CUDAGraph`` over HIP graphs) and replays it:
   before capture.
 
 The learning rate, betas, eps, weight decay and max_norm are frozen at
-capture (rebuild the object to change them).  Single process: the data-
-parallel reducer's collectives are not captured (``bench.py`` replays only
-at world size 1).
+capture (rebuild the object to change them).
+
+Data parallel (``reducer``, vaeunet_amd.parallel): the gradient buffers are
+the reducer's bucket views, and the bucketed all-reduces the fused backward
+launches (RCCL, c10d's ``nccl`` backend) are captured with the step: each
+collective's fork from and join to the compute stream become graph edges,
+so a replay overlaps the buckets with the backward exactly as the eager step
+does.  Only RCCL collectives are capturable (gloo runs on the host).
 """
 import gc
 import weakref
@@ -39,9 +44,21 @@ class GraphedTrainStep:
     """forward_backward(): runs the forward, the loss and ``loss.backward()``
     on static inputs and returns the loss tensor."""
 
-    def __init__(self, forward_backward, optimizer, max_norm=None, warmup=2):
+    def __init__(self, forward_backward, optimizer, max_norm=None, warmup=2, reducer=None):
         if not isinstance(optimizer, FusedAdamW):
             raise TypeError("GraphedTrainStep needs vaeunet_amd.optim.FusedAdamW")
+        if reducer is not None:
+            import torch.distributed as dist
+            if dist.get_backend(reducer.group) != "nccl":
+                raise RuntimeError("GraphedTrainStep: only RCCL (nccl backend) collectives can be captured")
+            inner = forward_backward
+
+            def forward_backward():
+                reducer.prepare()
+                loss = inner()
+                reducer.finish()
+                return loss
+        self.reducer = reducer
         self.fb = forward_backward
         self.opt = optimizer
         self.max_norm = max_norm
@@ -63,9 +80,18 @@ class GraphedTrainStep:
         self.params = params
         keep = set(id(p) for p in params)
         dev = params[0].device
-        # persistent zero gradients (the backward accumulates into them)
-        for p in params:
-            p.grad = torch.zeros_like(p)
+        # persistent zero gradients (the backward accumulates into them; the
+        # capturable AdamW clears them after use): the reducer's bucket views
+        # when data parallel
+        if reducer is not None:
+            reducer.zero_grad()
+            reducer._bind()
+            for p in params:
+                if p.grad is None:
+                    raise RuntimeError("GraphedTrainStep: a parameter outside the reducer's buckets")
+        else:
+            for p in params:
+                p.grad = torch.zeros_like(p)
         self.grads = [p.grad for p in params]
         self.clip_tab = _Table([(p.grad, p.grad, None, None, 0.0, 1.0) for p in params], dev)
         self.norm = torch.empty(2, dtype=torch.float32, device=dev)
