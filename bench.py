@@ -66,6 +66,8 @@ def parse():
                     help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
     ap.add_argument("--engine-flag", action="append", default=[], metavar="NAME=0|1",
                     help="set a vaeunet_amd.engine module switch (A/B runs), e.g. FUSE_BN_BWD_REDUCE=0")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VAL",
+                    help="vu_gemm_set_tuning(KEY, VAL) before the run (library A/B runs; include/vaeunet.h)")
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a side stream (engine.OVERLAP_WGRAD; measured slower, A/B only)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
@@ -347,6 +349,10 @@ def main():
     from vaeunet_amd.init import seeded_init_
     if args.overlap:
         E.OVERLAP_WGRAD = True
+    for kv in args.tune:
+        from vaeunet_amd import _lib
+        key, val = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(key), int(val))  # raises if the key / value is refused
     for kv in args.engine_flag:
         name, val = kv.split("=")
         if not hasattr(E, name):

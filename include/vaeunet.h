@@ -116,6 +116,11 @@ int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype);
 /* bytes of args->workspace the dispatcher needs for this problem (0 = none):
  * the split-K slabs of the 3x3 kernel when its grid is under one block per CU */
 int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype);
+/* the kernel the dispatcher picks for this problem (tests): 1 generic, 2 v2
+ * LDS-DMA tiles, 3 v3 halo, 4 v4 ping-pong, 5 v5 persistent short-K, 6 v6
+ * resident weights, 7 v7 small-grid, 8 1x1 stream, 9 image conv, 10 7x7 stem,
+ * 12 v2 small-grid mode */
+int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype);
 int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream);
 /* output tile (BI x BJ) the dispatcher picks for this problem (split-K sizing) */
 int vu_gemm_wgrad_tile(const VuGemmWgrad* args, int dtype, int* bi, int* bj);
@@ -167,6 +172,20 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 #define VU_TUNE_SLAB4 13
 #define VU_TUNE_V2_CFG 14
 #define VU_TUNE_BN_NT_MB 15
+/*   VU_TUNE_V7: small-grid 3x3 kernel (gemm_fwd7.hip): 0 = off (v4 split-K /
+ *     v2 small-grid tiles), 1 = default (grids under one 256x256 tile per CU,
+ *     except 32-pixel-wide ones with >= 512 input channels, which stay on the
+ *     ping-pong split-K), 2 = every small grid. */
+#define VU_TUNE_V7 16
+/*   VU_TUNE_V7_NBW: weight-ring slots (tap rows) of the small-grid kernel (3 default, 4) */
+#define VU_TUNE_V7_NBW 17
+/*   VU_TUNE_V7_XM: experiment mode of the small-grid kernel (A/B timing runs
+ *     only, results are wrong): 0 off, 2 no DMA inside the loop, 4 no loop */
+#define VU_TUNE_V7_XM 18
+/*   VU_TUNE_W3_SMALL: 1 (default) lets the halo weight-gradient kernel take
+ *     16-pixel-wide images and use 64-channel tiles on small grids; 0 = the
+ *     round-2 rules (A/B runs) */
+#define VU_TUNE_W3_SMALL 19
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */

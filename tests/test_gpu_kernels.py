@@ -60,6 +60,8 @@ CONV_CASES = [
     (2, [24, 8, 16], 6, 6, 40),    # three sources, ragged
     (2, [64, 128], 16, 48, 96),    # bf16 halo kernel: 16x16 tiles, 3 chunks, column tail
     (2, [128], 8, 64, 192),        # bf16 halo wgrad: 128-row co tiles with a 64-row tail
+    (8, [256], 32, 32, 256),       # small grid: 64-row co tiles (ResNet34 layer3 shape)
+    (4, [512], 16, 16, 512),       # 16-pixel-wide halo wgrad tiles (layer4 shape)
 ]
 
 
@@ -138,9 +140,10 @@ def _tune(*kv):
         _lib.call("vu_gemm_set_tuning", k, v)
 
 
-def _check_halo_conv(case, row_tiles):
+def _check_halo_conv(case, row_tiles, kernel=None):
     """forward with BN statistics, bias, accumulate into a channel slice, and
-    the flipped-weight input grad, on whatever halo kernel the tuning forces."""
+    the flipped-weight input grad, on whatever halo kernel the tuning forces
+    (kernel: the vu_gemm_fwd_kernel id the forward must be dispatched to)."""
     K, E = _k()
     N, cins, H, W, co = case[:5]
     g = torch.Generator().manual_seed(5)
@@ -153,6 +156,8 @@ def _check_halo_conv(case, row_tiles):
     srcs = [_act(x, "bf16") for x in xs]
     out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
     assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, srcs, E.w3x3_fwd(w.to(DEV), d), co, out)) in row_tiles
+    if kernel is not None:
+        assert K.query("vu_gemm_fwd_kernel", *_row_tile_args(K, srcs, E.w3x3_fwd(w.to(DEV), d), co, out)) == kernel
     st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, out, d, stats=True)
     ref = F.conv2d(torch.cat(xs, 1), wq, padding=1)
     _close(out, ref, "bf16", what="fwd")
@@ -210,11 +215,46 @@ SMALL_GRID_CASES = [
 ]
 
 
+TUNE_V7 = 16
+
+
 @pytest.mark.parametrize("case", SMALL_GRID_CASES)
 def test_conv3x3_small_grid_v2(case):
     """small grids (gemm_fwd2.hip small-grid mode + split-K finish): bias,
     BN partials per 128 rows, accumulate, input gradient."""
-    _check_halo_conv(case, (128,))
+    _tune((TUNE_V7, 0))
+    try:
+        _check_halo_conv(case, (128,), kernel=12)
+    finally:
+        _tune((TUNE_V7, 1))
+
+
+V7_CASES = [
+    # (N, [cin], H, W, cout, VU_TUNE_V7 mode): the small-grid two-K-group kernel (gemm_fwd7.hip)
+    (8, [512], 16, 16, 512, 1),        # 16-pixel-wide tiles, 2-way split-K + finish
+    (4, [512], 16, 16, 512, 1),        # 4-way split-K
+    (8, [256], 32, 32, 256, 1),        # 4 x 32 tiles, no split (the ResNet34 layer3 shape)
+    (8, [128], 64, 64, 128, 1),        # 512 blocks
+    (4, [64, 64], 32, 48, 128, 1),     # two concat sources, 48-wide image -> 8 x 16 tiles
+    (2, [512], 32, 32, 1024, 2),       # long K on a 32-wide grid (mode 2; mode 1 leaves it to v4 split-K)
+    (8, [1024], 16, 16, 512, 1),       # 32 chunks, 2-way split
+]
+
+
+TUNE_V7_NBW = 17
+
+
+@pytest.mark.parametrize("nbw", [3, 4])
+@pytest.mark.parametrize("case", V7_CASES)
+def test_conv3x3_small_grid_v7(case, nbw):
+    """small grids on gemm_fwd7.hip (3- and 4-slot weight rings): bias, BN
+    partials per 128-pixel tile, accumulate into a channel slice, input
+    gradient, split-K slabs."""
+    _tune((TUNE_V7, case[5]), (TUNE_V7_NBW, nbw))
+    try:
+        _check_halo_conv(case, (128,), kernel=7)
+    finally:
+        _tune((TUNE_V7, 1), (TUNE_V7_NBW, 3))
 
 
 def test_conv3x3_splitk_auto_32x32_level():

@@ -23,12 +23,20 @@ LAYERS = [("layer1", 64, 64, 128), ("layer2", 128, 128, 64), ("layer3", 256, 256
 
 
 def timeit(fn, reps=20):
+    """GPU time per call: the calls are captured in one HIP graph and replayed
+    (timed eagerly, the Python + ctypes enqueue of a ~10 us kernel is the
+    bottleneck, not the kernel)."""
     fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    g.replay()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps
@@ -58,13 +66,19 @@ def main():
         a.out = y.data_ptr()
         a.out_stride = K.pstride(y)
         a.out_mode = 0
-        diag = (K.query("vu_gemm_fwd_row_tile", C.byref(a), d), K.query("vu_gemm_fwd_workspace_bytes", C.byref(a), d))
+        diag = (K.query("vu_gemm_fwd_row_tile", C.byref(a), d), K.query("vu_gemm_fwd_workspace_bytes", C.byref(a), d),
+                "kernel", K.query("vu_gemm_fwd_kernel", C.byref(a), d))
         tf = timeit(lambda: K.gemm_fwd(K.gather3x3([x]), w3x3_fwd(w, d), co, y, d, stats=True))
         dx = K.empty_act(B, ci, S, S, torch.bfloat16, dev)
         tb = timeit(lambda: K.gemm_fwd(K.gather3x3([y]), w3x3_dgrad(w, d), ci, dx, d, kind="dgrad"))
-        tot += tf + tb
+        gw = torch.zeros(co, ci, 3, 3, device=dev)
+        from vaeunet_amd.engine import conv_layout
+        tw = timeit(lambda: K.gemm_wgrad(K.gather1x1([y]), K.gather3x3([x]), co, 9 * ci, gw, conv_layout(gw), d,
+                                         False))
+        tot += tf + tb + tw
         print(f"{name} {ci}->{co} @{S:3d} | fwd {tf * 1e3:7.1f}us {fl / tf / 1e9:6.0f}TF | "
-              f"dgrad {tb * 1e3:7.1f}us {fl / tb / 1e9:6.0f}TF | row_tile,ws {diag}")
+              f"dgrad {tb * 1e3:7.1f}us {fl / tb / 1e9:6.0f}TF | wgrad+reduce {tw * 1e3:7.1f}us "
+              f"{fl / tw / 1e9:6.0f}TF | row_tile,ws {diag}", flush=True)
     print(f"TOTAL {tot:.3f} ms")
 
 

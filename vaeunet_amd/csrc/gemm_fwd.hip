@@ -343,6 +343,9 @@ int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd6.hip (64 -> 6
 int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v6_bnb_tile(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v4_bnb_tile(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v7_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd7.hip (small-grid 3x3, two K groups)
+int gemm_fwd_v7_launch(const VuGemmFwd& p, hipStream_t st);
+int64_t gemm_fwd_v7_workspace(const VuGemmFwd& p, int dtype);
 
 // Highest kernel generation the dispatchers may pick (vu_gemm_set_tuning
 // VU_TUNE_GEN; tests and A/B runs only -- no environment lookups in the
@@ -368,6 +371,8 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
     if (bm) return bm;
     bm = gemm_fwd_v4_bm(*args, dtype);
     if (bm) return bm;
+    bm = gemm_fwd_v7_bm(*args, dtype);
+    if (bm) return bm;
   }
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return 128;
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 256;
@@ -385,6 +390,7 @@ extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype)
     return 0;
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return 0;
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_workspace(*args, dtype);
+  if (use_v4(dtype) && gemm_fwd_v7_bm(*args, dtype)) return gemm_fwd_v7_workspace(*args, dtype);
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_workspace(*args, dtype);
   return 0;
 }
@@ -397,6 +403,24 @@ extern "C" int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype) {
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return gemm_fwd_v6_bnb_tile(*args, dtype);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_bnb_tile(*args, dtype);
   return 0;
+}
+
+// Which kernel the dispatcher below picks (mirrors its order; tests assert the
+// path they mean to cover): 1 generic, 2 v2 LDS-DMA tiles, 3 v3 halo, 4 v4
+// ping-pong, 5 v5 persistent short-K, 6 v6 resident weights, 7 v7 small-grid,
+// 8 1x1 stream, 9 image conv, 10 7x7 stem, 12 v2 small-grid mode.
+extern "C" int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype) {
+  if (use_v2(dtype) && conv_image_bm(*args, dtype)) return 9;
+  if (use_v2(dtype) && conv_stem_bm(*args, dtype)) return 10;
+  if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return 8;
+  if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return 6;
+  if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return 4;
+  if (use_v4(dtype) && gemm_fwd_v7_bm(*args, dtype)) return 7;
+  if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return 12;
+  if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 3;
+  if (use_v2(dtype) && gemm_fwd_v5_bm(*args, dtype)) return 5;
+  if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return 2;
+  return 1;
 }
 
 extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
@@ -413,6 +437,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return gemm_fwd_v6_launch(*args, st);
   if (use_v4(dtype) && gemm_fwd_v4_bm(*args, dtype)) return gemm_fwd_v4_launch(*args, st);
+  if (use_v4(dtype) && gemm_fwd_v7_bm(*args, dtype)) return gemm_fwd_v7_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_small(*args, dtype)) return gemm_fwd_v2_small_launch(*args, st);
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v5_bm(*args, dtype)) return gemm_fwd_v5_launch(*args, st);

@@ -655,6 +655,7 @@ int g_split_min_chunks = 2;  // vu_gemm_set_tuning(VU_TUNE_V4_SPLIT_CHUNKS, ...)
 
 }  // namespace
 int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype);  // gemm_fwd2.hip
+int gemm_fwd_v7_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd7.hip
 namespace {
 
 template <int BN>
@@ -677,6 +678,8 @@ Plan plan(const VuGemmFwd& p) {
   // (>= 512 input channels: the UNet down4 input gradient, 1024 -> 512 at
   // 32^2, ran 201 us on v2 tiles vs 80 us split 4 ways here, tools/enc_bench.py)
   if (g_splitk == 1 && g.C < 512 && gemm_fwd_v2_small(p, VU_BF16)) return r;
+  // ... and those the small-grid kernel takes (gemm_fwd7.hip, VU_TUNE_V7)
+  if (g_splitk == 1 && gemm_fwd_v7_bm(p, VU_BF16)) return r;
   int bn = 0;
   int64_t blocks = 0;
   if (tiles_ok<256>(p)) {
@@ -785,6 +788,8 @@ int gemm_stream_tune(int key, int value);  // gemm_stream.hip
 int gemm_fwd_v2_tune(int key, int value);  // gemm_fwd2.hip
 int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
 int gemm_fwd_v6_tune(int key, int value);  // gemm_fwd6.hip
+int gemm_fwd_v7_tune(int key, int value);  // gemm_fwd7.hip
+int gemm_wgrad_v3_tune(int key, int value);  // gemm_wgrad3.hip
 int bn_tune(int key, int value);           // bn.hip
 extern int g_tune_gen;                     // gemm_fwd.hip
 extern int g_tune_slab4;                   // gemm_wgrad.hip
@@ -818,7 +823,8 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
     return 0;
   }
   if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0 || gemm_fwd_v2_tune(key, value) == 0 ||
-      gemm_fwd_v5_tune(key, value) == 0 || gemm_fwd_v6_tune(key, value) == 0 || bn_tune(key, value) == 0)
+      gemm_fwd_v5_tune(key, value) == 0 || gemm_fwd_v6_tune(key, value) == 0 || gemm_fwd_v7_tune(key, value) == 0 ||
+      gemm_wgrad_v3_tune(key, value) == 0 || bn_tune(key, value) == 0)
     return 0;
   return (int)hipErrorInvalidValue;
 }

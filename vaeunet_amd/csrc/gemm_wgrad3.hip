@@ -1,8 +1,8 @@
 // 3x3 / stride-1 / pad-1 convolution WEIGHT gradient over halo tiles ("v3",
 // bf16): slab[s][co][tap*C + ci] = sum_{pixels p of split s} dy[p][co] *
 // x[p + tap][ci].  Serves every DoubleConv / DecoderBlock 3x3 conv weight
-// gradient of the hot path (unet_parts.py:40,43) whose image width is a
-// multiple of 32.
+// gradient of the hot path (unet_parts.py:40,43) and of the ResNet34 encoder
+// (unet_resnet.py:131-137) whose image width is a multiple of 16.
 //
 // Why: the v2 kernel treats the nine taps as nine independent K columns and
 // gathers the shifted input separately for each, so every x pixel crosses
@@ -31,9 +31,13 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-constexpr int TW = 32, TH = 4, TP = TW * TH;   // pixel tile
-constexpr int HWP = 48;                        // halo row pitch (TW + 2 used)
-constexpr int HROWS = TH + 2;
+// pixel tile: 128 pixels = 4 x 32, or 8 x 16 for 16-pixel-wide images (the
+// ResNet34 encoder's 16^2 level); the halo row pitch (TW + 2 used) is a
+// multiple of 16 rows so that a tap / tile-row shift keeps the swizzle
+constexpr int TP = 128;
+template <int TW> struct WT {
+  static constexpr int TH = TP / TW, HWP = TW == 32 ? 48 : 32, HROWS = TH + 2;
+};
 
 template <int RB> VU_DEV int fsw(int m) {
   return RB >= 256 ? ((m & 3) | ((m >> 1) & 4)) : (((m >> 1) & 1) | ((m >> 2) & 2));
@@ -87,8 +91,9 @@ VU_DEV void lgkm_wait(int n) {
 }
 VU_DEV void tie(u32x4& v) { asm volatile("" : "+v"(v)); }
 
-template <int BI, int TJ>
+template <int BI, int TJ, int TW>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
+  constexpr int TH = WT<TW>::TH, HWP = WT<TW>::HWP, HROWS = WT<TW>::HROWS;
   constexpr int NT = 512;
   constexpr int RBP = BI * 2, CPI = BI / 8;
   constexpr int LP = TP * CPI / NT;                       // dy DMA instrs per thread per tile
@@ -191,7 +196,10 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int s = 0; s < 3; ++s)
-        offB[b][h][s] = tr_off<128>(8 * g4 + qd + 4 * h + s, (wci * TJ + b) * 16 + 4 * pp);
+        // pixel k of a 32-pixel k-step = tile row k / TW (of the step's
+        // 32 / TW rows), column k % TW; tap column shift s
+        offB[b][h][s] = tr_off<128>(((8 * g4 + qd + 4 * h) / TW) * HWP + (8 * g4 + qd + 4 * h) % TW + s,
+                                    (wci * TJ + b) * 16 + 4 * pp);
 
   f32x4 acc[TI][TJ][9];
 #pragma unroll
@@ -219,7 +227,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     auto load_b = [&](int g, u32x4* dst) {
       const int ks = g / 9, q = g - (g / 9) * 9, r = q / 3, s = q - (q / 3) * 3;
 #pragma unroll
-      for (int b = 0; b < TJ; ++b) dst[b] = tr_frag(Qb + (ks + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
+      for (int b = 0; b < TJ; ++b) dst[b] = tr_frag(Qb + (ks * (32 / TW) + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
     };
     auto load_a = [&](int ks, u32x4* dst) {
 #pragma unroll
@@ -272,19 +280,34 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       }
 }
 
-template <int BI>
+template <int BI, int TW>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int64_t nblk = (int64_t)((p.ni + BI - 1) / BI) * (p.q.C / 64) * p.splits;
   if (nblk <= 0) return 0;
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, TW>), dim3((unsigned)nblk), dim3(512), 0, st, p);
   return (int)hipGetLastError();
+}
+
+// Output-channel tile: 128 unless the grid is small -- fewer than 256 blocks
+// even at the finest split (4 pixel tiles per block) -- where 64-channel tiles
+// double the blocks (the ResNet34 encoder's 64^2 / 32^2 / 16^2 levels: 128
+// blocks, half the chip, with 128-channel tiles)
+int g_w3_small = 1;  // vu_gemm_set_tuning(VU_TUNE_W3_SMALL, ...): 0 = round-2 behaviour (A/B runs)
+
+int pick_bi(const VuGemmWgrad& p) {
+  if (p.ni <= 64 || p.q.W % 32 != 0) return 64;  // (128 x 16-wide tiles would spill)
+  if (!g_w3_small) return 128;
+  const int64_t T = (int64_t)p.q.N * p.q.H * p.q.W / TP;
+  const int64_t blocks128 = (int64_t)((p.ni + 127) / 128) * (p.q.C / 64) * (T / 4 > 0 ? T / 4 : 1);
+  return blocks128 < 256 ? 64 : 128;
 }
 
 }  // namespace
 
 // (BI, BJ = 9*64) when the halo kernel serves this problem, else 0: bf16, dy
 // a plain 1x1 NHWC map, x a 3x3 stride-1 pad-1 gather of 64-channel aligned
-// sources over an image whose width is a multiple of 32 and height of 4.
+// sources over an image whose width is a multiple of 32 and height of 4 (or
+// width a multiple of 16 and height of 8).
 // Splits must then be whole 128-pixel tiles (m_per_split % 128 == 0).
 int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
   const VuGather& a = p.p;
@@ -299,16 +322,26 @@ int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
   if (g.C % 64 || p.nj != 9 * g.C) return 0;
   for (int t = 0; t < g.nsrc; ++t)
     if (g.cend[t] % 64 || g.stride[t] % 8) return 0;
-  if (g.W % TW || g.H % TH) return 0;
+  const int tw = g.W % 32 == 0 ? 32 : (g.W % 16 == 0 && g_w3_small ? 16 : 0);
+  if (!tw || g.H % (TP / tw)) return 0;
   if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
-  if ((int64_t)TH * g.W * a.stride[0] >= (int64_t)1 << 31) return 0;   // 32-bit dy slot offsets
-  *bi = p.ni <= 64 ? 64 : 128;
+  if ((int64_t)(TP / tw) * g.W * a.stride[0] >= (int64_t)1 << 31) return 0;   // 32-bit dy slot offsets
+  *bi = pick_bi(p);
   *bj = 9 * 64;
   return 1;
 }
 
 int gemm_wgrad_v3_launch(const VuGemmWgrad& p, hipStream_t st) {
   if (p.m_per_split % TP) return (int)hipErrorInvalidValue;
-  if (p.ni <= 64) return launch<64>(p, st);
-  return launch<128>(p, st);
+  if (p.q.W % 32 != 0) return launch<64, 16>(p, st);
+  if (pick_bi(p) == 64) return launch<64, 32>(p, st);
+  return launch<128, 32>(p, st);
+}
+
+int gemm_wgrad_v3_tune(int key, int value) {
+  if (key == VU_TUNE_W3_SMALL) {
+    g_w3_small = value != 0;
+    return 0;
+  }
+  return -1;
 }
