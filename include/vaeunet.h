@@ -272,6 +272,18 @@ int vu_bn_eval_coeffs(const float* gamma, const float* beta,
                       float eps, int C, float* scale, float* shift,
                       float* save_mean, float* save_invstd, void* stream);
 /* y = max(0, x*scale[c] + shift[c]) (relu=1) or x*scale+shift (relu=0) */
+/* Train-mode BatchNorm forward in ONE launch for small tensors (tiles <=
+ * 256 partial-statistics tiles, C % 32 == 0, strides % 8 == 0:
+ * vu_bn_fwd_fused_supported): vu_bn_finalize's statistics (same fp64 group-mean
+ * combine, coef = [scale; shift; mean; invstd] rows of C floats, running
+ * statistics, num_batches_tracked) and out = relu?(y*scale + shift
+ * [+ res*rscale + rshift | + res]) (vu_bn_apply / vu_bn_add_relu). */
+int vu_bn_fwd_fused_supported(int tiles, int C, int64_t ys, int64_t rs, int64_t os);
+int vu_bn_fwd_fused(const float* psum, const float* pm2, int tiles, int64_t tile_rows, int64_t P, int C,
+                    const float* gamma, const float* beta, float* running_mean, float* running_var,
+                    int64_t* num_batches_tracked, float momentum, float eps, float* coef, const void* y,
+                    int64_t ys, const void* res, int64_t rs, const float* rscale, const float* rshift,
+                    void* out, int64_t os, int relu, int dtype, void* stream);
 int vu_bn_apply(const void* x, int64_t x_stride, void* y, int64_t y_stride,
                 int64_t P, int C, const float* scale, const float* shift,
                 int relu, int dtype, void* stream);
@@ -280,6 +292,15 @@ int vu_bn_apply(const void* x, int64_t x_stride, void* y, int64_t y_stride,
  * coefficients (k1, k2, k3) with dx = k1*dz + k2*(x - mean) + k3.
  * train = 1: mean/invstd are the batch statistics (differentiated through);
  * train = 0: eval mode, they are constants (k2 = k3 = 0). */
+/* BatchNorm(+ReLU) backward of a small tensor (partial-sum blocks <= 128:
+ * vu_bn_bwd_fused_supported) in two launches: vu_bn_bwd_reduce's partial pass,
+ * then its fp64 finish (dgamma, dbeta written or accumulated) folded into
+ * vu_bn_bwd_apply's pass.  workspace: vu_reduce_workspace_bytes(P, C). */
+int vu_bn_bwd_fused_supported(int64_t P, int C, int64_t dys, int64_t xs, int64_t dxs);
+int vu_bn_bwd_fused(const void* dy, int64_t dys, const void* x, int64_t xs, int64_t P, int C,
+                    const float* scale, const float* shift, const float* mean, const float* invstd,
+                    const float* gamma, int relu, int train, float* dgamma, float* dbeta,
+                    int accumulate, void* dx, int64_t dxs, float* workspace, int dtype, void* stream);
 int vu_bn_bwd_reduce(const void* dy, int64_t dy_stride, const void* x,
                      int64_t x_stride, int64_t P, int C, const float* scale,
                      const float* shift, const float* mean,

@@ -94,6 +94,12 @@ _SIGS = {
     "vu_bn_finalize_workspace_bytes": (_l, [_i, _i]),
     "vu_bn_eval_coeffs": (_i, [_p, _p, _p, _p, _f, _i, _p, _p, _p, _p, _p]),
     "vu_bn_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _i, _i, _p]),
+    "vu_bn_fwd_fused_supported": (_i, [_i, _i, _l, _l, _l]),
+    "vu_bn_bwd_fused_supported": (_i, [_l, _i, _l, _l, _l]),
+    "vu_bn_bwd_fused": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _p, _l, _p, _i,
+                             _p]),
+    "vu_bn_fwd_fused": (_i, [_p, _p, _i, _l, _l, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _l, _p, _l, _p, _p,
+                             _p, _l, _i, _i, _p]),
     "vu_bn_bwd_reduce": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i,
                               _p, _p, _i, _p]),
     "vu_bn_bwd_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _i, _p, _l, _i, _p]),

@@ -482,6 +482,253 @@ __global__ void bn_apply_maxpool_kernel(const T* y, int64_t ys, T* a, int64_t as
   }
 }
 
+// ---- BatchNorm forward for SMALL tensors: finalize + apply in one launch ----
+// The ResNet34 encoder's 64^2-16^2 levels (and the U-Net's 32^2 level) have
+// 16-256 partial-statistics tiles; there the two finalize launches and the
+// apply are each latency-bound (~5-10 us for a few MB), so a layer spent more
+// time in its BatchNorm than in its convolution.  Here a block owns 32
+// channels x a pixel range: it combines the (sum, centered M2) partials of its
+// 32 channels itself (fp64, the exact group-mean form of bn_stats_stage1 /
+// stage2), then applies out = [relu](y*scale + shift [+ residual]) to its
+// pixels.  The blocks of one channel group repeat the (small) combine; the
+// first writes the coefficients (scale, shift, mean, invstd) and the running
+// statistics.  256 threads = 32 channels x 8 tile lanes (combine), then 4
+// lanes x 8 channels x 64 pixel rows (apply).
+constexpr int BNF_MAXT = 256;  // tiles a block combines (8 tile lanes x 32)
+
+struct BnFusedArgs {
+  const float* psum; const float* pm2; int tiles; int64_t tile_rows; int64_t P; int C;
+  const float* gamma; const float* beta; float* rmean; float* rvar; int64_t* nbt; float momentum; float eps;
+  float* coef;                               // [4][C]: scale, shift, mean, invstd
+  const void* y; int64_t ys;
+  const void* res; int64_t rs; const float* rsc; const float* rsh;   // optional residual (+ its BN)
+  void* out; int64_t os; int relu; int split;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_fwd_fused_kernel(BnFusedArgs a) {
+  __shared__ double shd[8][32];
+  __shared__ float ssc[32], ssh[32];
+  const int cg = blockIdx.x / a.split, sp = blockIdx.x - cg * a.split;
+  const int tid = threadIdx.x;
+  // ---- combine: lane (cl, tl) takes tiles tl, tl + 8, ... of channel cg*32 + cl
+  {
+    const int cl = tid & 31, tl = tid >> 5;
+    const int c = cg * 32 + cl;
+    constexpr int U = BNF_MAXT / 8;
+    float sv[U], mv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = min(tl + 8 * u, a.tiles - 1);  // clamped, unconditional loads
+      sv[u] = a.psum[(int64_t)t * a.C + c];
+      mv[u] = a.pm2[(int64_t)t * a.C + c];
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += tl + 8 * u < a.tiles ? (double)sv[u] : 0.0;
+    shd[tl][cl] = s;
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tot += shd[k][cl];
+    const double m = tot / (double)a.P;
+    __syncthreads();
+    double q = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tl + 8 * u;
+      if (t < a.tiles) {
+        const int64_t nt64 = a.P - (int64_t)t * a.tile_rows;
+        const double nt = (double)(nt64 > a.tile_rows ? a.tile_rows : nt64);
+        const double d = (double)sv[u] / nt - m;
+        q += (double)mv[u] + nt * d * d;
+      }
+    }
+    shd[tl][cl] = q;
+    __syncthreads();
+    if (tl == 0) {
+      double M2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) M2 += shd[k][cl];
+      const double n = (double)a.P;
+      const double var = M2 / n;
+      const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
+      const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+      const float mean = (float)m;
+      const float scale = g * invstd, shift = b - mean * g * invstd;
+      ssc[cl] = scale;
+      ssh[cl] = shift;
+      if (sp == 0) {
+        a.coef[c] = scale;
+        a.coef[a.C + c] = shift;
+        a.coef[2 * a.C + c] = mean;
+        a.coef[3 * a.C + c] = invstd;
+        if (a.nbt && c == 0) a.nbt[0] += 1;
+        if (a.rmean && a.momentum != 0.f) {
+          const double unb = n > 1 ? M2 / (n - 1) : var;
+          a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * mean;
+          a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * (float)unb;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- apply over this block's pixel range
+  const int cv = tid & 3, row = tid >> 2;
+  const int c = cg * 32 + cv * 8;
+  float sc[8], sh[8], rsc[8], rsh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = ssc[cv * 8 + i];
+    sh[i] = ssh[cv * 8 + i];
+    rsc[i] = a.rsc ? a.rsc[c + i] : 1.f;
+    rsh[i] = a.rsc ? a.rsh[c + i] : 0.f;
+  }
+  const int64_t per = (a.P + a.split - 1) / a.split;
+  const int64_t p_beg = (int64_t)sp * per, p_end = min(a.P, p_beg + per);
+  const T* y = reinterpret_cast<const T*>(a.y);
+  const T* r = reinterpret_cast<const T*>(a.res);
+  T* out = reinterpret_cast<T*>(a.out);
+  for (int64_t p0 = p_beg + row; p0 < p_end; p0 += 64 * UNR) {
+    Vec8<T> vy[UNR], vr[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * 64;
+      if (p < p_end) {
+        vy[u].load(y + p * a.ys + c);
+        if (r) vr[u].load(r + p * a.rs + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * 64;
+      if (p >= p_end) continue;
+      Vec8<T> vo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float z = vy[u].get(i) * sc[i] + sh[i];
+        if (r) {
+          float rr = vr[u].get(i);
+          if (a.rsc) rr = rr * rsc[i] + rsh[i];
+          z = z + rr;
+        }
+        vo.set(i, a.relu ? fmaxf(z, 0.f) : z);
+      }
+      vo.store(out + p * a.os + c);
+    }
+  }
+}
+
+// ---- BatchNorm backward for SMALL tensors: the fp64 finish of the per-channel
+//      sums folded into the apply pass (bn_bwd_final + bn_bwd_apply in one
+//      launch; the partial pass chan_partial_kernel stays) ----
+// A block owns 32 channels x a pixel range; it sums the <= 128 partial rows
+// of its channels itself (fp64), forms k1 = gamma*invstd, k2 = -k1*invstd*
+// sum(dz*xhat)/P, k3 = -k1*sum(dz)/P exactly as bn_bwd_final, and applies
+// dx = k1*dz + k2*(x - mean) + k3; the first block of a channel group writes
+// dgamma / dbeta.
+constexpr int BNB_FUSED_MAXBLK = 128;
+
+struct BnBwdFusedArgs {
+  const void* dy; int64_t dys; const void* x; int64_t xs; int64_t P; int C;
+  const float* scale; const float* shift; const float* mean; const float* invstd; const float* gamma;
+  int relu; int train; const float* part; int nblk;
+  float* dgamma; float* dbeta; int accumulate;
+  void* dx; int64_t dxs; int split;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_fused_apply_kernel(BnBwdFusedArgs a) {
+  __shared__ double shd[2][8][32];
+  __shared__ float sk[3][32];
+  const int cg = blockIdx.x / a.split, sp = blockIdx.x - cg * a.split;
+  const int tid = threadIdx.x;
+  {
+    const int cl = tid & 31, tl = tid >> 5;
+    const int c = cg * 32 + cl;
+    double s0 = 0.0, s1 = 0.0;
+    for (int r0 = tl; r0 < a.nblk; r0 += 64) {
+      float v0[8], v1[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = min(r0 + 8 * u, a.nblk - 1);  // clamped, unconditional loads
+        v0[u] = a.part[((int64_t)r * 2 + 0) * a.C + c];
+        v1[u] = a.part[((int64_t)r * 2 + 1) * a.C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + 8 * u < a.nblk) {
+          s0 += (double)v0[u];
+          s1 += (double)v1[u];
+        }
+    }
+    shd[0][tl][cl] = s0;
+    shd[1][tl][cl] = s1;
+    __syncthreads();
+    if (tl == 0) {
+      double S0 = 0.0, S1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        S0 += shd[0][k][cl];
+        S1 += shd[1][k][cl];
+      }
+      const float g = a.gamma ? a.gamma[c] : 1.f;
+      const float is = a.invstd[c];
+      const float k1 = g * is;
+      sk[0][cl] = k1;
+      sk[1][cl] = a.train ? (float)(-(double)k1 * is * S1 / (double)a.P) : 0.f;
+      sk[2][cl] = a.train ? (float)(-(double)k1 * S0 / (double)a.P) : 0.f;
+      if (sp == 0) {
+        if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + (float)S1 : (float)S1;
+        if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + (float)S0 : (float)S0;
+      }
+    }
+    __syncthreads();
+  }
+  const int cv = tid & 3, row = tid >> 2;
+  const int c = cg * 32 + cv * 8;
+  float sc[8], sf[8], mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = a.scale[c + i];
+    sf[i] = a.shift[c + i];
+    mu[i] = a.mean[c + i];
+    k1[i] = sk[0][cv * 8 + i];
+    k2[i] = sk[1][cv * 8 + i];
+    k3[i] = sk[2][cv * 8 + i];
+  }
+  const int64_t per = (a.P + a.split - 1) / a.split;
+  const int64_t p_beg = (int64_t)sp * per, p_end = min(a.P, p_beg + per);
+  const T* dy = reinterpret_cast<const T*>(a.dy);
+  const T* x = reinterpret_cast<const T*>(a.x);
+  T* dx = reinterpret_cast<T*>(a.dx);
+  for (int64_t p0 = p_beg + row; p0 < p_end; p0 += 64 * UNR) {
+    Vec8<T> vd[UNR], vx[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * 64;
+      if (p < p_end) {
+        vd[u].load(dy + p * a.dys + c);
+        vx[u].load(x + p * a.xs + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * 64;
+      if (p >= p_end) continue;
+      Vec8<T> vo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = vx[u].get(i);
+        float dz = vd[u].get(i);
+        if (a.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+        vo.set(i, k1[i] * dz + k2[i] * (xv - mu[i]) + k3[i]);
+      }
+      vo.store(dx + p * a.dxs + c);
+    }
+  }
+}
+
 inline unsigned ew_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   if (g > 8192) g = 8192;
@@ -755,5 +1002,68 @@ extern "C" int vu_bn_apply_maxpool2(const void* y, int64_t ys, void* a, int64_t 
   else
     hipLaunchKernelGGL(bn_apply_maxpool_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)y, ys,
                        (float*)a, as, (float*)pool, ps, N, H, W, C, scale, shift, relu);
+  return (int)hipGetLastError();
+}
+
+// Single-launch train-mode BatchNorm forward (finalize + apply [+ residual] [+ ReLU])
+// for small tensors: vu_bn_fwd_fused_supported() says when it applies.
+extern "C" int vu_bn_fwd_fused_supported(int tiles, int C, int64_t ys, int64_t rs, int64_t os) {
+  return tiles >= 1 && tiles <= BNF_MAXT && C % 32 == 0 && ys % 8 == 0 && rs % 8 == 0 && os % 8 == 0;
+}
+
+extern "C" int vu_bn_fwd_fused(const float* psum, const float* pm2, int tiles, int64_t tile_rows, int64_t P, int C,
+                               const float* gamma, const float* beta, float* running_mean, float* running_var,
+                               int64_t* num_batches_tracked, float momentum, float eps, float* coef, const void* y,
+                               int64_t ys, const void* res, int64_t rs, const float* rscale, const float* rshift,
+                               void* out, int64_t os, int relu, int dtype, void* stream) {
+  if (!vu_bn_fwd_fused_supported(tiles, C, ys, res ? rs : 0, os) || P < 1) return (int)hipErrorInvalidValue;
+  if ((rscale == nullptr) != (rshift == nullptr)) return (int)hipErrorInvalidValue;
+  BnFusedArgs a{psum, pm2, tiles, tile_rows, P, C, gamma, beta, running_mean, running_var, num_batches_tracked,
+                momentum, eps, coef, y, ys, res, rs, rscale, rshift, out, os, relu, 1};
+  // pixel splits per 32-channel group: ~256 blocks in all, >= 128 pixels each
+  const int groups = C / 32;
+  int64_t split = (256 + groups - 1) / groups;
+  const int64_t maxs = (P + 127) / 128;
+  if (split > maxs) split = maxs;
+  if (split < 1) split = 1;
+  a.split = (int)split;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VU_BF16)
+    hipLaunchKernelGGL(bn_fwd_fused_kernel<bf16_t>, dim3((unsigned)(groups * split)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(bn_fwd_fused_kernel<float>, dim3((unsigned)(groups * split)), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// BatchNorm(+ReLU) backward for small tensors in two launches (the partial
+// pass, then the fused fp64 finish + apply) instead of three.
+extern "C" int vu_bn_bwd_fused_supported(int64_t P, int C, int64_t dys, int64_t xs, int64_t dxs) {
+  return C % 32 == 0 && chanmap_ok(C, dys, xs) && dxs % 8 == 0 && P >= 1 &&
+         (int)chan_grid(P, C, RED_MAXBLK) <= BNB_FUSED_MAXBLK;
+}
+
+extern "C" int vu_bn_bwd_fused(const void* dy, int64_t dys, const void* x, int64_t xs, int64_t P, int C,
+                               const float* scale, const float* shift, const float* mean, const float* invstd,
+                               const float* gamma, int relu, int train, float* dgamma, float* dbeta,
+                               int accumulate, void* dx, int64_t dxs, float* workspace, int dtype, void* stream) {
+  if (!vu_bn_bwd_fused_supported(P, C, dys, xs, dxs)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  RedArgs r{dy, dys, x, xs, P, C, scale, shift, mean, invstd, relu, workspace, 0, 0, 0, 0, 0, 0};
+  int nblk = 0, rc;
+  rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk) : launch_partial<float, 1>(r, st, nblk);
+  if (rc) return rc;
+  if (nblk > BNB_FUSED_MAXBLK) return (int)hipErrorInvalidValue;
+  BnBwdFusedArgs a{dy, dys, x, xs, P, C, scale, shift, mean, invstd, gamma, relu, train, workspace, nblk,
+                   dgamma, dbeta, accumulate, dx, dxs, 1};
+  const int groups = C / 32;
+  int64_t split = (256 + groups - 1) / groups;
+  const int64_t maxs = (P + 127) / 128;
+  if (split > maxs) split = maxs;
+  if (split < 1) split = 1;
+  a.split = (int)split;
+  if (dtype == VU_BF16)
+    hipLaunchKernelGGL(bn_bwd_fused_apply_kernel<bf16_t>, dim3((unsigned)(groups * split)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(bn_bwd_fused_apply_kernel<float>, dim3((unsigned)(groups * split)), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -384,6 +384,38 @@ def bn_coef(bn, st, C_):
     return K.bn_eval(C_, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
 
 
+FUSED_BN_FWD = True  # small train-mode BatchNorms as one finalize + apply launch (A/B switch)
+FUSED_BN_BWD = True  # small BatchNorm backwards: finish folded into the apply pass (A/B switch)
+
+
+def bn_fwd_apply(bn, st, y, a, relu, M, res=None, rcoef=None):
+    """Train/eval BatchNorm of y into a: a = relu?(BN(y) [+ BN_r(res) | + res]);
+    returns coef.  Small train-mode tensors take the single-launch fused path
+    (kernels.bn_forward_fused); otherwise finalize (bn_coef) + the apply."""
+    C_ = y.shape[1]
+    if FUSED_BN_FWD and bn.training and st is not None:
+        mom = 0.1 if bn.momentum is None else bn.momentum
+        track = bn.track_running_stats and bn.running_mean is not None
+        coef = K.bn_forward_fused(st, C_, bn.weight, bn.bias, bn.running_mean if track else None,
+                                  bn.running_var if track else None,
+                                  bn.num_batches_tracked if track else None, mom if track else 0.0, bn.eps,
+                                  y, a, relu, M.d, res=res, rcoef=rcoef)
+        if coef is not None:
+            return coef
+    coef = bn_coef(bn, st, C_)
+    if res is None:
+        K.bn_apply(y, a, coef, relu, M.d)
+    else:
+        if not relu:
+            raise ValueError("bn_fwd_apply: the residual form always applies ReLU (vu_bn_add_relu)")
+        N, _, H, W = y.shape
+        K.call("vu_bn_add_relu", K.ptr(y), K.pstride(y), K.ptr(coef[0]), K.ptr(coef[1]), K.ptr(res),
+               K.pstride(res), K.ptr(rcoef[0]) if rcoef is not None else None,
+               K.ptr(rcoef[1]) if rcoef is not None else None, N * H * W, C_, K.ptr(a), K.pstride(a),
+               M.d, K.stream())
+    return coef
+
+
 def bn_grad_sinks(bn):
     gw, accw = grad_sink(bn.weight)
     gb, accb = grad_sink(bn.bias)
@@ -405,7 +437,7 @@ def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None):
                            train=bn.training)
     else:
         K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
-                      train=bn.training)
+                      train=bn.training, fused=FUSED_BN_BWD)
     return dx
 
 
@@ -421,11 +453,10 @@ def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
     y = M.act(N, co, H, W)
     st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad), co, y, M.d,
                     stats=bn.training)
-    coef = bn_coef(bn, st, co)
     if defer and K.pool_fusable(y):
-        return None, (y, coef)
+        return None, (y, bn_coef(bn, st, co))
     a = M.act(N, co, H, W)
-    K.bn_apply(y, a, coef, True, M.d)
+    coef = bn_fwd_apply(bn, st, y, a, True, M)
     return a, (y, coef)
 
 

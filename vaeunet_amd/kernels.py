@@ -368,6 +368,24 @@ def bn_finalize(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps):
     return coef  # rows: scale, shift, mean, invstd
 
 
+def bn_forward_fused(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps, y, out, relu, dtype,
+                     res=None, rcoef=None):
+    """Train-mode BatchNorm finalize + apply [+ residual] [+ ReLU] as ONE launch
+    (vu_bn_fwd_fused) when the tensor is small enough; returns coef (rows:
+    scale, shift, mean, invstd), or None when not applicable (the caller then
+    runs bn_finalize + the apply)."""
+    rs = pstride(res) if res is not None else 0
+    if not query("vu_bn_fwd_fused_supported", st.tiles, C_, pstride(y), rs, pstride(out)):
+        return None
+    coef = torch.empty((4, C_), dtype=torch.float32, device=y.device)
+    call("vu_bn_fwd_fused", ptr(st.psum), ptr(st.pm2), st.tiles, st.tile_rows, st.rows, C_,
+         ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), ptr(nbt), momentum, eps, ptr(coef),
+         ptr(y), pstride(y), ptr(res), rs, ptr(rcoef[0]) if rcoef is not None else None,
+         ptr(rcoef[1]) if rcoef is not None else None, ptr(out), pstride(out), 1 if relu else 0, dtype,
+         stream())
+    return coef
+
+
 def bn_eval(C_, gamma, beta, rmean, rvar, eps):
     """Eval-mode coefficients; rows: scale, shift, running mean, 1/sqrt(running var + eps)."""
     coef = torch.empty((4, C_), dtype=torch.float32, device=rmean.device)
@@ -383,15 +401,21 @@ def bn_apply(x, y, coef, relu, dtype):
     return y
 
 
-def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
+def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True, fused=True):
     """dx = BN(+ReLU) backward; writes/accumulates dgamma, dbeta.  train=False:
-    the statistics are constants (eval mode)."""
+    the statistics are constants (eval mode).  fused: small tensors take the
+    two-launch path (vu_bn_bwd_fused) instead of reduce + finish + apply."""
     N, Cc, H, W = x.shape
     P = N * H * W
     dev = x.device
-    k = torch.empty((3, Cc), dtype=torch.float32, device=dev)
     ws = torch.empty(query("vu_reduce_workspace_bytes", P, Cc) // 4 + 1, dtype=torch.float32,
                      device=dev)
+    if fused and query("vu_bn_bwd_fused_supported", P, Cc, pstride(dy), pstride(x), pstride(dx)):
+        call("vu_bn_bwd_fused", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]), ptr(coef[1]),
+             ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0, 1 if train else 0, ptr(dgamma), ptr(dbeta),
+             1 if acc else 0, ptr(dx), pstride(dx), ptr(ws), dtype, stream())
+        return dx
+    k = torch.empty((3, Cc), dtype=torch.float32, device=dev)
     call("vu_bn_bwd_reduce", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
          ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
          1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype,

@@ -122,22 +122,17 @@ def conv_dgrad(M, dy, conv, dx, accumulate, bnb=None):
 def basic_fwd(M, blk, x):
     train = blk.bn1.training
     y1, st1 = conv_fwd(M, [x], blk.conv1, train)
-    c1 = E.bn_coef(blk.bn1, st1, y1.shape[1])
     a1 = torch.empty_like(y1)
-    K.bn_apply(y1, a1, c1, True, M.d)
+    c1 = E.bn_fwd_apply(blk.bn1, st1, y1, a1, True, M)
     y2, st2 = conv_fwd(M, [a1], blk.conv2, train)
-    c2 = E.bn_coef(blk.bn2, st2, y2.shape[1])
     yd = cd = None
     if blk.downsample is not None:
         yd, std = conv_fwd(M, [x], blk.downsample[0], train)
         cd = E.bn_coef(blk.downsample[1], std, yd.shape[1])
     out = torch.empty_like(y2)
-    N, C_, H, W = y2.shape
     r = yd if yd is not None else x
-    K.call("vu_bn_add_relu", K.ptr(y2), K.pstride(y2), K.ptr(c2[0]), K.ptr(c2[1]), K.ptr(r),
-           K.pstride(r), K.ptr(cd[0]) if cd is not None else None,
-           K.ptr(cd[1]) if cd is not None else None, N * H * W, C_, K.ptr(out), K.pstride(out),
-           M.d, K.stream())
+    # out = relu(bn2(y2) + (bn_d(yd) | x))  (timm BasicBlock)
+    c2 = E.bn_fwd_apply(blk.bn2, st2, y2, out, True, M, res=r, rcoef=cd)
     return out, (x, y1, c1, a1, y2, c2, yd, cd, out)
 
 
@@ -175,9 +170,8 @@ def basic_bwd(M, blk, saved, dout, need_dx=True):
 def encoder_fwd(M, enc, xa, cin_pad):
     train = enc.bn1.training
     y0, st0 = conv_fwd(M, [xa], enc.conv1, train, cin_pad=cin_pad)
-    c0 = E.bn_coef(enc.bn1, st0, y0.shape[1])
     f0 = torch.empty_like(y0)
-    K.bn_apply(y0, f0, c0, True, M.d)
+    c0 = E.bn_fwd_apply(enc.bn1, st0, y0, f0, True, M)
     N, C_, H, W = f0.shape
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     pm = M.act(N, C_, Ho, Wo)
@@ -242,9 +236,8 @@ def latent_map(M, z, N, H, W):
 def cbr1x1_fwd(M, seq, x, out=None):
     conv, bn = seq[0], seq[1]
     y, st = conv_fwd(M, [x], conv, bn.training)
-    c = E.bn_coef(bn, st, y.shape[1])
     a = torch.empty_like(y) if out is None else out
-    K.bn_apply(y, a, c, True, M.d)
+    c = E.bn_fwd_apply(bn, st, y, a, True, M)
     return a, (x, y, c)
 
 
