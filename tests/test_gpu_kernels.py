@@ -830,3 +830,30 @@ def test_permute_batch_matches_single_launches():
                    E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8)]
         for a, b in zip(single, batched):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", [
+    # (N, cin, cout, k, H) of a stride-2 conv (ResNet34 downsampling convs and their 1x1 shortcuts)
+    (8, 128, 256, 3, 64), (8, 256, 512, 3, 32), (8, 64, 128, 1, 128), (8, 256, 512, 1, 32), (2, 64, 128, 3, 30)])
+def test_conv_stride2_input_grad_parity_classes(case):
+    """stride-2 input gradient as four parity-class GEMMs scattered onto the
+    sub-lattices (out_mode 2; gemm_fwd2.hip small-grid mode incl. split-K
+    finish, or the generic kernel) vs torch's conv2d_input, bf16 storage."""
+    from vaeunet_amd import _lib, vae_engine as V
+    N, ci, co, k, H = case
+    g = torch.Generator().manual_seed(3)
+    conv = torch.nn.Conv2d(ci, co, k, stride=2, padding=k // 2, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(co, ci, k, k, generator=g) / (k * ci ** 0.5))
+    conv = conv.to(DEV)
+    Ho = (H + 2 * (k // 2) - k) // 2 + 1
+    dy = torch.randn(N, co, Ho, Ho, generator=g).to(torch.bfloat16).float()
+
+    class _M:
+        d = _lib.BF16
+
+    dx = torch.empty(N, ci, H, H, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=CL)
+    V.conv_dgrad(_M, _act(dy, "bf16"), conv, dx, False)
+    wq = conv.weight.detach().cpu().to(torch.bfloat16).float()
+    ref = torch.nn.grad.conv2d_input((N, ci, H, H), wq, dy, stride=2, padding=k // 2)
+    _close(dx, ref, "bf16", what="stride-2 dgrad")

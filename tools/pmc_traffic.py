@@ -14,7 +14,7 @@ import os
 import sys
 
 FAMILY = ("conv3x3_pp_kernel", "conv3x3_halo_kernel", "wgrad3x3_halo_kernel", "conv3x3_pers_kernel", "conv3x3_c64_kernel",
-          "conv3x3_sg_kernel", "splitk_finish_kernel")
+          "conv3x3_sg_kernel")
 
 
 def load(d, counter):

@@ -354,6 +354,10 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
 // (>= 1) when served, else 0.
 bool g_small = true;  // VU_TUNE_V2_SMALL
 
+// (The stride-2 parity-class input gradients -- out_mode 2 -- measured 0.3 %
+// slower end to end on these tiles than on the generic kernel, VAE same-box
+// A/B profiles/r3_ab_parity_v2small.log; they stay there.  splitk_finish_kernel
+// handles out_mode 2 all the same.)
 int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype) {
   if (!g_small || dtype != VU_BF16 || p.out_mode != 0) return 0;
   const VuGather& g = p.a;

@@ -531,7 +531,14 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
       v[q][e] = rnd<bf16_t>(a[e] + bv[e]);
       v[q][4 + e] = rnd<bf16_t>(b[e] + bv[4 + e]);
     }
-    bf16_t* dst = out + m * p.out_stride + p.out_coff + c0;
+    int64_t orow = m;
+    if (p.out_mode == 2) {  // stride-2 sub-lattice (parity-class input gradients)
+      const int64_t hw = (int64_t)p.a.H * p.a.W;
+      const int64_t n = m / hw, rem = m - n * hw;
+      const int h = (int)(rem / p.a.W), w = (int)(rem - (int64_t)h * p.a.W);
+      orow = ((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx;
+    }
+    bf16_t* dst = out + orow * p.out_stride + p.out_coff + c0;
     Vec8<bf16_t> o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o.set(e, v[q][e]);
