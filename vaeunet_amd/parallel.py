@@ -87,9 +87,14 @@ class GradBucketReducer:
                 off += n
 
     def zero_grad(self):
-        """Zero every bucket in place (the bound .grad views included)."""
+        """Zero every bucket in place (the bound .grad views included): one HIP
+        fill per bucket on the GPU (vu_zero), torch on CPU (gloo tests)."""
         for flat in self.flats:
-            flat.zero_()
+            if flat.is_cuda:
+                from . import kernels as K
+                K.call("vu_zero", K.ptr(flat), 0, 1, flat.numel(), K.dcode(flat.dtype), K.stream())
+            else:
+                flat.zero_()
 
     @contextlib.contextmanager
     def no_sync(self):
