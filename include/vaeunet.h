@@ -186,6 +186,13 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     16-pixel-wide images and use 64-channel tiles on small grids; 0 = the
  *     round-2 rules (A/B runs) */
 #define VU_TUNE_W3_SMALL 19
+/*   VU_TUNE_FP8_XM: experiment mode of the fp8 conv (A/B timing only, results
+ *     wrong): 0 off, 1 no MFMAs, 2 no DMA inside the loop */
+#define VU_TUNE_FP8_XM 20
+/*   VU_TUNE_FP8_PP: fp8 conv schedule: 1 (default) one tile per block on the
+ *     ping-pong step loop, 0 the persistent kernel (also used whenever
+ *     VU_TUNE_FP8_GRID caps the grid or an experiment mode is set) */
+#define VU_TUNE_FP8_PP 21
 int vu_gemm_set_tuning(int key, int value);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */

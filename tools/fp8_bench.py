@@ -52,7 +52,11 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--no-bf16", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--tune", default="", help="KEY=VAL,... vu_gemm_set_tuning before the run (A/B)")
     args = ap.parse_args()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(k), int(v))
     dev = torch.device("cuda")
     torch.manual_seed(0)
     B = args.batch

@@ -100,8 +100,10 @@ int cu_count() {
 }
 
 int g_grid = 0;  // VU_TUNE_FP8_GRID: grid cap (tests); 0 = CU count
+int g_xm = 0;    // VU_TUNE_FP8_XM: experiment mode (A/B timing only)
 
-template <int BN>
+// XM: experiment modes (A/B timing only, results wrong): 1 = no MFMAs, 2 = no DMA in the loop
+template <int BN, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_fp8_kernel(VuConvFp8 p) {
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
   constexpr int BM = TH * TW;
@@ -339,19 +341,24 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_kernel(VuConvFp8 p) {
     for (int j = 0; j < 2; ++j) wf[j] = frag32(Bw, wrow + 32 * j, hl);
 #pragma unroll
     for (int i = 0; i < 2; ++i) pf[i] = frag32(A, prow[i] + toff, hl);
-    if (!grp && gs + 2 < S) wstage(0, LB0A);
+    if (XM != 2 && !grp && gs + 2 < S) wstage(0, LB0A);
     pp_barrier();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
+        if (XM == 1)
+          acc[i][j][0] += __builtin_bit_cast(float, wf[j][0] ^ pf[i][1]);
+        else
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     pp_barrier();
 #pragma unroll
     for (int i = 0; i < 2; ++i) pf[i] = frag32(A, prow[2 + i] + toff, hl);
-    if (!grp) {
+    if (XM == 2) {
+      if (!grp) wnext();
+    } else if (!grp) {
       if (gs + 2 < S) {
         wstage(LB0A, LB0);
         wnext();
@@ -373,7 +380,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_kernel(VuConvFp8 p) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[2 + i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[2 + i][j], 0, 0, 0, 0, 0, 0);
+        if (XM == 1)
+          acc[2 + i][j][0] += __builtin_bit_cast(float, wf[j][0] ^ pf[i][1]);
+        else
+          acc[2 + i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[2 + i][j], 0, 0, 0, 0, 0,
+                                                                          0);
     __builtin_amdgcn_s_setprio(0);
     pp_barrier();
     if (++s == nk) {
@@ -384,6 +395,262 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_kernel(VuConvFp8 p) {
   }
   if (!grp) pp_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---- one tile per block on the bf16 ping-pong step loop (gemm_fwd4.hip) ----
+// Round 3: the persistent kernel above spends ~1.8x the cycles per K-step of
+// the bf16 ping-pong kernel (experiment modes: without its MFMAs it runs as
+// fast; without its loop DMA 35 % faster), so fp8 bought only 1.05x.  This
+// is the bf16 kernel's schedule with the fp8 bytes: one block per 8x32 /
+// 16x32 / 32x32-pixel tile, the (chunk, tap) step loop with the weight ring
+// slot = tap % 3, the next chunk's halo issued at tap 0 by half 1 and awaited
+// at tap 8, and the persistent kernel's 32x32x64 fragments, swizzle and
+// register epilogue.  A chunk is 64 e4m3 channels (one 64-byte row), so a
+// step carries twice the MFMA work of a bf16 step for the same DMA bytes.
+template <int BN>
+__global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
+  constexpr int NBW = 3;
+  constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
+  constexpr int BM = TH * TW;
+  static_assert(BM == WM * 128 && BN == WN * 64 && WM * WN == 8, "wave grid");
+  constexpr int HW = TW + 2, HP = (TH + 2) * HW;
+  constexpr int HPIECES = HP * 4;
+  constexpr int NHP1 = (HPIECES + 255) / 256;
+  constexpr int HALO = HP * 64;
+  constexpr int WPIECES = BN * 4;
+  constexpr int LB0 = WPIECES / 256;
+  constexpr int LB0A = (LB0 + 1) / 2;
+  constexpr int WSLOT = BN * 64;
+  constexpr int PD = NBW - 1;
+  constexpr int MAIN = 2 * HALO + NBW * WSLOT;
+  static_assert(MAIN <= 163840 && LB0 >= 1, "LDS / DMA schedule");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+
+  const VuGather& g = p.a;
+  const int H = g.H, W = g.W;
+  const int tx_n = W / TW, ty_n = H / TH;
+  const int mtiles = g.N * ty_n * tx_n;
+  const int ntiles = p.ncol / BN;
+  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int mt = bid / ntiles, nt = bid - mt * ntiles;
+  const int img = mt / (ty_n * tx_n);
+  const int trem = mt - img * (ty_n * tx_n);
+  const int y0 = (trem / tx_n) * TH, x0 = (trem - (trem / tx_n) * tx_n) * TW;
+  const int n0 = nt * BN;
+  const int nchunk = g.C / 64;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid - (wid / WN) * WN;
+  const int grp = wid >> 2;
+  const int gt = tid & 255, gw = wid & 3;
+  const uint8_t* bmat = reinterpret_cast<const uint8_t*>(p.w);
+  const void* zp = (const void*)vu_zero_page8;
+  char* const hbuf = smem;
+  char* const wbuf = smem + 2 * HALO;
+
+  const uint8_t* const src0 = reinterpret_cast<const uint8_t*>(g.src[0]);
+  const uint8_t* const src1 = reinterpret_cast<const uint8_t*>(g.src[1]);
+  const uint8_t* const src2 = reinterpret_cast<const uint8_t*>(g.src[2]);
+  const int64_t st0 = g.stride[0], st1 = g.stride[1], st2 = g.stride[2];
+  const int ce0 = g.cend[0], ce1 = g.nsrc > 2 ? g.cend[1] : (1 << 30);
+  auto halo_chunk = [&](int c, int buf) {
+    int ib = img, yb = y0, xb = x0;
+    asm volatile("" : "+s"(ib), "+s"(yb), "+s"(xb));
+    const int cb = c * 64;
+    const uint8_t* src;
+    int64_t st;
+    if (cb < ce0) {
+      src = src0 + cb;
+      st = st0;
+    } else if (cb < ce1) {
+      src = src1 + (cb - ce0);
+      st = st1;
+    } else {
+      src = src2 + (cb - ce1);
+      st = st2;
+    }
+    src += (int64_t)ib * H * W * st;
+#pragma unroll
+    for (int i = 0; i < NHP1; ++i) {
+      if (i * 256 + gw * 64 >= HPIECES) continue;  // wave-uniform
+      const int P = i * 256 + gt;
+      if (P < HPIECES) {
+        const int px = P >> 2;
+        const int hy = px / HW, hx = px - (px / HW) * HW;
+        const int y = yb - 1 + hy, x = xb - 1 + hx;
+        const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        const void* gp = ok ? (const void*)(src + (int64_t)(y * W + x) * st + pswz(px, P & 3)) : zp;
+        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(hbuf + buf * HALO + (i * 256 + gw * 64) * 16), 16, 0, 0);
+      }
+    }
+  };
+  const uint8_t* const wrow0 = bmat + (int64_t)n0 * p.ldw;
+  auto wstage = [&](int c, int t, int slot, int i0, int i1) {
+    const int k0 = t * g.C + c * 64;
+    char* B = wbuf + slot * WSLOT;
+#pragma unroll
+    for (int i = 0; i < LB0; ++i) {
+      if (i < i0 || i >= i1) continue;
+      const int P = i * 256 + gt;
+      const int row = P >> 2;
+      const void* gp = (const void*)(wrow0 + (int64_t)row * p.ldw + k0 + pswz(row, P & 3));
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * 256 + gw * 64) * 16), 16, 0, 0);
+    }
+  };
+
+  // fragment addressing (as the persistent kernel)
+  const int hl = lane >> 5;
+  int prow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = wm * 128 + i * 32 + (lane & 31);
+    prow[i] = (m / TW) * HW + (m - (m / TW) * TW);
+  }
+  const int rho = lane & 31;
+  const int wrow = wn * 64 + 16 * ((rho >> 2) & 1) + 4 * (rho >> 3) + (rho & 3);  // + 32*j
+  const int cb16 = wn * 64 + 16 * hl;  // acc[i][j][r]: channel cb16 + 32*j + r
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (grp) {
+    halo_chunk(0, 0);
+  } else {
+    wstage(0, 0, 0, 0, LB0);
+    wstage(0, 1, 1, 0, LB0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (grp) pp_barrier();
+
+  int hb = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    const bool next_here = c + 1 < nchunk;
+    const char* Ah = hbuf + hb * HALO;
+    // not unrolled: the compiler would hoist all nine taps' swizzled fragment
+    // addresses out of the loop and spill them
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int ty = (t * 11) >> 5, tx = t - ty * 3;
+      const int toff = ty * HW + tx;
+      const int slot = tx;
+      const char* Bw = wbuf + slot * WSLOT;
+      const int pslot = slot == 0 ? 2 : slot - 1;
+      const int pt = t + PD < 9 ? t + PD : t + PD - 9;
+      const bool pref = t + PD < 9 || next_here;
+      const int pc = t + PD < 9 ? c : c + 1;
+      i32x8 wf[2], pf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wf[j] = frag32(Bw, wrow + 32 * j, hl);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) pf[i] = frag32(Ah, prow[i] + toff, hl);
+      if (!grp && pref) wstage(pc, pt, pslot, 0, LB0A);
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+#pragma unroll
+      for (int i = 0; i < 2; ++i) pf[i] = frag32(Ah, prow[2 + i] + toff, hl);
+      if (!grp) {
+        if (pref) {
+          wstage(pc, pt, pslot, LB0A, LB0);
+          wait_vm((PD - 1) * LB0);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      } else {
+        if (t == 0 && next_here) halo_chunk(c + 1, hb ^ 1);
+        if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[2 + i][j] =
+              __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[2 + i][j], 0, 0, 0, 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    }
+    hb ^= 1;
+  }
+  if (!grp) pp_barrier();
+
+  // ---- register epilogue (the persistent kernel's) ---------------------------
+  const __attribute__((address_space(4))) VuConvFp8* ep =
+      (const __attribute__((address_space(4))) VuConvFp8*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ep));
+  const float xsc = *ep->x_scale;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c0 = n0 + cb16 + 32 * j;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float sc = xsc * ep->w_scale[c0 + r];
+      const float bv = ep->bias ? ep->bias[c0 + r] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][j][r] = rnd<bf16_t>(fmaf(acc[i][j][r], sc, bv));
+    }
+  }
+  if (ep->stat_sum) {
+    const int64_t so = (int64_t)(mt * WM + wm) * ep->ncol + n0 + cb16;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        f32x4 sm, m2;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = r4 * 4 + u;
+          float sv = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sv += acc[i][j][r];
+          sv = half32_sum(sv);
+          const float mean = sv * (1.f / 128);
+          float v = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = acc[i][j][r] - mean;
+            v += d * d;
+          }
+          sm[u] = sv;
+          m2[u] = half32_sum(v);
+        }
+        if ((lane & 31) == 0) {
+          *reinterpret_cast<f32x4*>(ep->stat_sum + so + 32 * j + 4 * r4) = sm;
+          *reinterpret_cast<f32x4*>(ep->stat_m2 + so + 32 * j + 4 * r4) = m2;
+        }
+      }
+  }
+  bf16_t* const out = reinterpret_cast<bf16_t*>(ep->out);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = wm * 128 + i * 32 + (lane & 31);
+    const int ty = m / TW, tx = m - (m / TW) * TW;
+    const int64_t pix = ((int64_t)img * H + y0 + ty) * W + x0 + tx;
+    bf16_t* dst = out + pix * ep->out_stride + ep->out_coff + n0 + cb16;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u32x4 pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = pack2(acc[i][j][8 * h + 2 * e], acc[i][j][8 * h + 2 * e + 1]);
+        *reinterpret_cast<u32x4*>(dst + 32 * j + 8 * h) = pk;
+      }
+  }
 }
 
 template <int BN>
@@ -413,13 +680,24 @@ bool served(const VuConvFp8& p) {
   return pick_bn(p) != 0;
 }
 
+int g_pp = 1;  // VU_TUNE_FP8_PP: 1 (default) one tile per block on the ping-pong step loop, 0 persistent (A/B)
+
 template <int BN>
 int launch(const VuConvFp8& p, hipStream_t st) {
   const VuGather& g = p.a;
   const int64_t tiles = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW) * (p.ncol / BN);
+  if (g_pp && g_xm == 0 && g_grid == 0) {
+    hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN>), dim3((unsigned)tiles), dim3(512), 0, st, p);
+    return (int)hipGetLastError();
+  }
   const int64_t cap = g_grid > 0 ? g_grid : cu_count();
   const int64_t nblk = tiles < cap ? tiles : cap;
-  hipLaunchKernelGGL((conv3x3_fp8_kernel<BN>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  if (g_xm == 1)
+    hipLaunchKernelGGL((conv3x3_fp8_kernel<BN, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  else if (g_xm == 2)
+    hipLaunchKernelGGL((conv3x3_fp8_kernel<BN, 2>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv3x3_fp8_kernel<BN>), dim3((unsigned)nblk), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -514,6 +792,14 @@ int nblocks(int64_t n, int per) {
 int conv_fp8_tune(int key, int value) {
   if (key == VU_TUNE_FP8_GRID) {
     g_grid = value;
+    return 0;
+  }
+  if (key == VU_TUNE_FP8_XM) {
+    g_xm = value;
+    return 0;
+  }
+  if (key == VU_TUNE_FP8_PP) {
+    g_pp = value != 0;
     return 0;
   }
   return -1;
