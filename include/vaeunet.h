@@ -194,6 +194,10 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     VU_TUNE_FP8_GRID caps the grid or an experiment mode is set) */
 #define VU_TUNE_FP8_PP 21
 int vu_gemm_set_tuning(int key, int value);
+/* ABI check: out[0..5] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
+ * VuPermJob, VuMtEntry as this library was compiled (bindings compare their
+ * own struct sizes against it; tests/test_modules.py) */
+void vu_abi_struct_sizes(int64_t* out);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */
 /* *amax (= or max=) max |x| over P pixels x C channels (C % 8 == 0); exact

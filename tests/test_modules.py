@@ -90,6 +90,18 @@ def test_library_exports_every_declared_symbol():
     _lib.lib()  # resolves every signature
 
 
+def test_abi_struct_sizes_match_the_binding():
+    """The ctypes mirrors of the C-ABI descriptors have the compiled sizes (a
+    field added on one side only would shift every later field)."""
+    from vaeunet_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    out = (ctypes.c_int64 * 6)()
+    lib.vu_abi_struct_sizes(out)
+    mine = [ctypes.sizeof(c) for c in (_lib.VuGather, _lib.VuGemmFwd, _lib.VuGemmWgrad, _lib.VuConvFp8,
+                                       _lib.VuPermJob, _lib.VuMtEntry)]
+    assert list(out) == mine, (list(out), mine)
+
+
 def test_product_path_has_no_oracle_or_fallback():
     pkg = os.path.join(ROOT, "vaeunet_amd")
     for fn in os.listdir(pkg):

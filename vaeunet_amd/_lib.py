@@ -75,6 +75,7 @@ _SIGS = {
     "vu_gemm_fwd_workspace_bytes": (_l, [C.POINTER(VuGemmFwd), _i]),
     "vu_gemm_fwd_bnb_tile": (_l, [C.POINTER(VuGemmFwd), _i]),
     "vu_gemm_fwd_kernel": (_i, [C.POINTER(VuGemmFwd), _i]),
+    "vu_abi_struct_sizes": (None, [_p]),
     "vu_bn_bwd_finish": (_i, [_p, _i, _l, _i, _p, _p, _i, _p, _p, _i, _p, _p, _p]),
     "vu_bn_bwd_finish_workspace_bytes": (_l, [_i, _i]),
     "vu_gemm_wgrad": (_i, [C.POINTER(VuGemmWgrad), _i, _p]),

@@ -444,3 +444,12 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);
 }
+
+extern "C" void vu_abi_struct_sizes(int64_t* out) {
+  out[0] = sizeof(VuGather);
+  out[1] = sizeof(VuGemmFwd);
+  out[2] = sizeof(VuGemmWgrad);
+  out[3] = sizeof(VuConvFp8);
+  out[4] = sizeof(VuPermJob);
+  out[5] = sizeof(VuMtEntry);
+}
