@@ -191,7 +191,7 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 #define VU_TUNE_FP8_XM 20
 /*   VU_TUNE_FP8_PP: fp8 conv schedule: 1 (default) one tile per block on the
  *     ping-pong step loop, 0 the persistent kernel (also used whenever
- *     VU_TUNE_FP8_GRID caps the grid or an experiment mode is set) */
+ *     VU_TUNE_FP8_GRID caps the grid) */
 #define VU_TUNE_FP8_PP 21
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..5] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,

@@ -407,7 +407,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_kernel(VuConvFp8 p) {
 // at tap 8, and the persistent kernel's 32x32x64 fragments, swizzle and
 // register epilogue.  A chunk is 64 e4m3 channels (one 64-byte row), so a
 // step carries twice the MFMA work of a bf16 step for the same DMA bytes.
-template <int BN>
+template <int BN, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
   constexpr int NBW = 3;
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -550,19 +550,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
       for (int j = 0; j < 2; ++j) wf[j] = frag32(Bw, wrow + 32 * j, hl);
 #pragma unroll
       for (int i = 0; i < 2; ++i) pf[i] = frag32(Ah, prow[i] + toff, hl);
-      if (!grp && pref) wstage(pc, pt, pslot, 0, LB0A);
+      if (XM != 2 && !grp && pref) wstage(pc, pt, pslot, 0, LB0A);
       pp_barrier();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
+          if (XM == 1)
+            acc[i][j][0] += __builtin_bit_cast(float, wf[j][0] ^ pf[i][1]);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
 #pragma unroll
       for (int i = 0; i < 2; ++i) pf[i] = frag32(Ah, prow[2 + i] + toff, hl);
-      if (!grp) {
+      if (XM == 2) {
+      } else if (!grp) {
         if (pref) {
           wstage(pc, pt, pslot, LB0A, LB0);
           wait_vm((PD - 1) * LB0);
@@ -579,8 +583,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[2 + i][j] =
-              __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[2 + i][j], 0, 0, 0, 0, 0, 0);
+          if (XM == 1)
+            acc[2 + i][j][0] += __builtin_bit_cast(float, wf[j][0] ^ pf[i][1]);
+          else
+            acc[2 + i][j] =
+                __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[2 + i][j], 0, 0, 0, 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
     }
@@ -686,8 +693,13 @@ template <int BN>
 int launch(const VuConvFp8& p, hipStream_t st) {
   const VuGather& g = p.a;
   const int64_t tiles = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW) * (p.ncol / BN);
-  if (g_pp && g_xm == 0 && g_grid == 0) {
-    hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN>), dim3((unsigned)tiles), dim3(512), 0, st, p);
+  if (g_pp && g_grid == 0) {
+    if (g_xm == 1)
+      hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN, 1>), dim3((unsigned)tiles), dim3(512), 0, st, p);
+    else if (g_xm == 2)
+      hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN, 2>), dim3((unsigned)tiles), dim3(512), 0, st, p);
+    else
+      hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN>), dim3((unsigned)tiles), dim3(512), 0, st, p);
     return (int)hipGetLastError();
   }
   const int64_t cap = g_grid > 0 ? g_grid : cu_count();
