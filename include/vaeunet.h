@@ -193,6 +193,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     ping-pong step loop, 0 the persistent kernel (also used whenever
  *     VU_TUNE_FP8_GRID caps the grid) */
 #define VU_TUNE_FP8_PP 21
+/*   VU_TUNE_ATTN: 1 (default) batched attention-gate kernels (U pixel rows /
+ *     vectors of loads in flight per lane), 0 = one row per iteration */
+#define VU_TUNE_ATTN 22
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..5] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry as this library was compiled (bindings compare their

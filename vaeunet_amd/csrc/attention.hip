@@ -112,6 +112,109 @@ __global__ void psi_fwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
   if (threadIdx.x == 0) { psum[blockIdx.x] = tot; pm2[blockIdx.x] = m2; }
 }
 
+// Batched variants (default, VU_TUNE_ATTN = 1): each lane issues the loads of
+// U pixel rows (or U 16-byte vectors) before it uses any of them, so a wave
+// keeps U times the bytes in flight; the loads of out-of-range rows are
+// clamped to the last valid row and their results dropped.  Same pixel -> lane
+// assignment and summation order as the one-row kernels (equal up to the
+// compiler's fma contraction of the per-lane sums).
+int g_attn = 1;
+
+template <typename T, int U>
+__global__ __launch_bounds__(256) void psi_fwd_u_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg,
+                                                        const float* tg, const float* sx, const float* tx,
+                                                        const float* wpsi, const float* bpsi, float* q, float* psum,
+                                                        float* pm2) {
+  __shared__ float sq[TILE];
+  __shared__ float red[4];
+  const int lpp = F >> 3, ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int64_t p0 = (int64_t)blockIdx.x * TILE;
+  const int c = sub * 8;
+  float wsg[8], wtg[8], wsx[8], wtx[8], wp[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wsg[k] = sg[c + k]; wtg[k] = tg[c + k]; wsx[k] = sx[c + k]; wtx[k] = tx[c + k]; wp[k] = wpsi[c + k];
+  }
+  const float b = bpsi[0];
+  const int niter = lpp;  // TILE / (4 * ppw)
+  for (int it = 0; it < niter; it += U) {
+    Vec8<T> va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (it + u < niter) {  // uniform
+        int64_t p = p0 + w * ppw + slot + (it + u) * 4 * ppw;
+        p = p < P ? p : P - 1;
+        va[u].load(ug + p * F + c);
+        vb[u].load(ux + p * F + c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (it + u >= niter) break;
+      const int i = w * ppw + slot + (it + u) * 4 * ppw;
+      const int64_t p = p0 + i;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s = fmaxf(va[u].get(k) * wsg[k] + wtg[k] + vb[u].get(k) * wsx[k] + wtx[k], 0.f);
+        acc += wp[k] * s;
+      }
+      if (p >= P) acc = 0.f;
+      acc = group_sum(acc, lpp) + b;
+      if (sub == 0) {
+        sq[i] = p < P ? acc : 0.f;
+        if (p < P) q[p] = acc;
+      }
+    }
+  }
+  __syncthreads();
+  int64_t nvalid = P - p0 < TILE ? P - p0 : TILE;
+  float v = threadIdx.x < nvalid ? sq[threadIdx.x] : 0.f;
+  float tot = block_sum(v, red);
+  float mean = tot / (float)nvalid;
+  float d = threadIdx.x < nvalid ? sq[threadIdx.x] - mean : 0.f;
+  float m2 = block_sum(d * d, red);
+  if (threadIdx.x == 0) { psum[blockIdx.x] = tot; pm2[blockIdx.x] = m2; }
+}
+
+// out = x * sigmoid(q*s + t): U independent 16-byte vectors per thread and
+// iteration; V = C/8 vectors per pixel, a power of two (shift, no division)
+template <typename T, int U>
+__global__ __launch_bounds__(256) void gate_fwd_u_kernel(const float* q, const float* st, const T* x, int64_t xs,
+                                                         int64_t P, int vsh, float* pmap, T* out, int64_t os) {
+  const int64_t tot = P << vsh;
+  const int vm = (1 << vsh) - 1;
+  const float s = st[0], t = st[1];
+  const int64_t step = (int64_t)gridDim.x * 256 * U;
+  for (int64_t e0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x; e0 < tot; e0 += step) {
+    Vec8<T> v[U];
+    float qv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t e = e0 + u * 256;
+      e = e < tot ? e : tot - 1;
+      const int64_t p = e >> vsh;
+      const int c = (int)(e & vm) * 8;
+      qv[u] = q[p];
+      v[u].load(x + p * xs + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = e0 + u * 256;
+      if (e >= tot) break;
+      const int64_t p = e >> vsh;
+      const int c = (int)(e & vm) * 8;
+      const float pv = 1.f / (1.f + __expf(-(qv[u] * s + t)));
+      if (c == 0 && pmap) pmap[p] = pv;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[u].set(k, v[u].get(k) * pv);
+      v[u].store(out + p * os + c);
+    }
+  }
+}
+
 template <typename T>
 __global__ void gate_fwd_kernel(const float* q, const float* st, const T* x, int64_t xs, int64_t P, int C,
                                 float* pmap, T* out, int64_t os) {
@@ -163,9 +266,117 @@ __global__ void gate_bwd_kernel(const T* dout, int64_t dos, const T* x, int64_t 
   }
 }
 
+// gate backward for C <= 512 (one 8-channel chunk per lane), U pixel rows of
+// loads in flight per lane
+template <typename T, int U>
+__global__ __launch_bounds__(256) void gate_bwd_u_kernel(const T* dout, int64_t dos, const T* x, int64_t xs,
+                                                         const float* pmap, int64_t P, int C, T* dx, int64_t dxs,
+                                                         float* dbnq) {
+  const int lpp = C >> 3;
+  const int ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int c = sub * 8;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t pb = wave * ppw * U; pb < P; pb += nwaves * ppw * U) {
+    Vec8<T> vd[U], vx[U];
+    float pv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t p = pb + u * ppw + slot;
+      p = p < P ? p : P - 1;
+      pv[u] = pmap[p];
+      vd[u].load(dout + p * dos + c);
+      vx[u].load(x + p * xs + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = pb + u * ppw + slot;
+      float acc = 0.f;
+      Vec8<T> vo;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc += vd[u].get(k) * vx[u].get(k);
+        vo.set(k, vd[u].get(k) * pv[u]);
+      }
+      if (p < P) vo.store(dx + p * dxs + c);
+      acc = group_sum(acc, lpp);
+      if (sub == 0 && p < P) dbnq[p] = acc * pv[u] * (1.f - pv[u]);
+    }
+  }
+}
+
 // ds[p,c] = dq[p]*wpsi[c]*(s>0); per-block partials of dwpsi[c] and dbpsi
 // (grid-stride over 256-pixel tiles, so at most MAXB partial rows)
 constexpr int MAXB = 1024;
+
+template <typename T, int U>
+__global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg,
+                                                        const float* tg, const float* sx, const float* tx,
+                                                        const float* wpsi, const float* dq, T* ds, float* part) {
+  __shared__ float sh[256 * 8];
+  __shared__ float sb[256];
+  const int lpp = F >> 3, ppw = 64 / lpp;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sub = lane % lpp, slot = lane / lpp;
+  const int c = sub * 8;
+  float wsg[8], wtg[8], wsx[8], wtx[8], wp[8], dw[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    wsg[k] = sg[c + k]; wtg[k] = tg[c + k]; wsx[k] = sx[c + k]; wtx[k] = tx[c + k]; wp[k] = wpsi[c + k];
+    dw[k] = 0.f;
+  }
+  float db = 0.f;
+  const int niter = lpp;  // TILE / (4 * ppw)
+  for (int64_t p0 = (int64_t)blockIdx.x * TILE; p0 < P; p0 += (int64_t)gridDim.x * TILE) {
+    for (int it = 0; it < niter; it += U) {
+      Vec8<T> va[U], vb[U];
+      float g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (it + u < niter) {
+          int64_t p = p0 + w * ppw + slot + (it + u) * 4 * ppw;
+          p = p < P ? p : P - 1;
+          g[u] = dq[p];
+          va[u].load(ug + p * F + c);
+          vb[u].load(ux + p * F + c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (it + u >= niter) break;
+        const int64_t p = p0 + w * ppw + slot + (it + u) * 4 * ppw;
+        if (p >= P) continue;
+        if (sub == 0) db += g[u];
+        Vec8<T> o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float s = va[u].get(k) * wsg[k] + wtg[k] + vb[u].get(k) * wsx[k] + wtx[k];
+          bool on = s > 0.f;
+          dw[k] += on ? g[u] * s : 0.f;
+          o.set(k, on ? g[u] * wp[k] : 0.f);
+        }
+        o.store(ds + p * F + c);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = dw[k];
+  sb[threadIdx.x] = db;
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < F; cc += 256) {
+    int sb_ = cc >> 3, k = cc & 7;
+    float s = 0.f;
+    for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
+    part[(int64_t)blockIdx.x * (F + 1) + cc] = s;
+  }
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int t = 0; t < 256; ++t) s += sb[t];
+    part[(int64_t)blockIdx.x * (F + 1) + F] = s;
+  }
+}
 
 template <typename T>
 __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg, const float* tg,
@@ -373,6 +584,14 @@ inline bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
 }  // namespace
 
+int attn_tune(int key, int value) {
+  if (key == VU_TUNE_ATTN) {
+    g_attn = value;
+    return 0;
+  }
+  return -1;
+}
+
 #define DISPATCH_T(dtype, ...) \
   if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
 
@@ -386,8 +605,12 @@ extern "C" int vu_attn_psi_fwd(const void* ug, const void* ux, int64_t P, int F,
   if (nblk == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((psi_fwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
-                       sx, tx, wpsi, bpsi, q, psum, pm2);
+    if (g_attn)
+      hipLaunchKernelGGL((psi_fwd_u_kernel<T, 4>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg,
+                         tg, sx, tx, wpsi, bpsi, q, psum, pm2);
+    else
+      hipLaunchKernelGGL((psi_fwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
+                         sx, tx, wpsi, bpsi, q, psum, pm2);
   })
   return (int)hipGetLastError();
 }
@@ -397,9 +620,14 @@ extern "C" int vu_attn_gate_fwd(const float* q, const float* st_, const void* x,
   if (C % 8 != 0 || xs % 8 != 0 || os % 8 != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (P == 0) return 0;
+  const int V = C / 8;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((gate_fwd_kernel<T>), dim3(ew_grid(P * C / 8)), dim3(256), 0, st, q, st_, (const T*)x, xs, P,
-                       C, pmap, (T*)out, os);
+    if (g_attn && pow2(V))
+      hipLaunchKernelGGL((gate_fwd_u_kernel<T, 4>), dim3(ew_grid(P * V / 4)), dim3(256), 0, st, q, st_, (const T*)x,
+                         xs, P, __builtin_ctz(V), pmap, (T*)out, os);
+    else
+      hipLaunchKernelGGL((gate_fwd_kernel<T>), dim3(ew_grid(P * C / 8)), dim3(256), 0, st, q, st_, (const T*)x, xs, P,
+                         C, pmap, (T*)out, os);
   })
   return (int)hipGetLastError();
 }
@@ -410,8 +638,12 @@ extern "C" int vu_attn_gate_bwd(const void* dout, int64_t dos, const void* x, in
   hipStream_t st = (hipStream_t)stream;
   if (P == 0) return 0;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((gate_bwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)dout, dos,
-                       (const T*)x, xs, pmap, P, C, (T*)dx, dxs, dqpre);
+    if (g_attn && C <= 512)
+      hipLaunchKernelGGL((gate_bwd_u_kernel<T, 2>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)dout, dos,
+                         (const T*)x, xs, pmap, P, C, (T*)dx, dxs, dqpre);
+    else
+      hipLaunchKernelGGL((gate_bwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)dout, dos,
+                         (const T*)x, xs, pmap, P, C, (T*)dx, dxs, dqpre);
   })
   return (int)hipGetLastError();
 }
@@ -431,8 +663,12 @@ extern "C" int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F,
   if (nblk > MAXB) nblk = MAXB;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((psi_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
-                       sx, tx, wpsi, dq, (T*)ds, workspace);
+    if (g_attn)
+      hipLaunchKernelGGL((psi_bwd_u_kernel<T, 4>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg,
+                         tg, sx, tx, wpsi, dq, (T*)ds, workspace);
+    else
+      hipLaunchKernelGGL((psi_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P, F, sg, tg,
+                         sx, tx, wpsi, dq, (T*)ds, workspace);
   })
   hipLaunchKernelGGL(part_final, dim3((F + 1 + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, F + 1, dwpsi, F, dbpsi,
                      accumulate);
