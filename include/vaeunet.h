@@ -196,6 +196,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 /*   VU_TUNE_ATTN: 1 (default) batched attention-gate kernels (U pixel rows /
  *     vectors of loads in flight per lane), 0 = one row per iteration */
 #define VU_TUNE_ATTN 22
+/*   VU_TUNE_BN_MINBLK: fewest blocks of the BatchNorm streaming kernels on
+ *     small tensors (default 256; 0 = ~16 pixel rows per thread only) */
+#define VU_TUNE_BN_MINBLK 23
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..5] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry as this library was compiled (bindings compare their

@@ -744,9 +744,27 @@ inline bool chanmap_ok(int C, int64_t s0, int64_t s1, int64_t s2 = 0) {
 }
 
 // blocks for a fixed-channel stream over P pixels: ~16 pixel rows per thread
+// (the size class the fused small-tensor paths are admitted by)
+inline unsigned chan_grid16(int64_t P, int C, int maxblk) {
+  int R = 256 / (C / 8);
+  int64_t g = (P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
+  if (g > maxblk) g = maxblk;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// Launch grid of the streaming kernels: ~16 pixel rows per thread on large
+// tensors, but on small ones at least g_bn_minblk blocks (down to one UNR-deep
+// load round per thread): a 64-block grid whose threads each wait out four
+// dependent load rounds was latency-bound (9 us for the 4 MB of a ResNet34
+// layer3 BN backward).  VU_TUNE_BN_MINBLK, 0 = the 16-row grid only.
+int g_bn_minblk = 256;
 inline unsigned chan_grid(int64_t P, int C, int maxblk) {
   int R = 256 / (C / 8);
   int64_t g = (P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
+  const int64_t g1 = (P + (int64_t)R * UNR - 1) / ((int64_t)R * UNR);
+  const int64_t lo = g1 < g_bn_minblk ? g1 : g_bn_minblk;
+  if (g < lo) g = lo;
   if (g > maxblk) g = maxblk;
   if (g < 1) g = 1;
   return (unsigned)g;
@@ -775,10 +793,10 @@ inline BwdApplyFn bn_bwd_apply_bf16(int64_t P, int C) {
 }
 
 template <typename T, int MODE>
-int launch_partial(const RedArgs& r, hipStream_t st, int& nblk) {
+int launch_partial(const RedArgs& r, hipStream_t st, int& nblk, int maxblk = RED_MAXBLK) {
   bool vec = chanmap_ok(r.C, r.as, MODE == 0 ? 8 : r.bs);
   if (vec) {
-    nblk = (int)chan_grid(r.P, r.C, RED_MAXBLK);
+    nblk = (int)chan_grid(r.P, r.C, maxblk);
     if (std::is_same<T, bf16_t>::value && bn_nt(r.P, r.C, 2))
       hipLaunchKernelGGL((chan_partial_kernel<T, MODE, true>), dim3(nblk), dim3(256), 0, st, r);
     else
@@ -799,6 +817,10 @@ int launch_partial(const RedArgs& r, hipStream_t st, int& nblk) {
 int bn_tune(int key, int value) {
   if (key == VU_TUNE_BN_NT_MB) {
     g_bn_nt_mb = value;
+    return 0;
+  }
+  if (key == VU_TUNE_BN_MINBLK) {
+    g_bn_minblk = value < 0 ? 0 : value;
     return 0;
   }
   return -1;
@@ -1039,7 +1061,7 @@ extern "C" int vu_bn_fwd_fused(const float* psum, const float* pm2, int tiles, i
 // pass, then the fused fp64 finish + apply) instead of three.
 extern "C" int vu_bn_bwd_fused_supported(int64_t P, int C, int64_t dys, int64_t xs, int64_t dxs) {
   return C % 32 == 0 && chanmap_ok(C, dys, xs) && dxs % 8 == 0 && P >= 1 &&
-         (int)chan_grid(P, C, RED_MAXBLK) <= BNB_FUSED_MAXBLK;
+         (int)chan_grid16(P, C, RED_MAXBLK) <= BNB_FUSED_MAXBLK;
 }
 
 extern "C" int vu_bn_bwd_fused(const void* dy, int64_t dys, const void* x, int64_t xs, int64_t P, int C,
@@ -1050,7 +1072,8 @@ extern "C" int vu_bn_bwd_fused(const void* dy, int64_t dys, const void* x, int64
   hipStream_t st = (hipStream_t)stream;
   RedArgs r{dy, dys, x, xs, P, C, scale, shift, mean, invstd, relu, workspace, 0, 0, 0, 0, 0, 0};
   int nblk = 0, rc;
-  rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk) : launch_partial<float, 1>(r, st, nblk);
+  rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk, BNB_FUSED_MAXBLK)
+                        : launch_partial<float, 1>(r, st, nblk, BNB_FUSED_MAXBLK);
   if (rc) return rc;
   if (nblk > BNB_FUSED_MAXBLK) return (int)hipErrorInvalidValue;
   BnBwdFusedArgs a{dy, dys, x, xs, P, C, scale, shift, mean, invstd, gamma, relu, train, workspace, nblk,
