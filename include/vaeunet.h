@@ -350,6 +350,10 @@ int64_t vu_reduce_workspace_bytes(int64_t P, int C);
 int64_t vu_bn_finalize_workspace_bytes(int tiles, int C);
 /* y[p][0..C) = 0 for P pixels at pixel stride ys (channel-slice zero fill) */
 int vu_zero(void* y, int64_t ys, int64_t P, int C, int dtype, void* stream);
+/* zero insertion for a stride-2 conv's input gradient: up (N,H,W,C) holds
+ * dy (N,h,w,C) at the even pixels, zeros elsewhere (C, strides % 8 == 0) */
+int vu_zero_insert2(const void* dy, int64_t dys, int N, int h, int w, int C,
+                    void* up, int64_t ups, int H, int W, int dtype, void* stream);
 /* generic NHWC copy/cast: y[p*ys + c] = x[p*xs + c] (+ y if accumulate) */
 int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys,
             int ydtype, int64_t P, int C, int accumulate, void* stream);

@@ -834,12 +834,18 @@ def test_permute_batch_matches_single_launches():
 
 @pytest.mark.parametrize("case", [
     # (N, cin, cout, k, H) of a stride-2 conv (ResNet34 downsampling convs and their 1x1 shortcuts)
-    (8, 128, 256, 3, 64), (8, 256, 512, 3, 32), (8, 64, 128, 1, 128), (8, 256, 512, 1, 32), (2, 64, 128, 3, 30)])
-def test_conv_stride2_input_grad_parity_classes(case):
-    """stride-2 input gradient as four parity-class GEMMs scattered onto the
-    sub-lattices (out_mode 2; gemm_fwd2.hip small-grid mode incl. split-K
-    finish, or the generic kernel) vs torch's conv2d_input, bf16 storage."""
-    from vaeunet_amd import _lib, vae_engine as V
+    (8, 128, 256, 3, 64), (8, 256, 512, 3, 32), (8, 64, 128, 1, 128), (8, 256, 512, 1, 32), (2, 64, 128, 3, 30),
+    (2, 64, 128, 3, 31)])
+@pytest.mark.parametrize("zi", [True, False])
+@pytest.mark.parametrize("acc", [False, True])
+def test_conv_stride2_input_grad_parity_classes(case, zi, acc):
+    """stride-2 input gradient, bf16 storage, vs torch's conv2d_input: 3x3 as
+    one stride-1 conv over the zero-inserted dy (zi, vu_zero_insert2 + the
+    halo kernels; the default) or as four parity-class GEMMs scattered onto
+    the sub-lattices (out_mode 2; gemm_fwd2.hip small-grid mode incl. split-K
+    finish, or the generic kernel) -- 1x1 shortcuts always the latter;
+    overwrite and accumulate."""
+    from vaeunet_amd import _lib, vae_engine as V, engine as E
     N, ci, co, k, H = case
     g = torch.Generator().manual_seed(3)
     conv = torch.nn.Conv2d(ci, co, k, stride=2, padding=k // 2, bias=False)
@@ -852,8 +858,21 @@ def test_conv_stride2_input_grad_parity_classes(case):
     class _M:
         d = _lib.BF16
 
-    dx = torch.empty(N, ci, H, H, dtype=torch.bfloat16, device=DEV).contiguous(memory_format=CL)
-    V.conv_dgrad(_M, _act(dy, "bf16"), conv, dx, False)
+        @staticmethod
+        def act(n, c, h, w):
+            return K.empty_act(n, c, h, w, torch.bfloat16, DEV)
+
+    K, _ = _k()
+    base = torch.randn(N, ci, H, H, generator=g).to(torch.bfloat16).float()
+    dx = _act(base, "bf16") if acc else torch.empty(N, ci, H, H, dtype=torch.bfloat16, device=DEV).contiguous(
+        memory_format=CL)
+    old = E.S2_ZERO_INSERT_DGRAD
+    E.S2_ZERO_INSERT_DGRAD = zi
+    try:
+        V.conv_dgrad(_M, _act(dy, "bf16"), conv, dx, acc)
+        torch.cuda.synchronize()
+    finally:
+        E.S2_ZERO_INSERT_DGRAD = old
     wq = conv.weight.detach().cpu().to(torch.bfloat16).float()
     ref = torch.nn.grad.conv2d_input((N, ci, H, H), wq, dy, stride=2, padding=k // 2)
-    _close(dx, ref, "bf16", what="stride-2 dgrad")
+    _close(dx, ref + base if acc else ref, "bf16", what="stride-2 dgrad")

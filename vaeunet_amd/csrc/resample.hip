@@ -506,6 +506,49 @@ extern "C" int vu_zero(void* y, int64_t ys, int64_t P, int C, int dtype, void* s
   return (int)hipGetLastError();
 }
 
+namespace {
+// up[n][y][x][c] = (y, x even and (y/2, x/2) inside dy) ? dy[n][y/2][x/2][c] : 0,
+// 16-byte vectors, one pixel row of 8-channel groups per lane group
+template <typename T>
+__global__ void zero_insert2_kernel(const T* dy, int64_t dys, int h, int w, T* up, int64_t ups, int H, int W,
+                                    int C, int64_t P) {
+  const int V = C >> 3;
+  const int64_t tot = P * V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = e / V;
+    const int c = (int)(e - p * V) * 8;
+    const int x = (int)(p % W);
+    const int64_t t = p / W;
+    const int y = (int)(t % H);
+    const int64_t n = t / H;
+    Vec8<T> v;
+    if (((x | y) & 1) == 0 && (y >> 1) < h && (x >> 1) < w)
+      v.load(dy + ((n * h + (y >> 1)) * w + (x >> 1)) * dys + c);
+    else
+      v.zero();
+    v.store(up + p * ups + c);
+  }
+}
+}  // namespace
+
+// Zero insertion for the input gradient of a stride-2 convolution (the VAE
+// encoder's 3x3/s2 convs, unet_resnet.py:131-137 via timm BasicBlock): the
+// (H, W) map holding dy (h, w) at the even pixels and zeros elsewhere, so the
+// input gradient runs as ONE stride-1 3x3 convolution on the halo kernels
+// instead of four small parity-class GEMMs.  C % 8 == 0, strides % 8 == 0.
+extern "C" int vu_zero_insert2(const void* dy, int64_t dys, int N, int h, int w, int C, void* up, int64_t ups,
+                               int H, int W, int dtype, void* stream) {
+  if (C % 8 != 0 || dys % 8 != 0 || ups % 8 != 0 || N < 0 || H < 0 || W < 0) return (int)hipErrorInvalidValue;
+  const int64_t P = (int64_t)N * H * W;
+  if (P == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((zero_insert2_kernel<T>), dim3(ew_grid(P * (C / 8))), dim3(256), 0, st, (const T*)dy, dys, h,
+                       w, (T*)up, ups, H, W, C, P);
+  })
+  return (int)hipGetLastError();
+}
+
 extern "C" int vu_copy(const void* x, int64_t xs, int xdtype, void* y, int64_t ys, int ydtype, int64_t P, int C,
                        int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;

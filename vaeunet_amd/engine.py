@@ -386,6 +386,10 @@ def bn_coef(bn, st, C_):
 
 FUSED_BN_FWD = True  # small train-mode BatchNorms as one finalize + apply launch (A/B switch)
 FUSED_BN_BWD = True  # small BatchNorm backwards: finish folded into the apply pass (A/B switch)
+# bf16 input gradients of 3x3 / stride-2 convs as one stride-1 conv over the
+# zero-inserted output gradient (vu_zero_insert2) instead of four parity-class
+# GEMMs (A/B switch; vae_engine.conv_dgrad)
+S2_ZERO_INSERT_DGRAD = True
 
 
 def bn_fwd_apply(bn, st, y, a, relu, M, res=None, rcoef=None):

@@ -92,6 +92,17 @@ def conv_dgrad(M, dy, conv, dx, accumulate, bnb=None):
     if s != 2:
         raise NotImplementedError("only stride 1 and 2 convolutions")
     Ho, Wo = dy.shape[2], dy.shape[3]
+    if E.S2_ZERO_INSERT_DGRAD and M.d != F32 and k == 3 and p == 1 and dy.shape[1] % 64 == 0 \
+            and ci % 64 == 0 and H <= 2 * Ho and W <= 2 * Wo:
+        # dx[y] = sum_ky dy[(y + 1 - ky) / 2] w[ky] over the even (y + 1 - ky):
+        # the stride-1 input gradient of the zero-inserted dy (one halo-kernel
+        # conv with 4x the MACs, instead of four small parity-class GEMMs)
+        up = M.act(N, dy.shape[1], H, W)
+        K.call("vu_zero_insert2", K.ptr(dy), K.pstride(dy), N, Ho, Wo, dy.shape[1], K.ptr(up), K.pstride(up),
+               H, W, M.d, K.stream())
+        g = K.gather([up], N, H, W, R=3, S=3, oy=-1, ox=-1)
+        K.gemm_fwd(g, E.w3x3_dgrad(conv.weight, M.d), ci, dx, M.d, accumulate=accumulate, kind="dgrad")
+        return dx
     classes = []
     for py in (0, 1):
         for px in (0, 1):
