@@ -196,6 +196,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 /*   VU_TUNE_ATTN: 1 (default) batched attention-gate kernels (U pixel rows /
  *     vectors of loads in flight per lane), 0 = one row per iteration */
 #define VU_TUNE_ATTN 22
+/*   VU_TUNE_FP8_C64: 1 (default) 64 -> 64 fp8 convs on the resident-weight
+ *     tile-stream kernel (statistics row tile 64), 0 = the step-loop kernel */
+#define VU_TUNE_FP8_C64 23
 /*   VU_TUNE_BN_MINBLK: fewest blocks of the BatchNorm streaming kernels on
  *     small tensors (default 256; 0 = ~16 pixel rows per thread only) */
 #define VU_TUNE_BN_MINBLK 23
@@ -239,7 +242,8 @@ typedef struct VuConvFp8 {
   float* stat_sum;
   float* stat_m2;
 } VuConvFp8;
-/* 128 when the kernel serves this problem, else 0 */
+/* statistics row tile (128, or 64 on the 64 -> 64 resident-weight kernel)
+ * when the kernel serves this problem, else 0 */
 int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args);
 int vu_conv3x3_fp8(const VuConvFp8* args, void* stream);
 

@@ -142,3 +142,51 @@ def test_double_conv_fp8_close_to_bf16_path():
         yb = mod(x).float()
     rel = ((y8 - yb).abs().max() / yb.abs().max()).item()
     assert rel < 0.15, rel
+
+
+TUNE_FP8_C64 = 23
+
+
+@pytest.mark.parametrize("shape", [(1, 1024, 1024), (2, 256, 512), (3, 256, 384)])
+def test_conv3x3_fp8_c64_matches_step_loop(shape):
+    """64 -> 64 fp8 conv on the resident-weight tile-stream kernel (default for
+    these shapes; LDS-staged (2) and direct (1) output stores) vs the
+    step-loop kernel (0): the same taps in the same order on
+    the same 32x32x64 MFMA fragments, so the bf16 outputs are bit-identical;
+    the BN partials (64- vs 128-pixel tiles) combine to the same moments."""
+    from vaeunet_amd import _lib, fp8
+    N, H, W = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, 64, H, W, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) / 24.0
+    b = torch.randn(64, generator=g)
+    xa = _act(x)
+    am = fp8.amax([xa])
+    q, dq = fp8.quantize(xa, am)
+    wq, ws = fp8.quantize_weight(w.to(DEV))
+    res = {}
+    for c64 in (2, 1, 0):
+        _lib.call("vu_gemm_set_tuning", TUNE_FP8_C64, c64)
+        try:
+            out, st = fp8.conv3x3([q], dq, wq, ws, 64, bias=b.to(DEV), stats=True)
+            torch.cuda.synchronize()
+            res[c64] = (out, st)
+        finally:
+            _lib.call("vu_gemm_set_tuning", TUNE_FP8_C64, 2)
+    (o2, s2), (o1, s1), (o0, s0) = res[2], res[1], res[0]
+    assert s2.tile_rows == 64 and s1.tile_rows == 64 and s0.tile_rows == 128
+    assert torch.equal(o1, o0)
+    assert torch.equal(o2, o0)
+    assert torch.equal(s2.psum, s1.psum) and torch.equal(s2.pm2, s1.pm2)
+
+    def moments(st):
+        n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
+                         dtype=torch.float64)
+        s = st.psum.double().cpu()
+        mean = s.sum(0) / n.sum()
+        m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+        return mean, m2.sum(0) / n.sum()
+    m1, v1 = moments(s1)
+    m0, v0 = moments(s0)
+    torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-6)

@@ -70,10 +70,13 @@ template <int R>
 VU_DEV float ror_add(float v) {
   return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xf, 0xf, false));
 }
-// sum over the 32 lanes of a half-wave (every lane receives the total)
+// sum over the 32 lanes of a half-wave (every lane receives the total): DPP
+// row sums, then v_permlane16_swap pairs rows 0/1 and 2/3 (a VALU exchange;
+// a __shfl_xor across rows is an LDS ds_bpermute round trip)
 VU_DEV float half32_sum(float v) {
   v = ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v))));
-  return v + __shfl_xor(v, 16, 64);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 VU_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
@@ -660,6 +663,237 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
   }
 }
 
+// ---- 64 -> 64 channels: resident weights, persistent tile stream ----------
+// The two 64-channel 1024^2 layers (inc.2, up4.2) have one 64-byte chunk per
+// pixel: on the step loop above a tile is nine steps long and its prologue
+// (first halo) and epilogue are not overlapped (0.93x the bf16 kernels).  As
+// the bf16 v6 kernel (gemm_fwd6.hip): the 64 x 576-byte weight matrix lands
+// in LDS once per block and stays; a block walks 16 x 32-pixel tiles, the
+// next tile's halo landing in the other buffer while this one computes; wave
+// w owns image rows 2w, 2w+1 (2 pixel x 2 channel 32x32x64 fragments, 36
+// MFMAs per tile); the epilogue (scales, bias, bf16, per-wave statistics of
+// its 64 pixels, stores) runs from registers.
+constexpr int C64_TH = 16, C64_TW = 32;
+constexpr int C64_HW = C64_TW + 2;
+constexpr int C64_HP = (C64_TH + 2) * C64_HW;       // 612 halo pixels
+constexpr int C64_HPIECES = C64_HP * 4;             // 16-byte pieces
+constexpr int C64_NHR = (C64_HPIECES + 511) / 512;  // 5 DMA rounds
+constexpr int C64_HALO = C64_HP * 64;
+constexpr int C64_WBYTES = 9 * 64 * 64;             // [tap][co][64 ci] e4m3
+constexpr int C64_WPIECES = C64_WBYTES / 16;
+constexpr int C64_NWR = (C64_WPIECES + 511) / 512;
+// output staging strip per wave: 32 pixel rows of 128 bytes (+16 B pad)
+constexpr int C64_SP = 144, C64_STRIP = 32 * C64_SP;
+constexpr int C64_LDS = C64_WBYTES + 2 * C64_HALO + 2 * 64 * 4 + 8 * C64_STRIP;
+static_assert(C64_LDS <= 163840, "LDS");
+
+// STG: the bf16 output goes through a private LDS strip per wave and leaves
+// as whole 128-byte pixel rows (1 KiB contiguous per store instruction)
+// instead of 16-byte pieces at a 128-byte pixel stride
+// XM (A/B timing only, results wrong): 1 no MFMAs, 2 no loop halo DMA, 3 no output stores
+template <bool STATS, bool STG, int XM = 0>
+__global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
+  __shared__ __attribute__((aligned(16))) char smem[C64_LDS];
+  char* const wl = smem;
+  char* const hl0 = smem + C64_WBYTES;
+  float* const ssc = reinterpret_cast<float*>(smem + C64_WBYTES + 2 * C64_HALO);  // x_scale * w_scale[c]
+  float* const sbi = ssc + 64;                                                     // bias[c]
+  char* const strip = smem + C64_WBYTES + 2 * C64_HALO + 2 * 64 * 4 + (threadIdx.x >> 6) * C64_STRIP;
+
+  const VuGather& g = p.a;
+  const int H = g.H, W = g.W;
+  const int txn = W / C64_TW, per_img = txn * (H / C64_TH);
+  const int T = g.N * per_img;
+  const int G = gridDim.x;
+  const int lb = xcd_remap(blockIdx.x, G);
+  const int ntile_blk = (T - lb + G - 1) / G;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint8_t* const src = reinterpret_cast<const uint8_t*>(g.src[0]);
+  const int64_t st = g.stride[0];
+  const void* const zp = (const void*)vu_zero_page8;
+
+  // resident weights: tap block t = 64 rows (output channels) of 64 bytes,
+  // piece q of row n holding logical piece q ^ ((n>>2)&3) (pswz)
+  {
+    const uint8_t* bm = reinterpret_cast<const uint8_t*>(p.w);
+#pragma unroll
+    for (int i = 0; i < C64_NWR; ++i) {
+      if (i * 512 + wid * 64 >= C64_WPIECES) continue;  // wave-uniform
+      const int s = i * 512 + tid;
+      const int tap = s >> 8, row = (s >> 2) & 63;
+      const void* gp = (const void*)(bm + (int64_t)row * p.ldw + tap * 64 + pswz(row, s & 3));
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(wl + (i * 512 + wid * 64) * 16), 16, 0, 0);
+    }
+  }
+  if (tid < 64) {
+    ssc[tid] = *p.x_scale * p.w_scale[tid];
+    sbi[tid] = p.bias ? p.bias[tid] : 0.f;
+  }
+  auto halo = [&](int t, int b) {
+    const int img = t / per_img, r = t - (t / per_img) * per_img;
+    const int ty = r / txn, tx = r - (r / txn) * txn;
+    const int y0 = ty * C64_TH - 1, x0 = tx * C64_TW - 1;
+    const uint8_t* s0 = src + (int64_t)img * H * W * st;
+    char* dst = hl0 + b * C64_HALO;
+#pragma unroll
+    for (int i = 0; i < C64_NHR; ++i) {
+      if (i * 512 + wid * 64 >= C64_HPIECES) continue;  // wave-uniform
+      const int s = i * 512 + tid;
+      if (s < C64_HPIECES) {
+        const int px = s >> 2;
+        const int hy = px / C64_HW, hx = px - (px / C64_HW) * C64_HW;
+        const int y = y0 + hy, x = x0 + hx;
+        const bool ok = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        const void* gp = ok ? (const void*)(s0 + (int64_t)(y * W + x) * st + pswz(px, s & 3)) : zp;
+        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(dst + (i * 512 + wid * 64) * 16), 16, 0, 0);
+      }
+    }
+  };
+
+  if (ntile_blk > 0) halo(lb, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int hl = lane >> 5, rho = lane & 31;
+  const int wrow = 16 * ((rho >> 2) & 1) + 4 * (rho >> 3) + (rho & 3);  // + 32*j: channel 16*hl + 32*j + r
+  const int cb16 = 16 * hl;
+  int prow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) prow[i] = (2 * wid + i) * C64_HW + rho;
+
+  f32x16 acc[2][2];
+  int t = lb, b = 0;
+  for (int ti = 0; ti < ntile_blk; ++ti, t += G) {
+    if (XM != 2 && ti + 1 < ntile_blk) halo(t + G, b ^ 1);
+    const char* hb = hl0 + (XM == 2 ? 0 : b) * C64_HALO;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // rolled: unrolled, the compiler hoists the nine taps' fragment reads
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int toff = (tap / 3) * C64_HW + tap % 3;
+      const char* wb = wl + tap * 4096;
+      i32x8 wf[2], pf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wf[j] = frag32(wb, wrow + 32 * j, hl);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) pf[i] = frag32(hb, prow[i] + toff, hl);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (XM == 1)
+            acc[i][j][0] += __builtin_bit_cast(float, wf[j][0] ^ pf[i][1]);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
+    }
+    // ---- epilogue: acc[i][j][r] = pixel (row 2*wid + i, column rho), channel cb16 + 32j + r
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(ssc + cb16 + 32 * j + 4 * q);
+        const f32x4 bi = *reinterpret_cast<const f32x4*>(sbi + cb16 + 32 * j + 4 * q);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) acc[i][j][4 * q + u] = rnd<bf16_t>(fmaf(acc[i][j][4 * q + u], sc[u], bi[u]));
+      }
+    const int img = t / per_img, r0 = t - (t / per_img) * per_img;
+    const int ty = r0 / txn, tx = r0 - (r0 / txn) * txn;
+    if (STATS) {
+      const int64_t so = (int64_t)(t * (C64_TH / 2) + wid) * p.ncol + cb16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          f32x4 sm, m2;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = r4 * 4 + u;
+            const float sv = half32_sum(acc[0][j][r] + acc[1][j][r]);
+            const float mean = sv * (1.f / 64);
+            const float d0 = acc[0][j][r] - mean, d1 = acc[1][j][r] - mean;
+            sm[u] = sv;
+            m2[u] = half32_sum(d0 * d0 + d1 * d1);
+          }
+          if (rho == 0) {
+            *reinterpret_cast<f32x4*>(p.stat_sum + so + 32 * j + 4 * r4) = sm;
+            *reinterpret_cast<f32x4*>(p.stat_m2 + so + 32 * j + 4 * r4) = m2;
+          }
+        }
+    }
+    bf16_t* const out = reinterpret_cast<bf16_t*>(p.out);
+    if (STG) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // this wave's image row 2*wid + i: lane (rho, hl) -> strip row rho
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            u32x4 pk;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pk[e] = pack2(acc[i][j][8 * h + 2 * e], acc[i][j][8 * h + 2 * e + 1]);
+            *reinterpret_cast<u32x4*>(strip + rho * C64_SP + (cb16 + 32 * j + 8 * h) * 2) = pk;
+          }
+        // (private strip: the wave's own LDS writes complete before its reads)
+        const int64_t pix0 = ((int64_t)img * H + ty * C64_TH + 2 * wid + i) * W + tx * C64_TW;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int pr = 8 * k + (lane >> 3), pc = lane & 7;
+          const u32x4 v = *reinterpret_cast<const u32x4*>(strip + pr * C64_SP + pc * 16);
+          if (XM == 3) {
+            if (v[0] == 0x7fc07fc0u && v[3] == 0x12345678u)  // (never: keeps the staging alive)
+              *reinterpret_cast<u32x4*>(out + (pix0 + pr) * p.out_stride + p.out_coff + pc * 8) = v;
+          } else {
+            *reinterpret_cast<u32x4*>(out + (pix0 + pr) * p.out_stride + p.out_coff + pc * 8) = v;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * !STG; ++i) {
+      const int64_t pix = ((int64_t)img * H + ty * C64_TH + 2 * wid + i) * W + tx * C64_TW + rho;
+      bf16_t* dst = out + pix * p.out_stride + p.out_coff + cb16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          u32x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = pack2(acc[i][j][8 * h + 2 * e], acc[i][j][8 * h + 2 * e + 1]);
+          *reinterpret_cast<u32x4*>(dst + 32 * j + 8 * h) = pk;
+        }
+    }
+    // the next tile's halo was issued before this tile's stores: wait for it
+    // only (16 statistics + 8 output stores may stay in flight)
+    if (XM == 3)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (STATS)
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    pp_barrier();  // (a __syncthreads() would drain the stores too)
+    b ^= 1;
+  }
+}
+
+int g_c64 = 2;  // VU_TUNE_FP8_C64: 2 (default) resident-weight kernel, staged stores; 1 direct stores; 0 off
+
+bool c64_ok(const VuConvFp8& p) {
+  const VuGather& g = p.a;
+  if (!g_c64 || g.nsrc != 1 || g.C != 64 || g.cend[0] != 64 || p.ncol != 64) return false;
+  if (g.H % C64_TH != 0 || g.W % C64_TW != 0) return false;
+  const int64_t T = (int64_t)g.N * (g.H / C64_TH) * (g.W / C64_TW);
+  return T >= 2 * (int64_t)cu_count();  // a tile stream per block
+}
+
 template <int BN>
 bool tiles_ok(const VuConvFp8& p) {
   const VuGather& g = p.a;
@@ -814,14 +1048,47 @@ int conv_fp8_tune(int key, int value) {
     g_pp = value != 0;
     return 0;
   }
+  if (key == VU_TUNE_FP8_C64) {
+    g_c64 = value < 0 ? 0 : value;
+    return 0;
+  }
   return -1;
 }
 
-extern "C" int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args) { return served(*args) ? 128 : 0; }
+extern "C" int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args) {
+  if (!served(*args)) return 0;
+  return c64_ok(*args) ? 64 : 128;
+}
 
 extern "C" int vu_conv3x3_fp8(const VuConvFp8* args, void* stream) {
   if (!served(*args)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (c64_ok(*args)) {
+    const VuGather& g = args->a;
+    const int64_t T = (int64_t)g.N * (g.H / C64_TH) * (g.W / C64_TW);
+    const int64_t grid = T < cu_count() ? T : cu_count();
+    if (g_xm >= 1 && g_xm <= 3 && args->stat_sum) {
+      if (g_xm == 1)
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true, 1>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+      else if (g_xm == 2)
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true, 2>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+      else
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true, 3>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+      return (int)hipGetLastError();
+    }
+    if (g_c64 >= 2) {
+      if (args->stat_sum)
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+      else
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+    } else {
+      if (args->stat_sum)
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, false>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+      else
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<false, false>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+    }
+    return (int)hipGetLastError();
+  }
   switch (pick_bn(*args)) {
     case 256: return launch<256>(*args, st);
     case 128: return launch<128>(*args, st);
