@@ -148,13 +148,14 @@ class BnbPart:
 
 
 def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
-             convT=None, kind="fwd", strided=None, bnb=None):
+             convT=None, kind="fwd", strided=None, bnb=None, flops=None):
     """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
     the pixel-shuffle epilogue, strided=(oH,oW,opy,opx) the stride-2 sub-lattice one.
     bnb=(x, coef, relu): also emit the BatchNorm-backward partials of the output
     for the train/eval BN over x (coef = bn_finalize's scale, shift, mean,
     invstd) when the selected kernel can (returns a BnbPart then, else None).
-    Returns Stats if requested."""
+    flops: the algorithmic work the roofline accounting credits this launch
+    with (default 2*M*N*K of the GEMM as launched).  Returns Stats if requested."""
     a = VuGemmFwd()
     a.a = g
     a.b = wmat.data_ptr()
@@ -213,7 +214,7 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
             a.workspace = ws.data_ptr()
     M = g.N * g.H * g.W
     _timed(_gemm_tag(g, kind),
-           2 * M * ncol * g.R * g.S * g.C,
+           2 * M * ncol * g.R * g.S * g.C if flops is None else flops,
            lambda: call("vu_gemm_fwd", C.byref(a), dtype, stream()))
     if bnb is not None:
         return part

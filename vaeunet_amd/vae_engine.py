@@ -98,10 +98,14 @@ def conv_dgrad(M, dy, conv, dx, accumulate, bnb=None):
         # the stride-1 input gradient of the zero-inserted dy (one halo-kernel
         # conv with 4x the MACs, instead of four small parity-class GEMMs)
         up = M.act(N, dy.shape[1], H, W)
-        K.call("vu_zero_insert2", K.ptr(dy), K.pstride(dy), N, Ho, Wo, dy.shape[1], K.ptr(up), K.pstride(up),
-               H, W, M.d, K.stream())
+        # roofline accounting (bench.py): the zero fill's time and only the
+        # algorithmic MACs of the stride-2 gradient (a quarter of the launch's)
+        K._timed("conv3x3_dgrad", 0,
+                 lambda: K.call("vu_zero_insert2", K.ptr(dy), K.pstride(dy), N, Ho, Wo, dy.shape[1], K.ptr(up),
+                                K.pstride(up), H, W, M.d, K.stream()))
         g = K.gather([up], N, H, W, R=3, S=3, oy=-1, ox=-1)
-        K.gemm_fwd(g, E.w3x3_dgrad(conv.weight, M.d), ci, dx, M.d, accumulate=accumulate, kind="dgrad")
+        K.gemm_fwd(g, E.w3x3_dgrad(conv.weight, M.d), ci, dx, M.d, accumulate=accumulate, kind="dgrad",
+                   flops=2 * N * Ho * Wo * dy.shape[1] * 9 * ci)
         return dx
     classes = []
     for py in (0, 1):
