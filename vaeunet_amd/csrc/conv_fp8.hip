@@ -81,6 +81,73 @@ VU_DEV float half32_sum(float v) {
 
 VU_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
 
+// ---- butterfly transpose-reduce over the 32 lanes of a half-wave ----------
+// v[k] (32 slots per lane) -> lane m of the half holds sum over the half's
+// lanes of slot m: each step pairs lanes across one lane bit and halves the
+// array (31 exchanges in all instead of 32 five-step row reductions).  Lane
+// bit 4 by v_permlane16_swap, 3 by row_ror:8, 2 by row_half_mirror +
+// quad reversal, 1 and 0 by quad permutations (all VALU: no LDS crossbar).
+template <int CTRL>
+VU_DEV float dmov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+VU_DEV float lx1(float v) { return dmov<0xB1>(v); }             // lane ^ 1
+VU_DEV float lx2(float v) { return dmov<0x4E>(v); }             // lane ^ 2
+VU_DEV float lx4(float v) { return dmov<0x1B>(dmov<0x141>(v)); }  // lane ^ 4
+VU_DEV float lx8(float v) { return dmov<0x128>(v); }            // lane ^ 8 (row_ror:8)
+
+VU_DEV float bfly32_reduce(const float (&v)[32], int lane) {
+  const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+  float w[16], x[8], y[4], z[2];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 16]), false, false);
+    w[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // even rows: slot k, odd rows: slot k + 16
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = (b3 ? w[k + 8] : w[k]) + lx8(b3 ? w[k] : w[k + 8]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) y[k] = (b2 ? x[k + 4] : x[k]) + lx4(b2 ? x[k] : x[k + 4]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) z[k] = (b1 ? y[k + 2] : y[k]) + lx2(b1 ? y[k] : y[k + 2]);
+  return (b0 ? z[1] : z[0]) + lx1(b0 ? z[0] : z[1]);
+}
+
+// inverse: lane m of a half holds the value of slot m -> every lane gets all 32
+VU_DEV void bfly32_bcast(float m, int lane, float (&out)[32]) {
+  const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+  float z[2], y[4], x[8], w[16];
+  {
+    const float q = lx1(m);
+    z[0] = b0 ? q : m;
+    z[1] = b0 ? m : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float q = lx2(z[k]);
+    y[k] = b1 ? q : z[k];
+    y[k + 2] = b1 ? z[k] : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float q = lx4(y[k]);
+    x[k] = b2 ? q : y[k];
+    x[k + 4] = b2 ? y[k] : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float q = lx8(x[k]);
+    w[k] = b3 ? q : x[k];
+    w[k + 8] = b3 ? x[k] : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w[k]), __float_as_uint(w[k]), false, false);
+    out[k] = __uint_as_float(r[0]);       // slot k (bit 4 clear): the even row's value
+    out[k + 16] = __uint_as_float(r[1]);  // slot k + 16: the odd row's
+  }
+}
+
 // piece swizzle of a 64-byte row (see header)
 VU_DEV int pswz(int row, int piece) { return (piece ^ ((row >> 2) & 3)) << 4; }
 
@@ -690,7 +757,8 @@ static_assert(C64_LDS <= 163840, "LDS");
 // STG: the bf16 output goes through a private LDS strip per wave and leaves
 // as whole 128-byte pixel rows (1 KiB contiguous per store instruction)
 // instead of 16-byte pieces at a 128-byte pixel stride
-// XM (A/B timing only, results wrong): 1 no MFMAs, 2 no loop halo DMA, 3 no output stores
+// XM (A/B timing only, results wrong): 1 no MFMAs, 2 no loop halo DMA, 3 no output stores,
+// 4 no statistics
 template <bool STATS, bool STG, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
   __shared__ __attribute__((aligned(16))) char smem[C64_LDS];
@@ -806,27 +874,31 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
       }
     const int img = t / per_img, r0 = t - (t / per_img) * per_img;
     const int ty = r0 / txn, tx = r0 - (r0 / txn) * txn;
-    if (STATS) {
-      const int64_t so = (int64_t)(t * (C64_TH / 2) + wid) * p.ncol + cb16;
+    if (STATS && XM != 4) {
+      // per-wave (sum, centered M2) of its 64 pixels: slot k = 16j + r of
+      // this lane half (channel 16*hl + 32j + r); after the butterfly lane m
+      // of a half holds slot m, i.e. lane l owns channel
+      // 16*(l>>5) + 32*((l>>4)&1) + (l&15): one 4-byte store per statistic
+      float v[32];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-          f32x4 sm, m2;
+        for (int r = 0; r < 16; ++r) v[16 * j + r] = acc[0][j][r] + acc[1][j][r];
+      const float sv = bfly32_reduce(v, lane);
+      float mb[32];
+      bfly32_bcast(sv * (1.f / 64), lane, mb);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int r = r4 * 4 + u;
-            const float sv = half32_sum(acc[0][j][r] + acc[1][j][r]);
-            const float mean = sv * (1.f / 64);
-            const float d0 = acc[0][j][r] - mean, d1 = acc[1][j][r] - mean;
-            sm[u] = sv;
-            m2[u] = half32_sum(d0 * d0 + d1 * d1);
-          }
-          if (rho == 0) {
-            *reinterpret_cast<f32x4*>(p.stat_sum + so + 32 * j + 4 * r4) = sm;
-            *reinterpret_cast<f32x4*>(p.stat_m2 + so + 32 * j + 4 * r4) = m2;
-          }
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d0 = acc[0][j][r] - mb[16 * j + r], d1 = acc[1][j][r] - mb[16 * j + r];
+          v[16 * j + r] = d0 * d0 + d1 * d1;
         }
+      const float mq = bfly32_reduce(v, lane);
+      const int64_t so = (int64_t)(t * (C64_TH / 2) + wid) * p.ncol + 16 * (lane >> 5) + 32 * ((lane >> 4) & 1) +
+                         (lane & 15);
+      p.stat_sum[so] = sv;
+      p.stat_m2[so] = mq;
     }
     bf16_t* const out = reinterpret_cast<bf16_t*>(p.out);
     if (STG) {
@@ -872,11 +944,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
         }
     }
     // the next tile's halo was issued before this tile's stores: wait for it
-    // only (16 statistics + 8 output stores may stay in flight)
+    // only (2 statistics + 8 output stores may stay in flight)
     if (XM == 3)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (STATS)
-      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (STATS && XM != 4)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // 2 statistics + 8 output stores
     else
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     pp_barrier();  // (a __syncthreads() would drain the stores too)
@@ -1067,8 +1139,10 @@ extern "C" int vu_conv3x3_fp8(const VuConvFp8* args, void* stream) {
     const VuGather& g = args->a;
     const int64_t T = (int64_t)g.N * (g.H / C64_TH) * (g.W / C64_TW);
     const int64_t grid = T < cu_count() ? T : cu_count();
-    if (g_xm >= 1 && g_xm <= 3 && args->stat_sum) {
-      if (g_xm == 1)
+    if (g_xm >= 1 && g_xm <= 4 && args->stat_sum) {
+      if (g_xm == 4)
+        hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true, 4>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+      else if (g_xm == 1)
         hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true, 1>), dim3((unsigned)grid), dim3(512), 0, st, *args);
       else if (g_xm == 2)
         hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, true, 2>), dim3((unsigned)grid), dim3(512), 0, st, *args);
