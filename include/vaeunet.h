@@ -199,6 +199,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 /*   VU_TUNE_FP8_C64: 1 (default) 64 -> 64 fp8 convs on the resident-weight
  *     tile-stream kernel (statistics row tile 64), 0 = the step-loop kernel */
 #define VU_TUNE_FP8_C64 23
+/*   VU_TUNE_FP8_SPLIT: 1 (default) split-K for fp8 grids under one block per
+ *     CU (slabs in VuConvFp8.workspace + the split-K finish), 0 off */
+#define VU_TUNE_FP8_SPLIT 24
 /*   VU_TUNE_BN_MINBLK: fewest blocks of the BatchNorm streaming kernels on
  *     small tensors (default 256; 0 = ~16 pixel rows per thread only) */
 #define VU_TUNE_BN_MINBLK 23
@@ -241,10 +244,15 @@ typedef struct VuConvFp8 {
   int64_t out_stride;
   float* stat_sum;
   float* stat_m2;
+  /* split-K over the input channels for grids under one block per CU:
+   * vu_conv3x3_fp8_workspace_bytes() of fp32 slab space (NULL when 0) */
+  float* workspace;
 } VuConvFp8;
 /* statistics row tile (128, or 64 on the 64 -> 64 resident-weight kernel)
  * when the kernel serves this problem, else 0 */
 int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args);
+/* fp32 split-K slab bytes vu_conv3x3_fp8 needs in args->workspace (0 = none) */
+int64_t vu_conv3x3_fp8_workspace_bytes(const VuConvFp8* args);
 int vu_conv3x3_fp8(const VuConvFp8* args, void* stream);
 
 /* ---- weights ----------------------------------------------------------- */

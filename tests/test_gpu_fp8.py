@@ -66,6 +66,10 @@ FP8_CASES = [
     (2, [64], 32, 64, 64, 3),           # 1024x64 tiles
     (3, [64, 64, 64], 32, 32, 64, 2),   # three sources, odd chunk count
     (1, [64], 1024, 1024, 64, 0),       # config 5 layer shape: 64->64 at 1x64x1024x1024
+    # small grids (tiles < CUs): split-K over chunk ranges + the deterministic finish
+    (2, [1024], 32, 64, 256, 0),        # 16 tiles -> 2 splits (capped: >= 8 chunks per split)
+    (1, [512, 512], 32, 32, 256, 0),    # two sources, the splits meet at the source boundary
+    (1, [512, 1024], 32, 32, 256, 0),   # 24 chunks over 3 splits, one inside the second source
 ]
 
 
@@ -190,3 +194,37 @@ def test_conv3x3_fp8_c64_matches_step_loop(shape):
     m0, v0 = moments(s0)
     torch.testing.assert_close(m1, m0, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(v1, v0, rtol=1e-5, atol=1e-6)
+
+
+TUNE_FP8_SPLIT = 24
+
+
+def test_conv3x3_fp8_split_matches_unsplit():
+    """split-K (default for small grids) vs one block per tile: same MACs,
+    partial tiles scaled before the fp32 slab sum -> equal to fp32 rounding of
+    the accumulation, i.e. bf16 outputs within one rounding step."""
+    from vaeunet_amd import _lib, fp8
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 1024, 64, 64, generator=g)
+    w = torch.randn(512, 1024, 3, 3, generator=g) / (3 * 1024 ** 0.5)
+    xa = _act(x)
+    am = fp8.amax([xa])
+    q, dq = fp8.quantize(xa, am)
+    wq, ws = fp8.quantize_weight(w.to(DEV))
+    outs = []
+    for sp in (1, 0):
+        _lib.call("vu_gemm_set_tuning", TUNE_FP8_SPLIT, sp)
+        try:
+            from vaeunet_amd._lib import VuConvFp8  # noqa: F401
+            out, st = fp8.conv3x3([q], dq, wq, ws, 512, stats=True)
+            torch.cuda.synchronize()
+            outs.append((out.float().cpu(), st))
+        finally:
+            _lib.call("vu_gemm_set_tuning", TUNE_FP8_SPLIT, 1)
+    (a, sa), (b, sb) = outs
+    torch.testing.assert_close(a, b, rtol=8e-3, atol=1e-3)
+    # (the finish's statistics tiles are 128 consecutive pixels, the kernel's
+    # its wave tiles: compare the combined moments)
+    for st, ref in ((sa, a), (sb, b)):
+        mean = st.psum.double().sum(0).cpu() / st.rows
+        torch.testing.assert_close(mean.float(), ref.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)

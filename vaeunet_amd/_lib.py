@@ -53,7 +53,7 @@ class VuGemmWgrad(C.Structure):
 class VuConvFp8(C.Structure):
     _fields_ = [("a", VuGather), ("w", _p), ("ldw", _l), ("ncol", C.c_int32), ("out_coff", C.c_int32),
                 ("x_scale", _p), ("w_scale", _p), ("bias", _p), ("out", _p), ("out_stride", _l),
-                ("stat_sum", _p), ("stat_m2", _p)]
+                ("stat_sum", _p), ("stat_m2", _p), ("workspace", _p)]
 
 
 class VuPermJob(C.Structure):
@@ -87,6 +87,7 @@ _SIGS = {
     "vu_quant_rows_fp8": (_i, [_p, _i, _l, _p, _l, _p, _p]),
     "vu_conv3x3_fp8_row_tile": (_l, [C.POINTER(VuConvFp8)]),
     "vu_conv3x3_fp8": (_i, [C.POINTER(VuConvFp8), _p]),
+    "vu_conv3x3_fp8_workspace_bytes": (_l, [C.POINTER(VuConvFp8)]),
     "vu_permute4_chunk": (_l, []),
     "vu_permute4_batch": (_i, [_p, _i, _l, _p]),
     "vu_permute4": (_i, [_p, _l, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),

@@ -32,7 +32,11 @@
 #include "common.h"
 #include "../../include/vaeunet.h"
 
+#include <cstring>
+
 static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page8[16];
+
+int splitk_finish_launch(const VuGemmFwd& p, hipStream_t st);  // gemm_fwd4.hip
 
 namespace {
 
@@ -477,7 +481,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_kernel(VuConvFp8 p) {
 // at tap 8, and the persistent kernel's 32x32x64 fragments, swizzle and
 // register epilogue.  A chunk is 64 e4m3 channels (one 64-byte row), so a
 // step carries twice the MFMA work of a bf16 step for the same DMA bytes.
-template <int BN, int XM = 0>
+// SPLIT: the block index also picks a contiguous range of 64-channel chunks
+// (grid = tiles x ksplit); the scaled fp32 tile goes to slab kidx and the
+// deterministic split-K finish of gemm_fwd4.hip adds bias, rounds and emits
+// the statistics (grids under one block per CU: the 64^2 level at batch 2)
+template <int BN, int XM = 0, bool SPLIT = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
   constexpr int NBW = 3;
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -501,13 +509,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
   const int tx_n = W / TW, ty_n = H / TH;
   const int mtiles = g.N * ty_n * tx_n;
   const int ntiles = p.ncol / BN;
-  const int bid = xcd_remap(blockIdx.x, mtiles * ntiles);
+  const int btiles = mtiles * ntiles;
+  const int ks = SPLIT ? (int)(gridDim.x / btiles) : 1;
+  const int bid0 = xcd_remap(blockIdx.x, btiles * ks);
+  const int kidx = SPLIT ? bid0 / btiles : 0;
+  const int bid = bid0 - kidx * btiles;
   const int mt = bid / ntiles, nt = bid - mt * ntiles;
   const int img = mt / (ty_n * tx_n);
   const int trem = mt - img * (ty_n * tx_n);
   const int y0 = (trem / tx_n) * TH, x0 = (trem - (trem / tx_n) * tx_n) * TW;
   const int n0 = nt * BN;
   const int nchunk = g.C / 64;
+  const int cbeg = SPLIT ? kidx * nchunk / ks : 0, cend = SPLIT ? (kidx + 1) * nchunk / ks : nchunk;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -590,18 +603,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   if (grp) {
-    halo_chunk(0, 0);
+    halo_chunk(cbeg, 0);
   } else {
-    wstage(0, 0, 0, 0, LB0);
-    wstage(0, 1, 1, 0, LB0);
+    wstage(cbeg, 0, 0, 0, LB0);
+    wstage(cbeg, 1, 1, 0, LB0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
   if (grp) pp_barrier();
 
   int hb = 0;
-  for (int c = 0; c < nchunk; ++c) {
-    const bool next_here = c + 1 < nchunk;
+  for (int c = cbeg; c < cend; ++c) {
+    const bool next_here = c + 1 < cend;
     const char* Ah = hbuf + hb * HALO;
     // not unrolled: the compiler would hoist all nine taps' swizzled fragment
     // addresses out of the loop and spill them
@@ -670,6 +683,27 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_pp_kernel(VuConvFp8 p) {
       (const __attribute__((address_space(4))) VuConvFp8*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(ep));
   const float xsc = *ep->x_scale;
+  if (SPLIT) {
+    // scaled fp32 partial tile -> slab kidx (row = pixel, ncol columns)
+    const int64_t M = (int64_t)g.N * H * W;
+    float* const slab = ep->workspace + (int64_t)kidx * M * ep->ncol;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = wm * 128 + i * 32 + (lane & 31);
+      const int ty = m / TW, tx = m - (m / TW) * TW;
+      float* const row = slab + (((int64_t)img * H + y0 + ty) * W + x0 + tx) * ep->ncol + n0 + cb16;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          f32x4 v;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = acc[i][j][4 * q + u] * (xsc * ep->w_scale[n0 + cb16 + 32 * j + 4 * q + u]);
+          *reinterpret_cast<f32x4*>(row + 32 * j + 4 * q) = v;
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int c0 = n0 + cb16 + 32 * j;
@@ -995,10 +1029,54 @@ bool served(const VuConvFp8& p) {
 
 int g_pp = 1;  // VU_TUNE_FP8_PP: 1 (default) one tile per block on the ping-pong step loop, 0 persistent (A/B)
 
+int g_split = 1;  // VU_TUNE_FP8_SPLIT: 1 (default) split-K for grids under one block per CU, 0 off
+
+template <int BN>
+int64_t bn_tiles(const VuConvFp8& p) {
+  const VuGather& g = p.a;
+  return (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW) * (p.ncol / BN);
+}
+
+// split factor of the step-loop kernel: tiles < CUs -> ceil(CUs / tiles)
+// chunk ranges of >= 8 chunks each (at batch 2 / 1024^2: down4.2, 1024
+// channels, 129 -> 117 us; down4.1 with 512 would be 73 -> 87 us -- the slab
+// round trip costs more than the idle half of the chip there)
+int fp8_ksplit(const VuConvFp8& p) {
+  if (!g_split || !g_pp || g_grid != 0 || c64_ok(p)) return 1;
+  const int bn = pick_bn(p);
+  const int64_t tiles = bn == 256 ? bn_tiles<256>(p) : bn == 128 ? bn_tiles<128>(p) : bn_tiles<64>(p);
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  if (tiles >= cu_count() || M % 128 != 0 || p.ncol % 64 != 0) return 1;
+  int ks = (int)((cu_count() + tiles - 1) / tiles);
+  const int maxks = p.a.C / 64 / 8;
+  if (ks > maxks) ks = maxks;
+  return ks < 2 ? 1 : ks;
+}
+
 template <int BN>
 int launch(const VuConvFp8& p, hipStream_t st) {
   const VuGather& g = p.a;
-  const int64_t tiles = (int64_t)g.N * (g.H / PP<BN>::TH) * (g.W / PP<BN>::TW) * (p.ncol / BN);
+  const int64_t tiles = bn_tiles<BN>(p);
+  const int ks = fp8_ksplit(p);
+  if (ks > 1) {
+    if (!p.workspace) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN, 0, true>), dim3((unsigned)(tiles * ks)), dim3(512), 0, st, p);
+    VuGemmFwd q;
+    memset(&q, 0, sizeof(q));
+    q.a = g;
+    q.ncol = p.ncol;
+    q.out = p.out;
+    q.out_stride = p.out_stride;
+    q.out_coff = p.out_coff;
+    q.bias = p.bias;
+    q.stat_sum = p.stat_sum;
+    q.stat_m2 = p.stat_m2;
+    q.workspace = p.workspace;
+    q.ksplit = ks;
+    q.out_mode = 0;
+    q.accumulate = 0;
+    return splitk_finish_launch(q, st);
+  }
   if (g_pp && g_grid == 0) {
     if (g_xm == 1)
       hipLaunchKernelGGL((conv3x3_fp8_pp_kernel<BN, 1>), dim3((unsigned)tiles), dim3(512), 0, st, p);
@@ -1108,6 +1186,10 @@ int nblocks(int64_t n, int per) {
 }  // namespace
 
 int conv_fp8_tune(int key, int value) {
+  if (key == VU_TUNE_FP8_SPLIT) {
+    g_split = value != 0;
+    return 0;
+  }
   if (key == VU_TUNE_FP8_GRID) {
     g_grid = value;
     return 0;
@@ -1130,6 +1212,12 @@ int conv_fp8_tune(int key, int value) {
 extern "C" int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args) {
   if (!served(*args)) return 0;
   return c64_ok(*args) ? 64 : 128;
+}
+
+extern "C" int64_t vu_conv3x3_fp8_workspace_bytes(const VuConvFp8* args) {
+  if (!served(*args)) return 0;
+  const int ks = fp8_ksplit(*args);
+  return ks > 1 ? (int64_t)ks * args->a.N * args->a.H * args->a.W * args->ncol * (int64_t)sizeof(float) : 0;
 }
 
 extern "C" int vu_conv3x3_fp8(const VuConvFp8* args, void* stream) {

@@ -100,6 +100,12 @@ def conv3x3(xqs, x_dq, wq, w_dq, ncol, out=None, out_coff=0, bias=None, stats=Fa
         pm2 = torch.empty_like(psum)
         a.stat_sum, a.stat_m2 = psum.data_ptr(), pm2.data_ptr()
         st = K.Stats(psum, pm2, tiles, bm, rows)
+    a.workspace = None
+    nb = query("vu_conv3x3_fp8_workspace_bytes", C.byref(a))
+    ws = None
+    if nb > 0:
+        ws = torch.empty(nb // 4, dtype=torch.float32, device=out.device)
+        a.workspace = ws.data_ptr()
     K._timed("conv3x3_fp8_fwd", 2 * rows * ncol * 9 * a.a.C,
              lambda: call("vu_conv3x3_fp8", C.byref(a), stream()))
     return out, st
