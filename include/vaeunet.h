@@ -91,7 +91,11 @@ typedef struct VuGemmFwd {
   const float* bnb_invstd;
   float* bnb_part;
   int32_t bnb_relu;
-  int32_t bnb_pad_;
+  /* epilogue ReLU: out = relu(acc + bias) before the storage rounding and the
+   * statistics (an eval-mode BatchNorm folded into the weights and bias,
+   * vaeunet_amd.engine.fold_bn_eval; with accumulate it applies to the new
+   * term).  0 = none. */
+  int32_t relu;
 } VuGemmFwd;
 
 /* Weight-gradient GEMM: out[s][i][j] = sum_{m in split s} P[m][i] * Q[m][j]

@@ -42,7 +42,7 @@ class VuGemmFwd(C.Structure):
                 ("ksplit", C.c_int32), ("workspace", _p),
                 ("bnb_x", _p), ("bnb_xstride", _l), ("bnb_scale", _p), ("bnb_shift", _p),
                 ("bnb_mean", _p), ("bnb_invstd", _p), ("bnb_part", _p), ("bnb_relu", C.c_int32),
-                ("bnb_pad_", C.c_int32)]
+                ("relu", C.c_int32)]
 
 
 class VuGemmWgrad(C.Structure):

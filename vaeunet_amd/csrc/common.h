@@ -31,6 +31,10 @@ template <typename T> VU_DEV void st1(T* p, float v);
 template <> VU_DEV void st1<float>(float* p, float v) { *p = v; }
 template <> VU_DEV void st1<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
 
+// Epilogue activation of the GEMM kernels (VuGemmFwd.relu): applied to
+// accumulator + bias before the storage rounding.
+VU_DEV float epi_act(float v, int relu) { return relu ? fmaxf(v, 0.f) : v; }
+
 // Round a float to the storage precision (identity for fp32).
 template <typename T> VU_DEV float rnd(float v);
 template <> VU_DEV float rnd<float>(float v) { return v; }

@@ -121,7 +121,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r], p.relu));
     if (p.stat_sum) {
       float* ss = p.stat_sum + (int64_t)mt * p.ncol + c0;
       float* sq = p.stat_m2 + (int64_t)mt * p.ncol + c0;

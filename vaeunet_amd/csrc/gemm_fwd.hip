@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int row = wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
-        E[row * ES + col] = rnd<T>(acc[i][j][r] + bv);
+        E[row * ES + col] = rnd<T>(epi_act(acc[i][j][r] + bv, p.relu));
       }
     }
   __syncthreads();

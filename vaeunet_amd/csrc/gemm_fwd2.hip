@@ -216,7 +216,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int row = wm * (BM / WM) + i * 16 + 4 * (lane >> 4) + r;
-        E[row * ES + col] = (bf16_t)f2bf(acc[i][j][r] + bv);
+        E[row * ES + col] = (bf16_t)f2bf(epi_act(acc[i][j][r] + bv, p.relu));
       }
     }
   __syncthreads();

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int row = wm * (BM / WM) + i * 16 + 4 * (lane >> 4) + r;
-        E[row * ES + col] = rnd<bf16_t>(acc[i][j][r] + bv);
+        E[row * ES + col] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv, p.relu));
       }
     }
   __syncthreads();

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     for (int r = 0; r < 4; ++r) {
       const float bv = ep->bias ? ep->bias[n0 + cbase + j * 16 + r] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
+      for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv, ep->relu));
     }
   }
   if (ep->stat_sum) {
@@ -528,8 +528,8 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
     const f32x4 a = sa[q], b = sb[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[q][e] = rnd<bf16_t>(a[e] + bv[e]);
-      v[q][4 + e] = rnd<bf16_t>(b[e] + bv[4 + e]);
+      v[q][e] = rnd<bf16_t>(epi_act(a[e] + bv[e], p.relu));
+      v[q][4 + e] = rnd<bf16_t>(epi_act(b[e] + bv[4 + e], p.relu));
     }
     int64_t orow = m;
     if (p.out_mode == 2) {  // stride-2 sub-lattice (parity-class input gradients)

@@ -246,7 +246,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv[r]);
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv[r], p.relu));
     }
     // the old values were loaded before stage(s + 2): only that stage may stay in flight
     if (ACC) {

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r]);
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r], p.relu));
     if (STATS) {
       // per-wave (sum, centered M2) of its 64 pixels; lane (kg, l16) keeps
       // channel 16*kg + l16 = lane: one store per statistic

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(acc[f][j][r] + bv[r]);
+        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(epi_act(acc[f][j][r] + bv[r], p.relu));
     }
     if (p.stat_sum) {
 #pragma unroll

@@ -99,6 +99,9 @@ class Mode:
         self.device = device
         self.grad_ready = grad_ready
         self.ov = SideStream.get(device) if OVERLAP_WGRAD else None
+        # no backward can follow a forward run with autograd off: eval-mode
+        # BatchNorms may then fold into their convolutions (fold_bn_eval)
+        self.infer = not torch.is_grad_enabled()
 
     def side(self, fn, *keep):
         """Run ``fn`` (weight-gradient launches) on the side stream, reading
@@ -449,11 +452,45 @@ def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None):
 # DoubleConv  (unet_parts.py:32-49; DecoderBlock conv1/conv2 unet_resnet.py:59-69)
 #   conv3x3(no bias) -> BN -> ReLU -> conv3x3(no bias) -> BN -> ReLU
 # ----------------------------------------------------------------------------
+# Inference (autograd off) with an eval-mode BatchNorm after a convolution:
+# the BN's affine map folds into the convolution (weight rows scaled, bias
+# shifted) and the ReLU runs in the GEMM epilogue, so conv + BN + ReLU is one
+# pass instead of two (visualize_vae.py:61-87,578-652 run the model this way
+# for every latent sample).  A/B switch.
+FOLD_BN_EVAL = True
+
+
+def can_fold(M, bn):
+    return FOLD_BN_EVAL and M.infer and not bn.training and bn.track_running_stats \
+        and bn.running_mean is not None
+
+
+def fold_bn_eval(M, conv, bn, cin_pad=None):
+    """(weight image, bias) of ``conv`` followed by the eval-mode ``bn``:
+    rows of the fp32 image scaled by gamma / sqrt(running_var + eps), bias
+    (conv bias) * scale + beta - running_mean * scale; storage dtype image.
+    Rebuilt per call (the running statistics are written in place by the
+    train-mode kernels, so no version counter would tell a cache)."""
+    co = conv.out_channels
+    coef = bn_coef(bn, None, co)                    # eval rows: scale, shift
+    img = w3x3_fwd(conv.weight, F32, cin_pad)       # [co][R*S*Cp] fp32, cached
+    w = img * coef[0][:, None]
+    if M.d != F32:
+        w = w.to(torch.bfloat16)
+    b = coef[1] if conv.bias is None else conv.bias.float() * coef[0] + coef[1]
+    return w, b.contiguous()
+
+
 def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
     """defer: leave BN + ReLU unapplied (returns a = None) when the consumer
     is a MaxPool2d that applies it in the same pass (down_fwd)."""
     N, _, H, W = srcs[0].shape
     co = conv.out_channels
+    if can_fold(M, bn) and not defer:
+        wf, bf = fold_bn_eval(M, conv, bn, cin_pad)
+        a = M.act(N, co, H, W)
+        K.gemm_fwd(K.gather3x3(srcs), wf, co, a, M.d, bias=bf, relu=True)
+        return a, None
     y = M.act(N, co, H, W)
     st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad), co, y, M.d,
                     stats=bn.training)

@@ -148,14 +148,16 @@ class BnbPart:
 
 
 def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
-             convT=None, kind="fwd", strided=None, bnb=None, flops=None):
+             convT=None, kind="fwd", strided=None, bnb=None, flops=None, relu=False):
     """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
     the pixel-shuffle epilogue, strided=(oH,oW,opy,opx) the stride-2 sub-lattice one.
     bnb=(x, coef, relu): also emit the BatchNorm-backward partials of the output
     for the train/eval BN over x (coef = bn_finalize's scale, shift, mean,
     invstd) when the selected kernel can (returns a BnbPart then, else None).
     flops: the algorithmic work the roofline accounting credits this launch
-    with (default 2*M*N*K of the GEMM as launched).  Returns Stats if requested."""
+    with (default 2*M*N*K of the GEMM as launched).  relu: epilogue ReLU on
+    acc + bias (an eval-mode BatchNorm folded into wmat / bias).  Returns
+    Stats if requested."""
     a = VuGemmFwd()
     a.a = g
     a.b = wmat.data_ptr()
@@ -175,6 +177,7 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
         a.out_mode = 0
     a.bias = bias.data_ptr() if bias is not None else None
     a.accumulate = 1 if accumulate else 0
+    a.relu = 1 if relu else 0
     st = None
     if stats:
         rows = g.N * g.H * g.W

@@ -134,11 +134,25 @@ def conv_dgrad(M, dy, conv, dx, accumulate, bnb=None):
 # ---------------------------------------------------------------------------
 # ResNet34 BasicBlock (timm) and encoder
 # ---------------------------------------------------------------------------
+def conv_bn_relu_fold(M, srcs, conv, bn, cin_pad=None):
+    """relu(BN(conv(x))) with an eval-mode BN folded into the conv and the
+    ReLU in the GEMM epilogue (inference only: engine.can_fold)."""
+    g, Ho, Wo = conv_gather(srcs, conv)
+    wf, bf = E.fold_bn_eval(M, conv, bn, cin_pad)
+    a = M.act(srcs[0].shape[0], conv.out_channels, Ho, Wo)
+    K.gemm_fwd(g, wf, conv.out_channels, a, M.d, bias=bf, relu=True)
+    return a
+
+
 def basic_fwd(M, blk, x):
     train = blk.bn1.training
-    y1, st1 = conv_fwd(M, [x], blk.conv1, train)
-    a1 = torch.empty_like(y1)
-    c1 = E.bn_fwd_apply(blk.bn1, st1, y1, a1, True, M)
+    if E.can_fold(M, blk.bn1):
+        y1 = st1 = c1 = None
+        a1 = conv_bn_relu_fold(M, [x], blk.conv1, blk.bn1)
+    else:
+        y1, st1 = conv_fwd(M, [x], blk.conv1, train)
+        a1 = torch.empty_like(y1)
+        c1 = E.bn_fwd_apply(blk.bn1, st1, y1, a1, True, M)
     y2, st2 = conv_fwd(M, [a1], blk.conv2, train)
     yd = cd = None
     if blk.downsample is not None:
@@ -184,9 +198,13 @@ def basic_bwd(M, blk, saved, dout, need_dx=True):
 
 def encoder_fwd(M, enc, xa, cin_pad):
     train = enc.bn1.training
-    y0, st0 = conv_fwd(M, [xa], enc.conv1, train, cin_pad=cin_pad)
-    f0 = torch.empty_like(y0)
-    c0 = E.bn_fwd_apply(enc.bn1, st0, y0, f0, True, M)
+    if E.can_fold(M, enc.bn1):
+        y0 = c0 = None
+        f0 = conv_bn_relu_fold(M, [xa], enc.conv1, enc.bn1, cin_pad=cin_pad)
+    else:
+        y0, st0 = conv_fwd(M, [xa], enc.conv1, train, cin_pad=cin_pad)
+        f0 = torch.empty_like(y0)
+        c0 = E.bn_fwd_apply(enc.bn1, st0, y0, f0, True, M)
     N, C_, H, W = f0.shape
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     pm = M.act(N, C_, Ho, Wo)
@@ -250,6 +268,8 @@ def latent_map(M, z, N, H, W):
 
 def cbr1x1_fwd(M, seq, x, out=None):
     conv, bn = seq[0], seq[1]
+    if E.can_fold(M, bn) and out is None:
+        return conv_bn_relu_fold(M, [x], conv, bn), None
     y, st = conv_fwd(M, [x], conv, bn.training)
     a = torch.empty_like(y) if out is None else out
     c = E.bn_fwd_apply(bn, st, y, a, True, M)
