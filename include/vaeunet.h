@@ -94,7 +94,7 @@ typedef struct VuGemmFwd {
   /* epilogue ReLU: out = relu(acc + bias) before the storage rounding and the
    * statistics (an eval-mode BatchNorm folded into the weights and bias,
    * vaeunet_amd.engine.fold_bn_eval; with accumulate it applies to the new
-   * term).  0 = none. */
+   * term; not with bnb_part).  0 = none. */
   int32_t relu;
 } VuGemmFwd;
 

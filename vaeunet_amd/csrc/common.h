@@ -32,8 +32,18 @@ template <> VU_DEV void st1<float>(float* p, float v) { *p = v; }
 template <> VU_DEV void st1<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
 
 // Epilogue activation of the GEMM kernels (VuGemmFwd.relu): applied to
-// accumulator + bias before the storage rounding.
+// accumulator + bias before the storage rounding (per element: the
+// LDS-staged kernels).  The register-epilogue kernels instead clamp their
+// rounded accumulators in one block behind a uniform branch (relu commutes
+// with the rounding), so the training instantiations pay one scalar branch.
 VU_DEV float epi_act(float v, int relu) { return relu ? fmaxf(v, 0.f) : v; }
+template <int N>
+VU_DEV void epi_relu(f32x4 (&a)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[i][r] = fmaxf(a[i][r], 0.f);
+}
 
 // Round a float to the storage precision (identity for fp32).
 template <typename T> VU_DEV float rnd(float v);

@@ -33,6 +33,7 @@ constexpr int NT = 256;  // 4 waves
 constexpr int TP = 64;   // pixels per wave tile (4 fragments; also the BN statistics row tile)
 constexpr int NF = TP / 16;
 
+template <bool RELU>  // epilogue ReLU (VuGemmFwd.relu) as its own instantiation
 __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
   const VuGather& g = p.a;
   const int H = g.H, W = g.W, HW = g.H * g.W;
@@ -121,7 +122,10 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r], p.relu));
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r]);
+    if constexpr (RELU)
+#pragma unroll
+      for (int i = 0; i < NF; ++i) epi_relu(acc[i]);
     if (p.stat_sum) {
       float* ss = p.stat_sum + (int64_t)mt * p.ncol + c0;
       float* sq = p.stat_m2 + (int64_t)mt * p.ncol + c0;
@@ -201,6 +205,9 @@ int conv_image_launch(const VuGemmFwd& p, hipStream_t st) {
   int64_t nblk = (tiles + 3) / 4;
   const int64_t cap = 8 * (int64_t)cu_count();  // 2 blocks (8 waves) per CU, 4 rounds
   if (nblk > cap) nblk = cap;
-  hipLaunchKernelGGL(conv3x3_image_kernel, dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  if (p.relu)
+    hipLaunchKernelGGL(conv3x3_image_kernel<true>, dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv3x3_image_kernel<false>, dim3((unsigned)nblk), dim3(NT), 0, st, p);
   return (int)hipGetLastError();
 }

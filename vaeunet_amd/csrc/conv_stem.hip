@@ -131,7 +131,10 @@ __global__ __launch_bounds__(NT, 2) void conv_stem_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv[j][r], p.relu));
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv[j][r]);
+    if (p.relu)
+#pragma unroll
+      for (int i = 0; i < NF; ++i) epi_relu(acc[i]);
     if (p.stat_sum) {
       // lane (gq, r16) keeps channel 16gq + r16 = lane of the wave tile
       float ms = 0.f, mq = 0.f;

@@ -426,6 +426,7 @@ extern "C" int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype) {
 extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   const VuGather& g = args->a;
   if (args->bnb_part && vu_gemm_fwd_bnb_tile(args, dtype) == 0) return (int)hipErrorInvalidValue;
+  if (args->bnb_part && args->relu) return (int)hipErrorInvalidValue;  // (an inference-only epilogue)
   int epc = dtype == VU_BF16 ? 8 : 4;
   if (g.C % epc != 0 || g.nsrc < 1 || g.nsrc > 3) return (int)hipErrorInvalidValue;
   for (int t = 0; t < g.nsrc; ++t)

@@ -80,7 +80,7 @@ VU_DEV float ror_add(float v) {
 }
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
-template <int BN, bool SPLIT, bool BNB>
+template <int BN, bool SPLIT, bool BNB, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -317,9 +317,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     for (int r = 0; r < 4; ++r) {
       const float bv = ep->bias ? ep->bias[n0 + cbase + j * 16 + r] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv, ep->relu));
+      for (int i = 0; i < 8; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
     }
   }
+  if constexpr (RELU)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) epi_relu(acc[i]);
   if (ep->stat_sum) {
     // per-wave statistics tile: its 128 pixels (8 fragments x one 16-lane DPP
     // row), two-pass (sum, centered M2) of the rounded values; lane (g4, x)
@@ -528,9 +531,12 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
     const f32x4 a = sa[q], b = sb[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[q][e] = rnd<bf16_t>(epi_act(a[e] + bv[e], p.relu));
-      v[q][4 + e] = rnd<bf16_t>(epi_act(b[e] + bv[4 + e], p.relu));
+      v[q][e] = rnd<bf16_t>(a[e] + bv[e]);
+      v[q][4 + e] = rnd<bf16_t>(b[e] + bv[4 + e]);
     }
+    if (p.relu)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[q][e] = fmaxf(v[q][e], 0.f);
     int64_t orow = m;
     if (p.out_mode == 2) {  // stride-2 sub-lattice (parity-class input gradients)
       const int64_t hw = (int64_t)p.a.H * p.a.W;
@@ -716,6 +722,8 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
     q.ksplit = 1;
     if (p.bnb_part)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+    else if (p.relu)
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     else
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     return (int)hipGetLastError();

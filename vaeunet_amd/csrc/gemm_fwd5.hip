@@ -53,7 +53,7 @@ VU_DEV float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 struct Pix { int n, h, w; bool ok; };
 
-template <int BN, bool STATS, bool ACC>
+template <int BN, bool STATS, bool ACC, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
 __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
   constexpr int WNC = BN / WN;          // columns per wave: 64 or 32
   constexpr int TM = BM / WM / 16;      // 4 pixel fragments per wave
@@ -246,8 +246,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv[r], p.relu));
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv[r]);
     }
+    if constexpr (RELU)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) epi_relu(acc[i]);
     // the old values were loaded before stage(s + 2): only that stage may stay in flight
     if (ACC) {
       if (s + 2 < S) wait_vm<NL>(); else wait_vm<0>();
@@ -321,7 +324,10 @@ int launch5(const VuGemmFwd& p, hipStream_t st) {
   const int64_t T = (M / BM) * (p.ncol / BN);
   int64_t grid = T < cu_count5() ? T : cu_count5();
   if (g_v5 >= 2 && grid > g_v5) grid = g_v5;
-  hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC>), dim3((unsigned)grid), dim3(NT), 0, st, p);
+  if (p.relu)
+    hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC, true>), dim3((unsigned)grid), dim3(NT), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC>), dim3((unsigned)grid), dim3(NT), 0, st, p);
   return (int)hipGetLastError();
 }
 

@@ -383,8 +383,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
       for (int r = 0; r < 4; ++r) {
         const float bv = ep->bias ? ep->bias[n0 + j * 16 + cl + r] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j][r] = rnd<bf16_t>(epi_act(acc[i][j][r] + bv, ep->relu));
+        for (int i = 0; i < 2; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
       }
+    if (ep->relu)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) epi_relu(acc[i]);
     if (ep->stat_sum) {
       // per-wave (sum, centered M2) over its 32 pixels for every channel
 #pragma unroll

@@ -38,7 +38,7 @@ constexpr int NT = 256;  // 4 waves
 
 // KS: k-steps of 32 (K = 32*KS); NJ: 16-column fragments (N = 16*NJ);
 // NF: 16-pixel fragments per wave tile.
-template <int KS, int NJ, int NF>
+template <int KS, int NJ, int NF, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
 __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
   constexpr int K = 32 * KS, N = 16 * NJ, PX = 16 * NF;
   constexpr int GS = NJ < 4 ? NJ : 4;   // fragments per column group (4*GS consecutive columns per lane)
@@ -126,8 +126,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(epi_act(acc[f][j][r] + bv[r], p.relu));
+        for (int f = 0; f < NF; ++f) acc[f][j][r] = rnd<bf16_t>(acc[f][j][r] + bv[r]);
     }
+    if constexpr (RELU)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) epi_relu(acc[f]);
     if (p.stat_sum) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -248,7 +251,10 @@ int launch_nj(const VuGemmFwd& p, hipStream_t st) {
   int64_t nblk = (tiles + 3) / 4;
   const int64_t cap = 2 * (int64_t)cu_count();
   if (nblk > cap) nblk = cap;
-  hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  if (p.relu)
+    hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF, true>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
   return (int)hipGetLastError();
 }
 
