@@ -37,6 +37,7 @@ constexpr int TP = 64;                  // pixels per wave tile (also the BN sta
 constexpr int NF = TP / 16;             // pixel fragments per wave tile
 constexpr int WLDS = KS * 4 * 64 * 16;  // 53,248 B: [ks][j][lane] 16-byte fragment pieces
 
+template <bool RELU>  // epilogue ReLU (VuGemmFwd.relu) as its own instantiation
 __global__ __launch_bounds__(NT, 2) void conv_stem_kernel(VuGemmFwd p) {
   __shared__ __attribute__((aligned(16))) char wl[WLDS];
   const VuGather& g = p.a;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(NT, 2) void conv_stem_kernel(VuGemmFwd p) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv[j][r]);
-    if (p.relu)
+    if constexpr (RELU)
 #pragma unroll
       for (int i = 0; i < NF; ++i) epi_relu(acc[i]);
     if (p.stat_sum) {
@@ -218,6 +219,9 @@ int conv_stem_launch(const VuGemmFwd& p, hipStream_t st) {
   int64_t nblk = (tiles + 3) / 4;
   const int64_t cap = 2 * (int64_t)cu_count_stem();  // persistent: 2 blocks (8 waves) per CU
   if (nblk > cap) nblk = cap;
-  hipLaunchKernelGGL(conv_stem_kernel, dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  if (p.relu)
+    hipLaunchKernelGGL(conv_stem_kernel<true>, dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv_stem_kernel<false>, dim3((unsigned)nblk), dim3(NT), 0, st, p);
   return (int)hipGetLastError();
 }

@@ -108,7 +108,7 @@ struct SG {
 
 // XM (experiment modes, A/B runs only; 0 in production): 2 = no DMA inside
 // the loop, 4 = no loop (launch + prologue + epilogue)
-template <int TW, int BN, int NBW, bool SPLIT, int XM = 0>
+template <int TW, int BN, int NBW, bool SPLIT, int XM = 0, bool RELU = false>  // RELU: epilogue ReLU
 __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
   using G = SG<TW, BN, NBW>;
   constexpr int TH = G::TH, HW = G::HW, HALO = G::HALO, HPIECES = G::HPIECES, NH = G::NH;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
       }
-    if (ep->relu)
+    if constexpr (RELU)
 #pragma unroll
       for (int i = 0; i < 2; ++i) epi_relu(acc[i]);
     if (ep->stat_sum) {
@@ -508,6 +508,8 @@ int launch7(const VuGemmFwd& p, const Plan7& r, hipStream_t st) {
     hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 4, false, 2>), gr, dim3(512), 0, st, q);
   else if (r.ks <= 1 && g_v7_xm == 4)
     hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 4, false, 4>), gr, dim3(512), 0, st, q);
+  else if (r.ks <= 1 && p.relu)
+    hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 3, false, 0, true>), gr, dim3(512), 0, st, q);
   else if (r.ks <= 1 && g_v7_nbw == 3)
     hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 3, false>), gr, dim3(512), 0, st, q);
   else if (r.ks <= 1)
