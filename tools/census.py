@@ -38,7 +38,8 @@ def _shape(name, args):
             M = g.N * g.H * g.W
             K_ = g.R * g.S * g.C
             b = M * g.C * 2 + M * a.ncol * 2 + a.ncol * K_ * 2
-            return f"fwd R{g.R} C{g.C} {g.H}x{g.W} N{a.ncol}", b, 2 * M * K_ * a.ncol
+            kid = _lib.query("vu_gemm_fwd_kernel", args[0], args[1])
+            return f"fwd R{g.R}x{g.S} s{g.sy} C{g.C} {g.H}x{g.W} N{a.ncol} om{a.out_mode} k{kid}", b, 2 * M * K_ * a.ncol
         if name == "vu_gemm_wgrad":
             w = args[0]._obj
             M = w.p.N * w.p.H * w.p.W
