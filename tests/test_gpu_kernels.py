@@ -36,10 +36,38 @@ def _act(t, mode):
     return t.to(DEV, _dt(mode)).contiguous(memory_format=CL)
 
 
-def _close(got, ref, mode, scale_floor=1e-3, what=""):
+U_STORE = {"f32": 2.0 ** -24, "bf16": 2.0 ** -8}
+C_SUM = 1e-5
+
+
+def _close(got, ref, mode, scale_floor=1e-3, what="", sabs=None, acc=None, u=None):
+    """GEMM kernels (``sabs`` given: sum_k |a_k||b_k| of every output element,
+    the same reference op on |operands|): PER-ELEMENT bound
+
+      |got - ref| <= u * max(|ref|, |got|)  [+ u * |acc|]  + C_SUM * sabs + 1e-7 * max |ref|
+
+    u = half an ulp of the storage dtype (2^-8 bf16, 2^-24 fp32; ``u``
+    overrides it for fp32 weight gradients), acc = the rounded new term of an
+    accumulating launch (rounded once more when added), C_SUM the fp32
+    summation-order noise of the two sides' accumulations.  Other kernels: a
+    max-relative tolerance."""
     got = got.detach().float().cpu()
     ref = ref.detach().float().cpu()
     diff = (got - ref).abs()
+    if sabs is not None:
+        uu = U_STORE[mode] if u is None else u
+        g64, r64 = got.double(), ref.double()
+        bound = uu * torch.maximum(r64.abs(), g64.abs()) + C_SUM * sabs.detach().double().cpu() \
+            + 1e-7 * float(r64.abs().max())
+        if acc is not None:
+            bound += uu * acc.detach().double().cpu().abs()
+        ratio = (g64 - r64).abs() / bound
+        i = int(ratio.flatten().argmax())
+        assert float(ratio.max()) <= 1.0, (
+            f"{what}: per-element bound exceeded at flat index {i} (got {got.flatten()[i].item():.6g}, "
+            f"ref {ref.flatten()[i].item():.6g}, bound {bound.flatten()[i].item():.3e}); "
+            f"{int((ratio > 1).sum())} elements off")
+        return
     err = diff.max().item()
     scale = max(ref.abs().max().item(), scale_floor)
     rtol = 2e-5 if mode == "f32" else 1.5e-2
@@ -83,7 +111,8 @@ def test_conv3x3_fwd_dgrad_wgrad(mode, case):
     wdev = w.to(DEV)
     out = K.empty_act(N, co, H, W, _dt(mode), DEV)
     st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(wdev, d), co, out, d, stats=True)
-    _close(out, ref, mode, what="fwd")
+    xa = torch.cat(xs, 1).abs()
+    _close(out, ref, mode, what="fwd", sabs=F.conv2d(xa, wq.abs(), padding=1))
     # statistics: combine partial (sum, M2) -> mean/var, compare with the stored values
     stored = out.float().cpu()
     n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
@@ -99,14 +128,16 @@ def test_conv3x3_fwd_dgrad_wgrad(mode, case):
     dref = torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1)
     dx = K.empty_act(N, cin, H, W, _dt(mode), DEV)
     K.gemm_fwd(K.gather3x3([_act(dy, mode)]), E.w3x3_dgrad(wdev, d), cin, dx, d)
-    _close(dx, dref, mode, what="dgrad")
+    _close(dx, dref, mode, what="dgrad",
+           sabs=torch.nn.grad.conv2d_input((N, cin, H, W), wq.abs(), dy.abs(), padding=1))
     # weight gradient, contiguous and channels_last parameter layouts
     wref = torch.nn.grad.conv2d_weight(torch.cat(xs, 1), (co, cin, 3, 3), dy, padding=1)
+    wabs = torch.nn.grad.conv2d_weight(xa, (co, cin, 3, 3), dy.abs(), padding=1)
     for fmt in (torch.contiguous_format, CL):
         gw = torch.zeros(co, cin, 3, 3, device=DEV).contiguous(memory_format=fmt)
         K.gemm_wgrad(K.gather1x1([_act(dy, mode)]), K.gather3x3(srcs), co, 9 * cin, gw,
                      E.conv_layout(gw), d, False)
-        _close(gw, wref, mode, what=f"wgrad {fmt}")
+        _close(gw, wref, mode, what=f"wgrad {fmt}", sabs=wabs, u=2.0 ** -23)
 
 
 V4_CASES = [
@@ -160,7 +191,8 @@ def _check_halo_conv(case, row_tiles, kernel=None):
         assert K.query("vu_gemm_fwd_kernel", *_row_tile_args(K, srcs, E.w3x3_fwd(w.to(DEV), d), co, out)) == kernel
     st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, out, d, stats=True)
     ref = F.conv2d(torch.cat(xs, 1), wq, padding=1)
-    _close(out, ref, "bf16", what="fwd")
+    xa = torch.cat(xs, 1).abs()
+    _close(out, ref, "bf16", what="fwd", sabs=F.conv2d(xa, wq.abs(), padding=1))
     stored = out.float().cpu()
     n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
                      dtype=torch.float64)
@@ -176,14 +208,20 @@ def _check_halo_conv(case, row_tiles, kernel=None):
     K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, wide, d, out_coff=64,
                bias=b.to(DEV), accumulate=True)
     exp = base.clone()
-    exp[:, 64:] += ref + b[None, :, None, None]
-    _close(wide, exp, "bf16", what="bias+accumulate")
+    new = ref + b[None, :, None, None]
+    exp[:, 64:] += new
+    sab = torch.zeros_like(exp)
+    sab[:, 64:] = F.conv2d(xa, wq.abs(), b.abs(), padding=1)
+    accn = torch.zeros_like(exp)
+    accn[:, 64:] = new
+    _close(wide, exp, "bf16", what="bias+accumulate", sabs=sab, acc=accn)
     # input gradient (flipped weights) when cin is a tile width
     if cin in (64, 128, 256, 512) and co % 32 == 0:
         dy = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
         dx = K.empty_act(N, cin, H, W, torch.bfloat16, DEV)
         K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), cin, dx, d)
-        _close(dx, torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1), "bf16", what="dgrad")
+        _close(dx, torch.nn.grad.conv2d_input((N, cin, H, W), wq, dy, padding=1), "bf16", what="dgrad",
+               sabs=torch.nn.grad.conv2d_input((N, cin, H, W), wq.abs(), dy.abs(), padding=1))
 
 
 @pytest.mark.parametrize("case", V4_CASES)
@@ -290,7 +328,8 @@ def test_conv3x3_image_kernel(case):
     assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out)) == 64
     st = K.gemm_fwd(K.gather3x3([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
     ref = F.conv2d(x[:, :3], w.to(torch.bfloat16).float(), b, padding=1)
-    _close(out, ref, "bf16", what="image conv")
+    _close(out, ref, "bf16", what="image conv",
+           sabs=F.conv2d(x[:, :3].abs(), w.to(torch.bfloat16).float().abs(), b.abs(), padding=1))
     stored = out.float().cpu()
     n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
                      dtype=torch.float64)
@@ -328,11 +367,12 @@ def test_gemm_stream_kernel(case):
     xs = _act(x, "bf16")
     wm = E.w1x1_fwd(w.to(DEV), d)
     ref = F.conv2d(x, w.to(torch.bfloat16).float(), b)
+    sab = F.conv2d(x.abs(), w.to(torch.bfloat16).float().abs(), b.abs())
     if not acc:
         out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
         assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out, K.gather1x1)) in (16, 32, 64)
         st = K.gemm_fwd(K.gather1x1([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
-        _close(out, ref, "bf16", what="stream fwd")
+        _close(out, ref, "bf16", what="stream fwd", sabs=sab)
         stored = out.float().cpu()
         n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)],
                          dtype=torch.float64)
@@ -348,7 +388,9 @@ def test_gemm_stream_kernel(case):
         K.gemm_fwd(K.gather1x1([xs]), wm, co, wide, d, out_coff=32, bias=b.to(DEV), accumulate=True)
         exp = base.clone()
         exp[:, 32:] += ref
-        _close(wide, exp, "bf16", what="stream accumulate")
+        sw, an = torch.zeros_like(exp), torch.zeros_like(exp)
+        sw[:, 32:], an[:, 32:] = sab, ref
+        _close(wide, exp, "bf16", what="stream accumulate", sabs=sw, acc=an)
 
 
 @pytest.mark.parametrize("cin,cout", [(128, 64), (64, 32)])
@@ -366,7 +408,8 @@ def test_gemm_stream_convT(cin, cout):
     K.gemm_fwd(K.gather1x1([_act(x, "bf16")]), E.wT_fwd(w.to(DEV), d), 4 * cout, out, d, bias=b.to(DEV),
                convT=(2 * H, 2 * W, 0, 0, cout))
     ref = F.conv_transpose2d(x, w.to(torch.bfloat16).float(), b, stride=2)
-    _close(out, ref, "bf16", what="stream convT")
+    _close(out, ref, "bf16", what="stream convT",
+           sabs=F.conv_transpose2d(x.abs(), w.to(torch.bfloat16).float().abs(), b.abs(), stride=2))
 
 
 TUNE_V5 = 10
@@ -411,7 +454,7 @@ def test_gemm_v5_fwd_stats_accumulate(case):
         out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
         assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wm, co, out, K.gather1x1)) == 64
         st = K.gemm_fwd(K.gather1x1([xs]), wm, co, out, d, bias=b.to(DEV), stats=True)
-        _close(out, F.conv2d(x, wq, b), "bf16", what="v5 fwd")
+        _close(out, F.conv2d(x, wq, b), "bf16", what="v5 fwd", sabs=F.conv2d(x.abs(), wq.abs(), b.abs()))
         _stats_check(st, out.float().cpu())
         # input gradient: K = co, N = cin, accumulated into channels [64, 64 + cin)
         du = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).float()
@@ -420,8 +463,11 @@ def test_gemm_v5_fwd_stats_accumulate(case):
         K.gemm_fwd(K.gather1x1([_act(du, "bf16")]), E.w1x1_dgrad(w.to(DEV), d), cin, wide, d, out_coff=64,
                    accumulate=True)
         exp = base.clone()
-        exp[:, 64:] += torch.nn.grad.conv2d_input((N, cin, H, W), wq, du)
-        _close(wide, exp, "bf16", what="v5 dgrad accumulate")
+        new = torch.nn.grad.conv2d_input((N, cin, H, W), wq, du)
+        exp[:, 64:] += new
+        sw, an = torch.zeros_like(exp), torch.zeros_like(exp)
+        sw[:, 64:], an[:, 64:] = torch.nn.grad.conv2d_input((N, cin, H, W), wq.abs(), du.abs()), new
+        _close(wide, exp, "bf16", what="v5 dgrad accumulate", sabs=sw, acc=an)
     finally:
         _tune((TUNE_V5, 1))
 
@@ -457,12 +503,14 @@ def test_conv3x3_c64_resident(case):
         out = K.empty_act(N, 64, H, W, torch.bfloat16, DEV)
         assert K.query("vu_gemm_fwd_row_tile", *_row_tile_args(K, [xs], wf, 64, out, K.gather3x3)) == 64
         st = K.gemm_fwd(K.gather3x3([xs]), wf, 64, out, d, bias=b.to(DEV), stats=True)
-        _close(out, F.conv2d(x, wq, b, padding=1), "bf16", what="v6 fwd")
+        _close(out, F.conv2d(x, wq, b, padding=1), "bf16", what="v6 fwd",
+               sabs=F.conv2d(x.abs(), wq.abs(), b.abs(), padding=1))
         _stats_check(st, out.float().cpu())
         dy = torch.randn(N, 64, H, W, generator=g).to(torch.bfloat16).float()
         dx = K.empty_act(N, 64, H, W, torch.bfloat16, DEV)
         K.gemm_fwd(K.gather3x3([_act(dy, "bf16")]), E.w3x3_dgrad(w.to(DEV), d), 64, dx, d, kind="dgrad")
-        _close(dx, torch.nn.grad.conv2d_input((N, 64, H, W), wq, dy, padding=1), "bf16", what="v6 dgrad")
+        _close(dx, torch.nn.grad.conv2d_input((N, 64, H, W), wq, dy, padding=1), "bf16", what="v6 dgrad",
+               sabs=torch.nn.grad.conv2d_input((N, 64, H, W), wq.abs(), dy.abs(), padding=1))
     finally:
         _tune((TUNE_V6, 1))
 
@@ -492,7 +540,8 @@ def test_conv_stem_7x7s2(N, H, W):
     a.a, a.b, a.ldb, a.ncol, a.out, a.out_stride, a.out_mode = gth, wf.data_ptr(), wf.shape[-1], 64, out.data_ptr(), K.pstride(out), 0
     assert K.query("vu_gemm_fwd_row_tile", C.byref(a), 1) == 64
     st = K.gemm_fwd(gth, wf, 64, out, d, bias=b.to(DEV), stats=True)
-    _close(out, F.conv2d(x, wq, b, stride=2, padding=3), "bf16", what="stem fwd")
+    _close(out, F.conv2d(x, wq, b, stride=2, padding=3), "bf16", what="stem fwd",
+           sabs=F.conv2d(x.abs(), wq.abs(), b.abs(), stride=2, padding=3))
     _stats_check(st, out.float().cpu())
 
 
@@ -516,12 +565,15 @@ def test_gemm_v5_convT(ci, co, h, cap):
                    convT=(2 * h, 2 * h, 0, 0, co))
         xr = x.clone().requires_grad_(True)
         ref = F.conv_transpose2d(xr, wq, b, stride=2)
-        _close(out, ref, "bf16", what="v5 convT fwd")
+        xa = x.abs().requires_grad_(True)
+        refa = F.conv_transpose2d(xa, wq.abs(), b.abs(), stride=2)
+        _close(out, ref, "bf16", what="v5 convT fwd", sabs=refa)
         du = torch.randn(N, co, 2 * h, 2 * h, generator=g).to(torch.bfloat16).float()
         ref.backward(du)
+        refa.backward(du.abs())
         dx = K.empty_act(N, ci, h, h, torch.bfloat16, DEV)
         K.gemm_fwd(K.gather_convT(_act(du, "bf16"), N, h, h), E.wT_dgrad(w.to(DEV), d), ci, dx, d)
-        _close(dx, xr.grad, "bf16", what="v5 convT dgrad")
+        _close(dx, xr.grad, "bf16", what="v5 convT dgrad", sabs=xa.grad)
     finally:
         _tune((TUNE_V5, 1))
 
@@ -559,16 +611,19 @@ def test_conv1x1_fwd_dgrad_wgrad(mode, case):
     d = _code(mode)
     u = K.empty_act(N, F_, H, W, _dt(mode), DEV)
     K.gemm_fwd(K.gather1x1([_act(x, mode)]), E.w1x1_fwd(w.to(DEV), d), F_, u, d, bias=b.to(DEV), stats=True)
-    _close(u, F.conv2d(x, wq, b), mode, what="fwd")
+    _close(u, F.conv2d(x, wq, b), mode, what="fwd", sabs=F.conv2d(x.abs(), wq.abs(), b.abs()))
     du = torch.randn(N, F_, H, W, generator=g).to(_dt(mode)).float()
     base = torch.randn(N, C_, H, W, generator=g).to(_dt(mode)).float()
     dx = _act(base, mode)
     K.gemm_fwd(K.gather1x1([_act(du, mode)]), E.w1x1_dgrad(w.to(DEV), d), C_, dx, d, accumulate=True)
-    _close(dx, base + torch.nn.grad.conv2d_input((N, C_, H, W), wq, du), mode, what="dgrad")
+    new = torch.nn.grad.conv2d_input((N, C_, H, W), wq, du)
+    _close(dx, base + new, mode, what="dgrad", acc=new,
+           sabs=torch.nn.grad.conv2d_input((N, C_, H, W), wq.abs(), du.abs()))
     gw = torch.zeros(F_, C_, 1, 1, device=DEV)
     K.gemm_wgrad(K.gather1x1([_act(du, mode)]), K.gather1x1([_act(x, mode)]), F_, C_, gw,
                  E.conv_layout(gw), d, False)
-    _close(gw, torch.nn.grad.conv2d_weight(x, (F_, C_, 1, 1), du), mode, what="wgrad")
+    _close(gw, torch.nn.grad.conv2d_weight(x, (F_, C_, 1, 1), du), mode, what="wgrad", u=2.0 ** -23,
+           sabs=torch.nn.grad.conv2d_weight(x.abs(), (F_, C_, 1, 1), du.abs()))
 
 
 @pytest.mark.parametrize("mode", ["f32", "bf16"])
@@ -589,24 +644,30 @@ def test_conv_transpose(mode, case):
     wr = wq.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)
     ref = F.pad(F.conv_transpose2d(xr, wr, br, stride=2), [px, dxp - px, py, dyp - py])
+    # the same ops on |operands|: sum_k |a_k||b_k| of every output / gradient element
+    xa = x.abs().requires_grad_(True)
+    wa = wq.abs().requires_grad_(True)
+    ba = b.abs().requires_grad_(True)
+    refa = F.pad(F.conv_transpose2d(xa, wa, ba, stride=2), [px, dxp - px, py, dyp - py])
     d = _code(mode)
     u = K.zeros_act(N, co, H, W, _dt(mode), DEV)
     K.gemm_fwd(K.gather1x1([_act(x, mode)]), E.wT_fwd(wt.to(DEV), d), 4 * co, u, d,
                bias=b.to(DEV), convT=(H, W, py, px, co))
-    _close(u, ref, mode, what="convT fwd")
+    _close(u, ref, mode, what="convT fwd", sabs=refa)
     du = torch.randn(N, co, H, W, generator=g).to(_dt(mode)).float()
     ref.backward(du)
+    refa.backward(du.abs())
     dua = _act(du, mode)
     dx = K.empty_act(N, ci, h, w, _dt(mode), DEV)
     K.gemm_fwd(K.gather_convT(dua, N, h, w, py, px), E.wT_dgrad(wt.to(DEV), d), ci, dx, d)
-    _close(dx, xr.grad, mode, what="convT dgrad")
+    _close(dx, xr.grad, mode, what="convT dgrad", sabs=xa.grad)
     gw = torch.zeros(ci, co, 2, 2, device=DEV)
     K.gemm_wgrad(K.gather1x1([_act(x, mode)]), K.gather_convT(dua, N, h, w, py, px), ci, 4 * co, gw,
                  E.convT_layout(gw), d, False)
-    _close(gw, wr.grad, mode, what="convT wgrad")
+    _close(gw, wr.grad, mode, what="convT wgrad", sabs=wa.grad, u=2.0 ** -23)
     gb = torch.zeros(co, device=DEV)
     K.chan_sum(dua, gb, False, d, window=(py, px, 2 * h, 2 * w))
-    _close(gb, br.grad, mode, what="convT bias grad")
+    _close(gb, br.grad, mode, what="convT bias grad", sabs=ba.grad, u=2.0 ** -23)
 
 
 @pytest.mark.parametrize("mode", ["f32", "bf16"])
@@ -875,4 +936,5 @@ def test_conv_stride2_input_grad_parity_classes(case, zi, acc):
         E.S2_ZERO_INSERT_DGRAD = old
     wq = conv.weight.detach().cpu().to(torch.bfloat16).float()
     ref = torch.nn.grad.conv2d_input((N, ci, H, H), wq, dy, stride=2, padding=k // 2)
-    _close(dx, ref + base if acc else ref, "bf16", what="stride-2 dgrad")
+    sab = torch.nn.grad.conv2d_input((N, ci, H, H), wq.abs(), dy.abs(), stride=2, padding=k // 2)
+    _close(dx, ref + base if acc else ref, "bf16", what="stride-2 dgrad", sabs=sab, acc=ref if acc else None)

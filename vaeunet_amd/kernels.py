@@ -109,6 +109,13 @@ class LaunchTimer:
 
 TIMER = None
 
+# Observation point for the production-size parity tests
+# (tests/gemm_audit.py): when set, every GEMM launch goes through
+# AUDIT.gemm_fwd / AUDIT.gemm_wgrad, which run the launch and then compare its
+# output element by element with the contraction its descriptor defines.  The
+# launch itself is the same call either way (same dispatch, same kernel).
+AUDIT = None
+
 
 def _timed(tag, flops, fn):
     if TIMER is None:
@@ -216,9 +223,11 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
             ws = torch.empty(nb // 4, dtype=torch.float32, device=out.device)
             a.workspace = ws.data_ptr()
     M = g.N * g.H * g.W
-    _timed(_gemm_tag(g, kind),
-           2 * M * ncol * g.R * g.S * g.C if flops is None else flops,
-           lambda: call("vu_gemm_fwd", C.byref(a), dtype, stream()))
+    launch = lambda: call("vu_gemm_fwd", C.byref(a), dtype, stream())  # noqa: E731
+    if AUDIT is not None:
+        AUDIT.gemm_fwd(a, dtype, g, wmat, out, bias, st, launch)
+    else:
+        _timed(_gemm_tag(g, kind), 2 * M * ncol * g.R * g.S * g.C if flops is None else flops, launch)
     if bnb is not None:
         return part
     return st
@@ -264,12 +273,21 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
     slab = torch.empty((splits, ni, nj), dtype=torch.float32, device=grad.device)
     w.splits, w.m_per_split = splits, mps
     w.out = slab.data_ptr()
+    s_i, s_tap, s_c = layout
+    cv = gq.C if cvalid is None else cvalid
+
+    def reduce():
+        call("vu_slab_reduce", ptr(slab), splits, ni, nj, gq.C, cv, s_i, s_tap, s_c, ptr(grad),
+             1 if accumulate else 0, stream())
+    if AUDIT is not None:
+        def launch():
+            call("vu_gemm_wgrad", C.byref(w), dtype, stream())
+            reduce()
+        AUDIT.gemm_wgrad(w, dtype, kind, gp, gq, ni, nj, grad, layout, accumulate, cv, launch)
+        return slab
     _timed(_gemm_tag(gq, "wgrad"), 2 * M * ni * nj,
            lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()))
-    s_i, s_tap, s_c = layout
-    call("vu_slab_reduce", ptr(slab), splits, ni, nj, gq.C, gq.C if cvalid is None else cvalid,
-         s_i, s_tap, s_c, ptr(grad),
-         1 if accumulate else 0, stream())
+    reduce()
     return slab
 
 
