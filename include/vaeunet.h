@@ -207,12 +207,18 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     CU (slabs in VuConvFp8.workspace + the split-K finish), 0 off */
 #define VU_TUNE_FP8_SPLIT 24
 /*   VU_TUNE_BN_MINBLK: fewest blocks of the BatchNorm streaming kernels on
- *     small tensors (default 256; 0 = ~16 pixel rows per thread only) */
-#define VU_TUNE_BN_MINBLK 23
+ *     small tensors (default 256; 0 = ~16 pixel rows per thread only).
+ *     (Was 23 until round 4, the same key as VU_TUNE_FP8_C64, which took it.) */
+#define VU_TUNE_BN_MINBLK 25
+/*   VU_TUNE_W3_FAST: 1 (default) the halo weight-gradient main loop with
+ *     immediate-offset fragment reads and incremental tile addressing, 0 the
+ *     round-3 loop, 2 the round-4 loop without s_setprio (A/B runs) */
+#define VU_TUNE_W3_FAST 26
 int vu_gemm_set_tuning(int key, int value);
-/* ABI check: out[0..5] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
- * VuPermJob, VuMtEntry as this library was compiled (bindings compare their
- * own struct sizes against it; tests/test_modules.py) */
+/* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
+ * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was
+ * compiled (bindings compare their own struct sizes against it;
+ * tests/test_modules.py) */
 void vu_abi_struct_sizes(int64_t* out);
 
 /* ---- fp8 (OCP e4m3fn) 3x3 conv forward: BASELINE.json configs[4] ------- */
@@ -568,6 +574,90 @@ int vu_reparam_fwd(const float* mu, const float* lv, const float* eps, int n,
                    float* z, void* stream);
 int vu_reparam_bwd(const float* lv, const float* eps, const float* dz, int n,
                    float* dmu, float* dlv, int accumulate, void* stream);
+
+/* ---- fused VAE bottleneck + latent injection (round 4) -------------------
+ * Replaces, for a latent VECTOR z, the heads / reparameterize / broadcast /
+ * z_initial / z_proj chain of unet_resnet.py:140-154,191-194,217-229 and
+ * :37-41,93-94 (DecoderBlock).  Downstream of z every map is a per-sample
+ * constant, so each 1x1 conv + BatchNorm2d + ReLU "consumer" is computed on
+ * the N sample vectors (train-mode statistics over N*HW pixels == over the N
+ * vectors, running_var unbiased with count N*HW) and its map is written once,
+ * activated.  latent.hip. */
+
+/* one block per sample: pooled[n][c] = mean_p f4[n,p,c]; mu / logvar[n][j] =
+ * b[j] + sum_c w[j][c] pooled[n][c] (the conv1x1 + AdaptiveAvgPool2d heads,
+ * pool and 1x1 conv commuted); z = mu + eps * exp(logvar / 2), or z = mu when
+ * eps == NULL.  C = 8 * 2^k <= 2048, fs % 8 == 0. */
+int vu_vae_heads_fwd(const void* f4, int64_t fs, int N, int HW, int C, const float* w_mu,
+                     const float* b_mu, const float* w_lv, const float* b_lv, int L, const float* eps,
+                     float* pooled, float* mu, float* logvar, float* z, int dtype, void* stream);
+
+/* One latent consumer (device table entry): map[n, p, c] = relu(BN(W z[n] +
+ * b))[c] for c < co, 0 for co <= c < cpad, at out + (n*HW + p)*out_stride.
+ * Forward saves y[n][c] = W z[n] + b and coef [4][co] = scale, shift, mean,
+ * invstd.  Backward: dmap (pixel stride dmap_stride, co channels) -> part
+ * [N][splits][co] partial pixel sums -> weight / bias / gamma / beta
+ * gradients (written, or added when grad_acc) and the consumer's share of
+ * dz.  The entry points take a HOST array of at most 8 entries and pass it
+ * by value in the kernel arguments (a captured graph replays it); block0,
+ * sblock0 and cgroups are filled in by the library. */
+typedef struct VuLatentJob {
+  const float* w;              /* [co][L] */
+  const float* bias;           /* [co] or NULL */
+  const float* gamma;
+  const float* beta;
+  float* running_mean;         /* NULL: not tracked */
+  float* running_var;
+  int64_t* num_batches_tracked;
+  float momentum, eps;
+  int32_t train, co, cpad, HW;
+  void* out;
+  int64_t out_stride;
+  float* y;                    /* [N][co] */
+  float* coef;                 /* [4][co] */
+  int64_t block0;
+  int32_t cgroups, grad_acc;
+  const void* dmap;            /* backward: d(map), co channels */
+  int64_t dmap_stride;
+  float* part;                 /* vu_latent_part_floats(N, co) */
+  int64_t sblock0;
+  float* dw;                   /* [co][L] or NULL */
+  float* dbias;
+  float* dgamma;
+  float* dbeta;
+} VuLatentJob;
+
+/* the heads' backward inputs / outputs for vu_latent_bwd */
+typedef struct VuLatentHeads {
+  const float* z;              /* [N][L] */
+  const float* eps;            /* NULL: z = mu */
+  const float* logvar;
+  const float* dmu_in;         /* incoming d/dmu, d/dlogvar (KL term) or NULL */
+  const float* dlv_in;
+  const float* pooled;         /* [N][C] */
+  const float* w_mu;
+  const float* w_lv;           /* [L][C] */
+  float* dw_mu;
+  float* db_mu;
+  float* dw_lv;
+  float* db_lv;                /* written, or added when grad_acc */
+  float* dpooled;              /* [N][C] (the caller broadcasts dpooled / HW into d f4) */
+  int32_t C, grad_acc;
+} VuLatentHeads;
+
+int64_t vu_latent_fwd_blocks(int N, int HW, int cpad);
+/* jobs: host array (<= 8); z [N][L] fp32 device (L <= 64, N <= 64) */
+int vu_latent_fwd(const VuLatentJob* jobs, int njobs, const float* z, int N, int L, int dtype, void* stream);
+int64_t vu_latent_part_floats(int N, int co);
+int vu_latent_bwd_sums(const VuLatentJob* jobs, int njobs, int N, int dtype, void* stream);
+int64_t vu_latent_bwd_workspace_bytes(int N, int L, int64_t sum_co);
+/* one block: every consumer's BN / ReLU / conv backward on the vectors, dz,
+ * reparameterize backward, both heads' backward -> dpooled */
+int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentHeads* heads, int N, int L,
+                  float* workspace, void* stream);
+/* 0 when a consumer of this geometry is served (co = 8 * 2^k <= 2048, cpad % 8,
+ * stride % 8), else hipErrorInvalidValue */
+int vu_latent_check_job(int co, int cpad, int64_t out_stride, int dtype);
 
 /* ---- inference sampling path (utils/vae_utils.py, visualize_vae.py) --- */
 /* out[e] = (sum_{k < groups} x[k*n + e]) / groups  (stack(preds).mean(0)) */

@@ -68,6 +68,25 @@ VU_DEV u32x4 tr_frag(const char* base, int off_lo, int off_hi) {
   return u32x4{l2[0], l2[1], h2[0], h2[1]};
 }
 
+// The same read from a per-lane LDS byte address held in a VGPR plus a
+// compile-time byte offset in the instruction's 16-bit offset field: the
+// tap / k-step shifts of a tile cost no address arithmetic (off folds to a
+// constant once the group loop is unrolled).
+VU_DEV u32x2 tr_read_o(uint32_t a, const int off) {
+  u32x2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(off));
+  return r;
+}
+VU_DEV u32x4 tr_frag_o(uint32_t lo, uint32_t hi, const int off) {
+  u32x2 l2 = tr_read_o(lo, off), h2 = tr_read_o(hi, off);
+  return u32x4{l2[0], l2[1], h2[0], h2[1]};
+}
+VU_DEV u32x4 tr_frag_o2(uint32_t a, const int off_lo, const int off_hi) {
+  u32x2 l2 = tr_read_o(a, off_lo), h2 = tr_read_o(a, off_hi);
+  return u32x4{l2[0], l2[1], h2[0], h2[1]};
+}
+VU_DEV uint32_t lds_addr(const char* p) { return (uint32_t)(uintptr_t)(const lds_void*)p; }
+
 // at most n LDS operations outstanding (n folds to a constant after unrolling)
 VU_DEV void lgkm_wait(int n) {
   switch (n) {
@@ -91,8 +110,18 @@ VU_DEV void lgkm_wait(int n) {
 }
 VU_DEV void tie(u32x4& v) { asm volatile("" : "+v"(v)); }
 
-template <int BI, int TJ, int TW>
+// FAST (round 4, the default): per tile, the fragment-read base addresses of
+// the tile's LDS stage are formed once (14 VGPRs) and every (k-step, tap)
+// read uses the instruction offset field; the tile walk advances its
+// (image, row, column) counters instead of dividing; interior tiles (halo
+// inside the image) take precomputed 32-bit per-lane halo offsets with no
+// bounds test.  The round-3 loop formed every read address with a VALU add
+// and recomputed the DMA addresses per tile: ~190 VALU + ~110 SALU per
+// 144-MFMA tile per wave (1.3 VALU per MFMA at BI = 128, 2.6 at BI = 64;
+// profiles/r3e_sq_timing_unet.txt).
+template <int BI, int TJ, int TW, int FASTM>
 __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
+  constexpr bool FAST = FASTM != 0, PRIO = FASTM != 2;   // FASTM 2: no s_setprio around the MFMA groups
   constexpr int TH = WT<TW>::TH, HWP = WT<TW>::HWP, HROWS = WT<TW>::HROWS;
   constexpr int NT = 512;
   constexpr int RBP = BI * 2, CPI = BI / 8;
@@ -152,6 +181,66 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     q_pk[k] = (hy < HROWS && hx < TW + 2) ? (hy | hx << 4 | swz_col<128>(hp, pc) << 10) : -1;
   }
 
+  // FAST: 32-bit offset of each halo slot's source element from the tile's
+  // first pixel (interior tiles), INT32_MIN for a slot that loads nothing;
+  // border tiles re-derive the slot geometry from the thread id
+  int q_rel[FAST ? NH : 1];
+  if constexpr (FAST) {
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int q = q_pk[k];
+      q_rel[k] = q >= 0 ? (int)((int64_t)(((q & 15) - 1) * W + ((q >> 4) & 63) - 1) * xst + (q >> 10)) : INT32_MIN;
+    }
+  }
+  // tile walk counters (FAST): image, tile row, tile column of the next stage
+  int w_img = 0, w_ty = 0, w_tx = 0;
+  if constexpr (FAST) {
+    w_img = t_beg / tiles_img;
+    const int tr = t_beg - w_img * tiles_img;
+    w_ty = tr / tiles_w;
+    w_tx = tr - w_ty * tiles_w;
+  }
+  const int tiles_h = H / TH;
+
+  auto stage_fast = [&](int buf) {
+    const int img = w_img, y0 = w_ty * TH, x0 = w_tx * TW;
+    if (++w_tx == tiles_w) {
+      w_tx = 0;
+      if (++w_ty == tiles_h) { w_ty = 0; ++w_img; }
+    }
+    char* Pb = smem + buf * STAGE;
+    char* Qb = Pb + PB;
+    const int64_t pix0 = ((int64_t)img * H + y0) * W + x0;
+    const bf16_t* dtile = dsrc + pix0 * dst_;
+#pragma unroll
+    for (int k = 0; k < LP; ++k) {
+      const void* s = p_off[k] >= 0 ? (const void*)(dtile + p_off[k]) : zp;
+      __builtin_amdgcn_global_load_lds(s, (lds_void*)(Pb + (k * NT + wid * 64) * 16), 16, 0, 0);
+    }
+    if (y0 > 0 && y0 + TH < H && x0 > 0 && x0 + TW < W) {
+      const bf16_t* xtile = xsrc + pix0 * xst;
+#pragma unroll
+      for (int k = 0; k < NH; ++k)
+        if (q_rel[k] != INT32_MIN)
+          __builtin_amdgcn_global_load_lds((const void*)(xtile + q_rel[k]), (lds_void*)(Qb + (k * NT + wid * 64) * 16),
+                                           16, 0, 0);
+    } else {
+      const bf16_t* ximg = xsrc + (int64_t)img * H * W * xst;
+#pragma unroll
+      for (int k = 0; k < NH; ++k) {
+        const int e = k * NT + tid, hp = e >> 3, pc = e & 7;
+        const int hy = hp / HWP, hx = hp - hy * HWP;
+        if (hy < HROWS && hx < TW + 2) {
+          const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+          const void* s = zp;
+          if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+            s = ximg + (int64_t)(y * W + x) * xst + swz_col<128>(hp, pc);
+          __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
+        }
+      }
+    }
+  };
+
   auto stage = [&](int t, int buf) {
     const int img = t / tiles_img, tr = t - img * tiles_img;
     const int y0 = (tr / tiles_w) * TH, x0 = (tr - (tr / tiles_w) * tiles_w) * TW;
@@ -183,7 +272,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
   // fragment read offsets (bytes; every k-step / tap shift is an immediate)
   const int g4 = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
   const int wco = wid / WCI, wci = wid - (wid / WCI) * WCI;   // co pair, ci group of this wave
-  int offA[TI][2];
+  int offA[TI][2];   // (FAST uses [a][0] only: [a][1] = [a][0] + 4 * RBP, rows m and m + 4 share the swizzle)
 #pragma unroll
   for (int a = 0; a < TI; ++a)
 #pragma unroll
@@ -210,14 +299,34 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       for (int t = 0; t < 9; ++t) acc[a][b][t] = f32x4{0, 0, 0, 0};
 
   const int nsteps = t_end > t_beg ? t_end - t_beg : 0;
-  if (nsteps > 0) stage(t_beg, 0);
+  if (nsteps > 0) {
+    if constexpr (FAST) stage_fast(0);
+    else stage(t_beg, 0);
+  }
   for (int st = 0; st < nsteps; ++st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (st + 1 < nsteps) stage(t_beg + st + 1, (st + 1) & 1);
+    if (st + 1 < nsteps) {
+      if constexpr (FAST) stage_fast((st + 1) & 1);
+      else stage(t_beg + st + 1, (st + 1) & 1);
+    }
     const char* Pb = smem + (st & 1) * STAGE;
     const char* Qb = Pb + PB;
+    // FAST: this stage's per-lane fragment base addresses (the +4-row half
+    // of an A fragment keeps the swizzle: an immediate 4 * RBP)
+    uint32_t bA[TI], bB[TJ][2][3];
+    if constexpr (FAST) {
+      const uint32_t pa = lds_addr(Pb), qa = lds_addr(Qb);
+#pragma unroll
+      for (int a = 0; a < TI; ++a) bA[a] = pa + offA[a][0];
+#pragma unroll
+      for (int b = 0; b < TJ; ++b)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int s = 0; s < 3; ++s) bB[b][h][s] = qa + offB[b][h][s];
+    }
     // software-pipelined fragment reads over the 36 (k-step, tap) MFMA groups
     // of a tile: group g's B fragments are read two groups ahead (and a
     // k-step's A fragments two groups before its first tap), so an MFMA group
@@ -227,11 +336,17 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
     auto load_b = [&](int g, u32x4* dst) {
       const int ks = g / 9, q = g - (g / 9) * 9, r = q / 3, s = q - (q / 3) * 3;
 #pragma unroll
-      for (int b = 0; b < TJ; ++b) dst[b] = tr_frag(Qb + (ks * (32 / TW) + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
+      for (int b = 0; b < TJ; ++b) {
+        if constexpr (FAST) dst[b] = tr_frag_o(bB[b][0][s], bB[b][1][s], (ks * (32 / TW) + r) * HWP * 128);
+        else dst[b] = tr_frag(Qb + (ks * (32 / TW) + r) * HWP * 128, offB[b][0][s], offB[b][1][s]);
+      }
     };
     auto load_a = [&](int ks, u32x4* dst) {
 #pragma unroll
-      for (int a = 0; a < TI; ++a) dst[a] = tr_frag(Pb + ks * 32 * RBP, offA[a][0], offA[a][1]);
+      for (int a = 0; a < TI; ++a) {
+        if constexpr (FAST) dst[a] = tr_frag_o2(bA[a], ks * 32 * RBP, ks * 32 * RBP + 4 * RBP);
+        else dst[a] = tr_frag(Pb + ks * 32 * RBP, offA[a][0], offA[a][1]);
+      }
     };
     load_a(0, aq[0]);
     load_b(0, bq[0]);
@@ -253,14 +368,14 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       for (int a = 0; a < TI; ++a) tie(aq[ks & 1][a]);
 #pragma unroll
       for (int b = 0; b < TJ; ++b) tie(bq[g % 3][b]);
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int a = 0; a < TI; ++a)
 #pragma unroll
         for (int b = 0; b < TJ; ++b)
           acc[a][b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               __builtin_bit_cast(bf16x8, aq[ks & 1][a]), __builtin_bit_cast(bf16x8, bq[g % 3][b]), acc[a][b][t], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
 
@@ -280,11 +395,20 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       }
 }
 
+// vu_gemm_set_tuning(VU_TUNE_W3_FAST, ...): 1 (default) the round-4 main loop,
+// 0 the round-3 loop, 2 the round-4 loop without s_setprio (A/B runs)
+int g_w3_fast = 1;
+
 template <int BI, int TW>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int64_t nblk = (int64_t)((p.ni + BI - 1) / BI) * (p.q.C / 64) * p.splits;
   if (nblk <= 0) return 0;
-  hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, TW>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  if (g_w3_fast == 1)
+    hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, TW, 1>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  else if (g_w3_fast == 2)
+    hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, TW, 2>), dim3((unsigned)nblk), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL((wgrad3x3_halo_kernel<BI, 1, TW, 0>), dim3((unsigned)nblk), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -326,6 +450,8 @@ int gemm_wgrad_v3_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
   if (!tw || g.H % (TP / tw)) return 0;
   if ((int64_t)g.N * g.H * g.W >= (int64_t)1 << 31) return 0;
   if ((int64_t)(TP / tw) * g.W * a.stride[0] >= (int64_t)1 << 31) return 0;   // 32-bit dy slot offsets
+  for (int t = 0; t < g.nsrc; ++t)                                               // 32-bit halo slot offsets
+    if ((int64_t)(TP / tw + 2) * (g.W + 2) * g.stride[t] >= (int64_t)1 << 31) return 0;
   *bi = pick_bi(p);
   *bj = 9 * 64;
   return 1;
@@ -341,6 +467,11 @@ int gemm_wgrad_v3_launch(const VuGemmWgrad& p, hipStream_t st) {
 int gemm_wgrad_v3_tune(int key, int value) {
   if (key == VU_TUNE_W3_SMALL) {
     g_w3_small = value != 0;
+    return 0;
+  }
+  if (key == VU_TUNE_W3_FAST) {
+    if (value < 0 || value > 2) return (int)hipErrorInvalidValue;
+    g_w3_fast = value;
     return 0;
   }
   return -1;
