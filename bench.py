@@ -65,14 +65,16 @@ def parse():
     ap.add_argument("--torch-optim", action="store_true",
                     help="torch.optim.AdamW + torch clip_grad_norm_ instead of the fused HIP ones")
     ap.add_argument("--engine-flag", action="append", default=[], metavar="NAME=0|1",
-                    help="set a vaeunet_amd.engine module switch (A/B runs), e.g. FUSE_BN_BWD_REDUCE=0")
+                    help="set a vaeunet_amd.engine module switch (A/B runs), e.g. FUSE_BN_BWD_REDUCE=0, or "
+                         "MODULE.NAME for another vaeunet_amd module, e.g. vae_engine.LATENT_VECTORS=0")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VAL",
                     help="vu_gemm_set_tuning(KEY, VAL) before the run (library A/B runs; include/vaeunet.h)")
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a side stream (engine.OVERLAP_WGRAD; measured slower, A/B only)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the step as one captured HIP graph (vaeunet_amd.graph); auto = on "
-                         "at world size 1 with the fused optimizer")
+                         "at world size 1 with the fused optimizer; at N > 1 only with 'on' (the captured "
+                         "RCCL all-reduces are untested across GPUs: experimental)")
     return ap.parse_args()
 
 
@@ -164,12 +166,12 @@ def cpu_baseline(args, dev):
     """The CPU oracle (clean-room restatement of the reference, oracle/cpu_ref.py;
     kind "port") timed on this host: the same synthetic batch
     (B x 3 x S x S, rank-0 seed), 1 warmup + K timed full train steps (fwd,
-    loss, bwd, clip, AdamW).  Legs: fp32 on every core of the affinity mask
-    (the headline: reference semantics, threads = len(sched_getaffinity)),
-    CPU autocast bf16 on the same threads (train.py's amp default on CPU),
-    and fp32 on the per-GPU share (OMP_NUM_THREADS) when that differs.
-    --model vae: UNetResNet with CombinedLoss + 1e-3 * KL (free bits 1e-3)
-    and a fixed latent draw.
+    loss, bwd, clip, AdamW).  Threads: len(sched_getaffinity) capped by the
+    cgroup CPU quota (_cpu_threads; the thread probe measured in the same run
+    is reported beside it).  Legs, both on those threads: fp32 (the headline:
+    reference semantics) and CPU autocast bf16 (train.py's amp default on
+    CPU; --cpu-no-bf16 skips it).  --model vae: UNetResNet with CombinedLoss +
+    1e-3 * KL (free bits 1e-3) and a fixed latent draw.
 
     The first fp32 warmup step's pre-update outputs are also the parity
     reference: the GPU model (fp32 parity mode, same weights, same batch) is
@@ -355,9 +357,14 @@ def main():
         _lib.call("vu_gemm_set_tuning", int(key), int(val))  # raises if the key / value is refused
     for kv in args.engine_flag:
         name, val = kv.split("=")
-        if not hasattr(E, name):
+        mod = E
+        if "." in name:   # e.g. vae_engine.LATENT_VECTORS
+            import importlib
+            modname, name = name.rsplit(".", 1)
+            mod = importlib.import_module("vaeunet_amd." + modname)
+        if not hasattr(mod, name):
             raise SystemExit(f"bench: no engine switch {name}")
-        setattr(E, name, bool(int(val)))
+        setattr(mod, name, bool(int(val)))
     from vaeunet_amd.loss import CombinedLoss
     from vaeunet_amd import parallel
 
@@ -406,10 +413,14 @@ def main():
         return loss
 
     graphed = None
-    # the step replays as one HIP graph with the fused optimizer; at N > 1 the
-    # bucketed RCCL all-reduces are captured with it (gloo rehearsals run eagerly)
+    # the step replays as one HIP graph with the fused optimizer at N = 1.  At
+    # N > 1 the default is the eager step (the bucketed RCCL all-reduces still
+    # overlap the backward): a captured multi-rank step has not been compared
+    # with the eager one on a multi-GPU box yet, so it is opt-in ("--graph on",
+    # experimental; gloo cannot be captured at all).  The UNet step is
+    # GPU-bound, so eager costs it nothing measurable.
     capturable = not args.torch_optim and (world == 1 or dist.get_backend() == "nccl")
-    use_graph = args.graph == "on" or (args.graph == "auto" and capturable)
+    use_graph = args.graph == "on" or (args.graph == "auto" and capturable and world == 1)
     if use_graph:
         if not capturable:
             raise SystemExit("--graph on needs the fused optimizer and (at N > 1) the nccl backend")
@@ -459,14 +470,17 @@ def main():
             eager_step()   # the same kernels, launched one by one so each can be bracketed
         summ = K.TIMER.summary()
         K.TIMER = None
-        fl = sum(v[0] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
-        tm = sum(v[1] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
-        n = sum(v[2] for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k)
+        fam = {k: v for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k}
+        fl = sum(v[0] for v in fam.values())
+        tm = sum(v[1] for v in fam.values())
+        n = sum(v[2] for v in fam.values())
+        knames = sorted(set().union(*(v[3] for v in fam.values()))) if fam else []
         achieved = fl / (tm * 1e-3) / 1e12 if tm > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": pmc_traffic(args.model),
                 "traffic_unit": f"HBM bytes per launch ({os.path.relpath(PMC_TRAFFIC[args.model], ROOT)})",
-                "kernel": "gemm_fwd_kernel+gemm_wgrad_kernel (3x3 conv fwd/dgrad/wgrad, inc.0 excluded)",
+                "kernel": ("3x3 conv fwd/dgrad/wgrad (inc.0 excluded; the weight gradients' vu_slab_reduce "
+                           "passes are not in the family): " + ", ".join(knames)),
                 "launches_per_step": n // 2,
                 "per_kind": {k: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1),
                                  "ms_per_step": round(v[1] / 2, 3)} for k, v in sorted(summ.items())}}
@@ -486,7 +500,8 @@ def main():
                                         "+clip+AdamW), random-init weights"),
                            "image": f"3x{args.size}x{args.size}", "batch_per_gpu": args.batch,
                            "global_batch": args.batch * world, "parallelism": f"dp{world}",
-                           "execution": "hipgraph-replay" if graphed is not None else "eager",
+                           "execution": ("hipgraph-replay" + (" (experimental at N>1)" if world > 1 else ""))
+                           if graphed is not None else "eager",
                            "wgrad_side_stream": bool(E.OVERLAP_WGRAD),
                            "bn_bwd_reduce_in_dgrad_epilogue": bool(E.FUSE_BN_BWD_REDUCE)},
                 "loss": round(float(loss.item()), 6),

@@ -634,6 +634,7 @@ typedef struct VuLatentHeads {
   const float* logvar;
   const float* dmu_in;         /* incoming d/dmu, d/dlogvar (KL term) or NULL */
   const float* dlv_in;
+  const float* dz_in;          /* incoming d/dz from outside the consumers, or NULL */
   const float* pooled;         /* [N][C] */
   const float* w_mu;
   const float* w_lv;           /* [L][C] */

@@ -222,8 +222,11 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
 # parameter gradient of the HIP fp32 path vs the fp64 oracle, judged against
 # the fp32 oracle's OWN error at the same size (the reference's CPU fp32
 # autograd is what a user of the reference gets):
-#   ||g_hip - g64|| / ||g64||  <=  GRAD_ERR_FACTOR * ||g32 - g64|| / ||g64|| + GRAD_ERR_FLOOR
-# Gradients that are mathematically zero (the bias of a conv feeding a
+#   ||g_hip - g64||  <=  GRAD_ERR_FACTOR * ||g32 - g64||  +  GRAD_ERR_FLOOR * max_k ||g64_k||
+# (the floor: an error below 1e-6 of the largest parameter gradient is fp32
+# summation noise -- a cancellation-dominated sum such as an attention psi
+# BatchNorm(1) bias gradient carries a relative error of several % in the
+# reference's own fp32 path).  Gradients that are mathematically zero (the bias of a conv feeding a
 # train-mode BatchNorm: BN(x + b) does not depend on b) are written as exact
 # zeros by the HIP path for the 1x1 / ConvT convs (engine.bias_grad), where
 # the reference's autograd leaves summation noise (the psi conv's bias, summed
@@ -231,7 +234,7 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
 # floor 1e-5 * max ||g||" instead, and the exact zeros are counted.
 # ---------------------------------------------------------------------------
 GRAD_ERR_FACTOR = 4.0
-GRAD_ERR_FLOOR = 2e-6
+GRAD_ERR_FLOOR = 1e-6
 BW_B = 2
 
 
@@ -245,15 +248,16 @@ def _grad_adjudicate(tag, names, g_hip, g32, g64):
             assert float(g_hip[k].norm()) <= 1e-5 * gmax, (k, float(g_hip[k].norm()))
             assert float(g32[k].norm()) <= 1e-5 * gmax, (k, float(g32[k].norm()))
             continue
-        e_h = float((g_hip[k] - g64[k]).norm()) / r
-        e_32 = float((g32[k] - g64[k]).norm()) / r
-        worst.append((e_h - GRAD_ERR_FACTOR * e_32, k, e_h, e_32))
+        d_h = float((g_hip[k] - g64[k]).norm())
+        d_32 = float((g32[k] - g64[k]).norm())
+        # > 1: outside the bound
+        worst.append((d_h / (GRAD_ERR_FACTOR * d_32 + GRAD_ERR_FLOOR * gmax), k, d_h / r, d_32 / r))
     worst.sort(reverse=True)
     print(f"{tag}: {len(worst)} gradients adjudicated vs fp64, {len(zero)} mathematically zero "
           f"({sum(zero)} written as exact zeros); worst "
-          f"(excess, name, HIP rel err, fp32-oracle rel err): "
+          f"(err / bound, name, HIP rel err, fp32-oracle rel err): "
           f"{[(f'{a:.2e}', b, f'{c:.2e}', f'{d:.2e}') for a, b, c, d in worst[:4]]}")
-    assert worst[0][0] <= GRAD_ERR_FLOOR, worst[:4]
+    assert worst[0][0] <= 1.0, worst[:4]
     return worst
 
 
@@ -290,7 +294,7 @@ def test_unet_config2_fp32_backward_512_vs_fp64():
     model = model.to(DEV).to(memory_format=CL).train()
     loss = CombinedLoss()(model(x.to(DEV)), t.to(DEV))
     loss.backward()
-    assert abs(float(loss) - loss64) < 1e-5
+    assert abs(float(loss.detach()) - loss64) < 1e-5
     params = dict(model.named_parameters())
     gh = {k: params[k].grad.detach().double().cpu() for k in names}
     _grad_adjudicate("config2 fp32 backward B=2 512^2", names, gh, g32, g64)
@@ -321,7 +325,7 @@ def test_unetresnet_config3_fp32_backward_512_vs_fp64():
     lg, mu, lv = model(x.to(DEV))
     loss = CombinedLoss()(lg, t.to(DEV)) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
     loss.backward()
-    assert abs(float(loss) - loss64) < 1e-5
+    assert abs(float(loss.detach()) - loss64) < 1e-5
     params = dict(model.named_parameters())
     gh = {k: (params[k].grad.detach().double().cpu() if params[k].grad is not None
               else torch.zeros_like(params[k], dtype=torch.float64, device="cpu")) for k in names}

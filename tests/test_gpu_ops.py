@@ -128,3 +128,160 @@ def test_opcheck():
     for op, args in cases:
         torch.library.opcheck(op, args, test_utils=("test_schema", "test_faketensor",
                                                     "test_autograd_registration"))
+
+
+# ---- round 4: the remaining SURVEY §8(b) units ----------------------------------------
+def test_convT2x2_ops_vs_torch():
+    """ConvTranspose2d(k=2, s=2) + bias (unet_parts.py:76) and its autograd."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 16, 6, 5, generator=g)
+    w = torch.randn(16, 8, 2, 2, generator=g) * 0.2
+    b = torch.randn(8, generator=g)
+    xd, wd, bd = _act(x).requires_grad_(True), w.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    y = v.convT2x2_fwd(xd, wd, bd)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(_act(dy))
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = F.conv_transpose2d(xr, wr, br, stride=2)
+    yr.backward(dy)
+    _close(y, yr, 1e-5, "convT fwd")
+    for got, ref, n in ((xd.grad, xr.grad, "dx"), (wd.grad, wr.grad, "dw"), (bd.grad, br.grad, "db")):
+        _close(got, ref, 1e-4, n)
+
+
+def test_upsample_bilinear_ac_ops_vs_torch():
+    """F.interpolate(bilinear, align_corners=True) to a non-2x size
+    (unet_resnet.py:79,238) and its transposed-gather backward."""
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(2, 8, 5, 7, generator=g)
+    xd = _act(x).requires_grad_(True)
+    y = v.upsample_bilinear_ac_fwd(xd, 9, 13)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(_act(dy))
+    xr = x.clone().requires_grad_(True)
+    yr = F.interpolate(xr, size=(9, 13), mode="bilinear", align_corners=True)
+    yr.backward(dy)
+    _close(y, yr, 1e-5, "upsample fwd")
+    _close(xd.grad, xr.grad, 1e-5, "upsample bwd")
+
+
+def _gate_params(g, F_g, F_l, F_int):
+    return [torch.randn(F_int, F_g, 1, 1, generator=g) * 0.3, torch.randn(F_int, generator=g) * 0.1,
+            torch.rand(F_int, generator=g) + 0.5, torch.randn(F_int, generator=g) * 0.1,
+            torch.randn(F_int, F_l, 1, 1, generator=g) * 0.3, torch.randn(F_int, generator=g) * 0.1,
+            torch.rand(F_int, generator=g) + 0.5, torch.randn(F_int, generator=g) * 0.1,
+            torch.randn(1, F_int, 1, 1, generator=g) * 0.3, torch.randn(1, generator=g) * 0.1,
+            torch.rand(1, generator=g) + 0.5, torch.randn(1, generator=g) * 0.1]
+
+
+def _gate_ref(gt, xt, p, running, momentum, eps):
+    wg, bg, gg, btg, wx, bx, gx, btx, wp, bp, gp, btp = p
+    g1 = F.batch_norm(F.conv2d(gt, wg, bg), running[0], running[1], gg, btg, True, momentum, eps)
+    x1 = F.batch_norm(F.conv2d(xt, wx, bx), running[2], running[3], gx, btx, True, momentum, eps)
+    psi = torch.sigmoid(F.batch_norm(F.conv2d(torch.relu(g1 + x1), wp, bp), running[4], running[5], gp, btp, True,
+                                     momentum, eps))
+    return xt * psi, psi
+
+
+def test_attn_gate_ops_vs_torch():
+    """AttentionGate (unet_parts.py:7-30), train-mode BatchNorms: output, psi
+    map, running statistics and every input / parameter gradient."""
+    g = torch.Generator().manual_seed(13)
+    F_g, F_l, F_int = 16, 24, 8
+    gt = torch.randn(2, F_g, 12, 10, generator=g)
+    xt = torch.randn(2, F_l, 12, 10, generator=g)
+    params = _gate_params(g, F_g, F_l, F_int)
+    running = [torch.zeros(F_int), torch.ones(F_int), torch.zeros(F_int), torch.ones(F_int), torch.zeros(1),
+               torch.ones(1)]
+    gd, xd = _act(gt).requires_grad_(True), _act(xt).requires_grad_(True)
+    pd = [p.to(DEV).requires_grad_(True) for p in params]
+    out, psi, rnew = v.attn_gate_fwd(gd, xd, pd, [r.to(DEV) for r in running], 0.1, 1e-5)
+    dout = torch.randn(out.shape, generator=g)
+    out.backward(_act(dout))
+    gr, xr = gt.clone().requires_grad_(True), xt.clone().requires_grad_(True)
+    pr = [p.clone().requires_grad_(True) for p in params]
+    rr = [r.clone() for r in running]
+    outr, psir = _gate_ref(gr, xr, pr, rr, 0.1, 1e-5)
+    outr.backward(dout)
+    _close(out, outr, 1e-4, "gate out")
+    _close(psi, psir, 1e-4, "psi map")
+    for a, b_, i in zip(rnew, rr, range(6)):
+        _close(a, b_, 1e-4, f"running {i}")
+    _close(gd.grad, gr.grad, 5e-4, "dg")
+    _close(xd.grad, xr.grad, 5e-4, "dx")
+    for i, (a, b_) in enumerate(zip(pd, pr)):
+        if i in (1, 5):   # conv biases feeding a train-mode BN: exactly zero here, rounding noise in torch
+            assert float(a.grad.abs().max()) == 0.0 and float(b_.grad.abs().max()) < 1e-5
+            continue
+        _close(a.grad, b_.grad, 1e-3, f"param {i}")
+
+
+def test_vae_bottleneck_ops_vs_torch():
+    """mu / logvar heads (1x1 conv + AdaptiveAvgPool2d, unet_resnet.py:140-147)
+    + reparameterize (:191-194) in one launch, and the backward."""
+    g = torch.Generator().manual_seed(14)
+    N, C4, L = 3, 64, 8
+    f4 = torch.randn(N, C4, 4, 6, generator=g)
+    wm, bm = torch.randn(L, C4, 1, 1, generator=g) * 0.1, torch.randn(L, generator=g) * 0.1
+    wl, bl = torch.randn(L, C4, 1, 1, generator=g) * 0.1, torch.randn(L, generator=g) * 0.1
+    eps = torch.randn(N, L, generator=g)
+    rz, rm, rl = (torch.randn(N, L, generator=g) for _ in range(3))
+    fd = _act(f4).requires_grad_(True)
+    td = [t.to(DEV).requires_grad_(True) for t in (wm, bm, wl, bl)]
+    mu, lv, z, _ = v.vae_bottleneck_fwd(fd, *td, eps.to(DEV))
+    ((z * rz.to(DEV)).sum() + (mu * rm.to(DEV)).sum() + (lv * rl.to(DEV)).sum()).backward()
+    fr = f4.clone().requires_grad_(True)
+    tr = [t.clone().requires_grad_(True) for t in (wm, bm, wl, bl)]
+    mur = F.adaptive_avg_pool2d(F.conv2d(fr, tr[0], tr[1]), 1).flatten(1)
+    lvr = F.adaptive_avg_pool2d(F.conv2d(fr, tr[2], tr[3]), 1).flatten(1)
+    zr = mur + eps * torch.exp(0.5 * lvr)
+    ((zr * rz).sum() + (mur * rm).sum() + (lvr * rl).sum()).backward()
+    for got, ref, n in ((mu, mur, "mu"), (lv, lvr, "logvar"), (z, zr, "z"), (fd.grad, fr.grad, "df4")):
+        _close(got, ref, 1e-5, n)
+    for a, b_, n in zip(td, tr, ("dw_mu", "db_mu", "dw_lv", "db_lv")):
+        _close(a.grad, b_.grad, 1e-5, n)
+
+
+def test_bn_finalize_op():
+    g = torch.Generator().manual_seed(15)
+    tiles, rows_t, C_ = 37, 64, 16
+    y = torch.randn(tiles * rows_t, C_, generator=g, dtype=torch.float64) * 2 + 1
+    ys = y.view(tiles, rows_t, C_)
+    psum = ys.sum(1).float()
+    pm2 = ((ys - ys.mean(1, keepdim=True)) ** 2).sum(1).float()
+    gamma, beta = torch.rand(C_, generator=g) + 0.5, torch.randn(C_, generator=g)
+    coef, rm, rv = v.bn_finalize(psum.to(DEV), pm2.to(DEV), rows_t, tiles * rows_t, gamma.to(DEV), beta.to(DEV),
+                                 torch.zeros(C_, device=DEV), torch.ones(C_, device=DEV), 0.1, 1e-5)
+    mean, var = y.mean(0), y.var(0, unbiased=False)
+    invstd = 1 / torch.sqrt(var + 1e-5)
+    torch.testing.assert_close(coef[2].cpu().double(), mean, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(coef[3].cpu().double(), invstd, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(coef[0].cpu().double(), gamma.double() * invstd, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv.cpu().double(), 0.9 + 0.1 * y.var(0, unbiased=True), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rm.cpu().double(), 0.1 * mean, rtol=1e-5, atol=1e-6)
+
+
+def test_opcheck_round4_ops():
+    g = torch.Generator().manual_seed(16)
+    x = _act(torch.randn(2, 8, 6, 6, generator=g)).requires_grad_(True)
+    w = (torch.randn(8, 8, 2, 2, generator=g) * 0.1).to(DEV).requires_grad_(True)
+    gt = _act(torch.randn(2, 16, 6, 6, generator=g)).requires_grad_(True)
+    xt = _act(torch.randn(2, 24, 6, 6, generator=g)).requires_grad_(True)
+    params = [p.to(DEV).requires_grad_(True) for p in _gate_params(g, 16, 24, 8)]
+    running = [torch.zeros(8, device=DEV), torch.ones(8, device=DEV), torch.zeros(8, device=DEV),
+               torch.ones(8, device=DEV), torch.zeros(1, device=DEV), torch.ones(1, device=DEV)]
+    f4 = _act(torch.randn(2, 64, 2, 2, generator=g)).requires_grad_(True)
+    wm = (torch.randn(8, 64, 1, 1, generator=g) * 0.1).to(DEV).requires_grad_(True)
+    bm = torch.zeros(8, device=DEV, requires_grad=True)
+    psum, pm2 = torch.randn(5, 8, device=DEV), torch.rand(5, 8, device=DEV)
+    cases = [
+        (v.convT2x2_fwd.default, (x, w, None)),
+        (v.upsample_bilinear_ac_fwd.default, (x, 11, 7)),
+        (v.attn_gate_fwd.default, (gt, xt, params, running, 0.1, 1e-5)),
+        (v.vae_bottleneck_fwd.default, (f4, wm, bm, wm, bm, torch.randn(2, 8, device=DEV))),
+        (v.bn_finalize.default, (psum, pm2, 16, 80, torch.ones(8, device=DEV), torch.zeros(8, device=DEV),
+                                 torch.zeros(8, device=DEV), torch.ones(8, device=DEV), 0.1, 1e-5)),
+    ]
+    for op, args in cases:
+        torch.library.opcheck(op, args, test_utils=("test_schema", "test_faketensor",
+                                                    "test_autograd_registration"))

@@ -220,3 +220,78 @@ def test_dp_graph_capture_rccl_world1():
         assert abs(a - b) <= 1e-6 * max(1.0, abs(a)), (le, lg)
     for i, (a, b) in enumerate(zip(pg, pe)):
         assert _close(a, b), i
+
+
+def _unused_worker(rank, world, port, backend, out_q):
+    """UNetResNet(latent_injection='none') under the DP reducer: z_initial gets
+    no gradient (use_bottleneck False) -- eager DP steps and the captured DP
+    step both leave it untouched (.grad None, no AdamW state, no decay)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        from vaeunet_amd import UNetResNet, parallel
+        from vaeunet_amd.graph import GraphedTrainStep
+        from vaeunet_amd.init import seeded_init_
+        from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
+        from vaeunet_amd.optim import FusedAdamW, clip_grad_norm_
+        g = torch.Generator().manual_seed(5)
+        x = torch.rand(2, 3, 64, 64, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+        t = (torch.rand(2, 1, 64, 64, generator=g) > 0.5).float().cuda()
+        res = {}
+        for mode in ("eager", "graph"):
+            model = seeded_init_(UNetResNet(3, 1, pretrained=False, latent_injection="none"), 0)
+            model = model.cuda().to(memory_format=torch.channels_last).train()
+            z0 = {n: p.detach().clone() for n, p in model.named_parameters() if n.startswith("z_initial")}
+            red = parallel.attach(model, bucket_bytes=2 * 1024 * 1024)
+            opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=1e-2)
+
+            def fb():
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    lg, mu, lv = model(x)
+                    loss = CombinedLoss()(lg, t) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+                loss.backward()
+                return loss
+            if mode == "eager":
+                for _ in range(3):
+                    red.prepare()
+                    fb()
+                    red.finish()
+                    clip_grad_norm_([p for p in model.parameters() if p.grad is not None], 1.0)
+                    opt.step()
+                    red.zero_grad()
+            else:
+                gs = GraphedTrainStep(fb, opt, max_norm=1.0, warmup=1, reducer=red)
+                for _ in range(2):
+                    gs.step()
+            torch.cuda.synchronize()
+            ok = []
+            for n, p in model.named_parameters():
+                if n.startswith("z_initial"):
+                    ok.append((n, p.grad is None, bool(torch.equal(p.detach(), z0[n])), len(opt.state.get(p, {}))))
+            moved = sum(1 for n, p in model.named_parameters() if not n.startswith("z_initial") and p.grad is not None)
+            res[mode] = (ok, moved)
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_unused_parameter_left_untouched():
+    """with the reducer bound, an unused parameter must not pick up a
+    zero gradient view, AdamW state or weight decay (torch semantics)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join(
+        [os.path.dirname(here), here] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_unused_worker, args=(0, 1, _free_port(), "nccl", q))
+    p.start()
+    _, res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for mode in ("eager", "graph"):
+        ok, moved = res[mode]
+        assert ok and moved > 0, (mode, ok, moved)
+        for name, grad_none, same, nstate in ok:
+            assert same and nstate == 0, (mode, name, grad_none, same, nstate)

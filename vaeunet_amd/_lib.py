@@ -68,6 +68,21 @@ class VuMtEntry(C.Structure):
                 ("numel", _l), ("chunk0", _l), ("step_size", _f), ("bc2_sqrt", _f)]
 
 
+class VuLatentJob(C.Structure):
+    _fields_ = [("w", _p), ("bias", _p), ("gamma", _p), ("beta", _p), ("running_mean", _p),
+                ("running_var", _p), ("num_batches_tracked", _p), ("momentum", _f), ("eps", _f),
+                ("train", C.c_int32), ("co", C.c_int32), ("cpad", C.c_int32), ("HW", C.c_int32),
+                ("out", _p), ("out_stride", _l), ("y", _p), ("coef", _p), ("block0", _l),
+                ("cgroups", C.c_int32), ("grad_acc", C.c_int32), ("dmap", _p), ("dmap_stride", _l),
+                ("part", _p), ("sblock0", _l), ("dw", _p), ("dbias", _p), ("dgamma", _p), ("dbeta", _p)]
+
+
+class VuLatentHeads(C.Structure):
+    _fields_ = [("z", _p), ("eps", _p), ("logvar", _p), ("dmu_in", _p), ("dlv_in", _p), ("dz_in", _p), ("pooled", _p),
+                ("w_mu", _p), ("w_lv", _p), ("dw_mu", _p), ("db_mu", _p), ("dw_lv", _p), ("db_lv", _p),
+                ("dpooled", _p), ("C", C.c_int32), ("grad_acc", C.c_int32)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "vu_gemm_fwd": (_i, [C.POINTER(VuGemmFwd), _i, _p]),
@@ -150,6 +165,14 @@ _SIGS = {
     "vu_linear_small_bwd": (_i, [_p, _i, _i, _p, _i, _p, _p, _i, _p, _p, _i, _p]),
     "vu_reparam_fwd": (_i, [_p, _p, _p, _i, _p, _p]),
     "vu_reparam_bwd": (_i, [_p, _p, _p, _i, _p, _p, _i, _p]),
+    "vu_vae_heads_fwd": (_i, [_p, _l, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _i, _p]),
+    "vu_latent_fwd_blocks": (_l, [_i, _i, _i]),
+    "vu_latent_fwd": (_i, [_p, _i, _p, _i, _i, _i, _p]),
+    "vu_latent_part_floats": (_l, [_i, _i]),
+    "vu_latent_bwd_sums": (_i, [_p, _i, _i, _i, _p]),
+    "vu_latent_bwd_workspace_bytes": (_l, [_i, _i, _l]),
+    "vu_latent_bwd": (_i, [_p, _i, C.POINTER(VuLatentHeads), _i, _i, _p, _p]),
+    "vu_latent_check_job": (_i, [_i, _i, _l, _i]),
     "vu_mean_groups": (_i, [_p, _i, _l, _p, _p]),
     "vu_sigmoid": (_i, [_p, _l, _p, _p]),
     "vu_patch_blend": (_i, [_p, _l, _i, _i, _i, _p, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p]),

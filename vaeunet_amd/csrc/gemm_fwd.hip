@@ -453,4 +453,6 @@ extern "C" void vu_abi_struct_sizes(int64_t* out) {
   out[3] = sizeof(VuConvFp8);
   out[4] = sizeof(VuPermJob);
   out[5] = sizeof(VuMtEntry);
+  out[6] = sizeof(VuLatentJob);
+  out[7] = sizeof(VuLatentHeads);
 }

@@ -92,13 +92,19 @@ def _decode(model, M, feats, z, skip_always=False):
     output [B', n_classes, h, w] (fp32 NHWC, decoder resolution)."""
     N = z.shape[0]
     H4, W4 = feats[-1].shape[2], feats[-1].shape[3]
-    if model.use_bottleneck:
+    zps = [None] * len(model.decoder_blocks)
+    if V.latent_vectors_ok(M, model, N):
+        # z_initial and every z_proj on the [N, L] vectors, maps written once
+        cons, zps = V.latent_consumers(M, model, feats, N, skip_always)
+        V.latent_fwd(M, z.float().contiguous(), cons)
+        h = cons[0].out if model.use_bottleneck else feats[-1]
+    elif model.use_bottleneck:
         h, _ = V.cbr1x1_fwd(M, model.z_initial, V.latent_map(M, z, N, H4, W4))
     else:
         h = feats[-1]
     for i, blk in enumerate(model.decoder_blocks):
         use = i < len(feats) - 1 and (skip_always or model.use_skip)
-        h, _ = V.decoder_fwd(M, blk, h, feats[-(i + 2)] if use else None, z)
+        h, _ = V.decoder_fwd(M, blk, h, feats[-(i + 2)] if use else None, z, zp_vec=zps[i])
     out, _ = E.outconv_fwd(M, model.final_conv, h)
     return out
 

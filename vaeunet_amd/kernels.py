@@ -96,14 +96,17 @@ class LaunchTimer:
         self.recs = []
 
     def summary(self):
+        """tag -> [flops, ms, launches, {kernel names}]"""
         torch.cuda.synchronize()
         out = {}
-        for tag, flops, s, e in self.recs:
+        for tag, flops, s, e, kname in self.recs:
             ms = s.elapsed_time(e)
-            d = out.setdefault(tag, [0, 0.0, 0])
+            d = out.setdefault(tag, [0, 0.0, 0, set()])
             d[0] += flops
             d[1] += ms
             d[2] += 1
+            if kname:
+                d[3].add(kname)
         return out
 
 
@@ -117,7 +120,15 @@ TIMER = None
 AUDIT = None
 
 
-def _timed(tag, flops, fn):
+# kernel ids of vu_gemm_fwd_kernel / vu_gemm_wgrad_tile -> the __global__
+# functions the launch runs (the roofline line names what it timed)
+FWD_KERNELS = {1: "gemm_fwd_kernel", 2: "gemm_fwd_v2_kernel", 3: "conv3x3_halo_kernel", 4: "conv3x3_pp_kernel",
+               5: "gemm_fwd_v5_kernel", 6: "conv3x3_c64_kernel", 7: "conv3x3_sg_kernel", 8: "gemm_stream_kernel",
+               9: "conv3x3_image_kernel", 10: "conv_stem_kernel", 12: "gemm_fwd_v2_kernel(small-grid)"}
+WGRAD_KERNELS = {1: "gemm_wgrad_kernel", 2: "gemm_wgrad_v2_kernel", 3: "wgrad3x3_halo_kernel"}
+
+
+def _timed(tag, flops, fn, kname=None):
     if TIMER is None:
         return fn()
     s = torch.cuda.Event(enable_timing=True)
@@ -125,7 +136,7 @@ def _timed(tag, flops, fn):
     s.record()
     r = fn()
     e.record()
-    TIMER.recs.append((tag, flops, s, e))
+    TIMER.recs.append((tag, flops, s, e, kname() if callable(kname) else kname))
     return r
 
 
@@ -227,7 +238,10 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     if AUDIT is not None:
         AUDIT.gemm_fwd(a, dtype, g, wmat, out, bias, st, launch)
     else:
-        _timed(_gemm_tag(g, kind), 2 * M * ncol * g.R * g.S * g.C if flops is None else flops, launch)
+        def kname():
+            k = FWD_KERNELS.get(query("vu_gemm_fwd_kernel", C.byref(a), dtype), "?")
+            return k + "+splitk_finish_kernel" if ws is not None else k
+        _timed(_gemm_tag(g, kind), 2 * M * ncol * g.R * g.S * g.C if flops is None else flops, launch, kname)
     if bnb is not None:
         return part
     return st
@@ -286,7 +300,7 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
         AUDIT.gemm_wgrad(w, dtype, kind, gp, gq, ni, nj, grad, layout, accumulate, cv, launch)
         return slab
     _timed(_gemm_tag(gq, "wgrad"), 2 * M * ni * nj,
-           lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()))
+           lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()), WGRAD_KERNELS.get(kind, "?"))
     reduce()
     return slab
 

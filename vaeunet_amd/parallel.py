@@ -145,10 +145,20 @@ class GradBucketReducer:
 
     def finish(self):
         """Launch any bucket the engine did not report, then fence on all of
-        them (a no-op after a ``no_sync`` micro-batch)."""
+        them (a no-op after a ``no_sync`` micro-batch).
+
+        A parameter the engine never reported during a synchronised backward
+        received no gradient (UNetResNet's z_initial when use_bottleneck is
+        False): its ``.grad`` is reset to None afterwards -- torch semantics,
+        so the optimizer skips it (no AdamW state, no weight decay) as it
+        would without the reducer.  Only when the engine reported at all (a
+        model without the grad_ready hook keeps every bound gradient)."""
         if not self._sync:
             return
+        unseen = []
         if self._pending is not None:
+            if self._seen:
+                unseen = [p for p in self.params if id(p) not in self._seen]
             for bi, left in enumerate(self._pending):
                 if left > 0:
                     self._pending[bi] = 0
@@ -159,6 +169,8 @@ class GradBucketReducer:
                 flat.div_(self.world)
         self._handles = []
         self._pending = None
+        for p in unseen:
+            p.grad = None
 
 
 def attach(model, **kw):

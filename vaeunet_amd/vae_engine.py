@@ -13,8 +13,11 @@
 * DecoderBlock (31-101): bilinear(align_corners) to the skip size, attention
   gate, z_proj, three-source channel concat fed straight into conv1's K loop.
 """
+import ctypes as C
+
 import torch
 
+from . import _lib
 from . import engine as E
 from . import kernels as K
 from ._lib import F32
@@ -302,7 +305,10 @@ def sample_sum(M, x, scale=1.0, out=None, accumulate=False):
 # ---------------------------------------------------------------------------
 # DecoderBlock (unet_resnet.py:31-101)
 # ---------------------------------------------------------------------------
-def decoder_fwd(M, blk, x, skip, z):
+def decoder_fwd(M, blk, x, skip, z, zp_vec=None):
+    """zp_vec: the block's z_proj map already written by the latent vector
+    path (latent_fwd; cpad channels incl. the zero padding) -- its backward
+    is then deferred to latent_bwd (decoder_bwd returns the map's gradient)."""
     N = x.shape[0]
     if skip is not None:
         H, W = skip.shape[2], skip.shape[3]
@@ -320,7 +326,14 @@ def decoder_fwd(M, blk, x, skip, z):
         srcs.append(sk)
     szp = None
     cpad = None
-    if blk.use_latent:
+    if blk.use_latent and zp_vec is not None:
+        L = blk.z_proj[0].out_channels
+        lead = sum(t.shape[1] for t in srcs)
+        if zp_vec.shape[1] != L:
+            cpad = lead + zp_vec.shape[1]
+        srcs.append(zp_vec)
+        szp = "vec"
+    elif blk.use_latent:
         if z.dim() == 2:
             # interpolate([B, L, 1, 1] -> (H, W), align_corners) is a broadcast
             zb = latent_map(M, z, N, H, W)
@@ -367,7 +380,10 @@ def decoder_bwd(M, blk, saved, dout, z=None):
         else:
             dskip = dsk
         off += cs
-    if blk.use_latent:
+    if blk.use_latent and szp == "vec":
+        # the z_proj backward runs on the sample vectors (latent_bwd)
+        dz = ("vec", dsrc[:, off:off + blk.z_proj[0].out_channels])
+    elif blk.use_latent:
         dzp = dsrc[:, off:off + blk.z_proj[0].out_channels]
         dzb = cbr1x1_bwd(M, blk.z_proj, szp, dzp)
         if z is not None and z.dim() == 4:
@@ -379,6 +395,178 @@ def decoder_bwd(M, blk, saved, dout, z=None):
     H, W = xu.shape[2], xu.shape[3]
     K.upsample_bwd(dsrc[:, :cx], dx, H, W, 0, 0, False, M.d)
     return dx, dskip, dz
+
+
+# ---------------------------------------------------------------------------
+# latent vector path (round 4; csrc/latent.hip): the bottleneck heads,
+# reparameterize and every consumer of z (z_initial, the DecoderBlocks'
+# z_proj) on the [N, L] sample vectors -- downstream of z every map is a
+# per-sample constant (interpolate of z[..., None, None] is a broadcast), so a
+# 1x1 conv + train-mode BatchNorm + ReLU of it is the same arithmetic on the N
+# vectors, with the batch statistics over N * HW pixels equal to those of the
+# vectors.  4 launches per step instead of ~50 (sample sums, two heads,
+# reparameterize, 5 broadcasts, 5 1x1 GEMMs, their BatchNorm passes, and the
+# same again backwards).
+# ---------------------------------------------------------------------------
+LATENT_VECTORS = True  # A/B switch: False = the round-3 map path
+
+
+def _consumer_ok(M, seq):
+    conv, bn = seq[0], seq[1]
+    co = conv.out_channels
+    return (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.groups == 1
+            and (bn.training or bn.running_mean is not None) and bn.momentum is not None
+            and co % 8 == 0 and (co // 8) & (co // 8 - 1) == 0 and co <= 2048)
+
+
+def latent_vectors_ok(M, model, N):
+    """The vector path serves this model / batch (otherwise the map path)."""
+    if not LATENT_VECTORS or N > 64 or model.latent_dim > 64:
+        return False
+    c4 = model.mu_head[0].in_channels
+    if c4 % 8 or (c4 // 8) & (c4 // 8 - 1) or c4 > 2048:
+        return False
+    seqs = ([model.z_initial] if model.use_bottleneck else []) + \
+        [b.z_proj for b in model.decoder_blocks if b.use_latent]
+    return all(_consumer_ok(M, s) for s in seqs)
+
+
+def heads_fwd(M, model, f4, eps):
+    """pooled [N, C], mu, logvar, z [N, L] (fp32) in one launch."""
+    N, C4, H4, W4 = f4.shape
+    L = model.latent_dim
+    dev = f4.device
+    pooled = torch.empty((N, C4), dtype=torch.float32, device=dev)
+    mu = torch.empty((N, L), dtype=torch.float32, device=dev)
+    logvar = torch.empty_like(mu)
+    z = torch.empty_like(mu)
+    hm, hl = model.mu_head[0], model.logvar_head[0]
+    K.call("vu_vae_heads_fwd", K.ptr(f4), K.pstride(f4), N, H4 * W4, C4, K.ptr(hm.weight), K.ptr(hm.bias),
+           K.ptr(hl.weight), K.ptr(hl.bias), L, K.ptr(eps), K.ptr(pooled), K.ptr(mu), K.ptr(logvar), K.ptr(z),
+           K.dcode(f4.dtype), K.stream())
+    return pooled, mu, logvar, z
+
+
+class LatentConsumer:
+    """One 1x1 conv + BatchNorm + ReLU applied to the broadcast latent: its
+    output map (``out``, cpad >= co channels, zeros past co) and the saved
+    vectors y [N, co] (pre-BN) and coef [4, co] (scale, shift, mean, invstd)."""
+
+    def __init__(self, seq, out):
+        self.conv, self.bn = seq[0], seq[1]
+        self.out = out
+        N, _, H, W = out.shape
+        co = self.conv.out_channels
+        self.HW = H * W
+        self.y = torch.empty((N, co), dtype=torch.float32, device=out.device)
+        self.coef = torch.empty((4, co), dtype=torch.float32, device=out.device)
+        self.dmap = None
+
+    def job(self):
+        conv, bn = self.conv, self.bn
+        j = _lib.VuLatentJob()
+        track = bn.running_mean is not None
+        j.w, j.bias = conv.weight.data_ptr(), (conv.bias.data_ptr() if conv.bias is not None else None)
+        j.gamma, j.beta = bn.weight.data_ptr(), bn.bias.data_ptr()
+        j.running_mean = bn.running_mean.data_ptr() if track else None
+        j.running_var = bn.running_var.data_ptr() if track else None
+        j.num_batches_tracked = bn.num_batches_tracked.data_ptr() if track and bn.training else None
+        j.momentum, j.eps = float(bn.momentum), float(bn.eps)
+        j.train = 1 if bn.training else 0
+        j.co, j.cpad, j.HW = conv.out_channels, self.out.shape[1], self.HW
+        j.out, j.out_stride = self.out.data_ptr(), K.pstride(self.out)
+        j.y, j.coef = self.y.data_ptr(), self.coef.data_ptr()
+        return j
+
+
+def _jobs(cons):
+    arr = (_lib.VuLatentJob * len(cons))()
+    for i, c in enumerate(cons):
+        arr[i] = c.job()
+    return arr
+
+
+def latent_consumers(M, model, feats, N, skip_always=False):
+    """The consumers of z for a batch of N over encoder features ``feats``:
+    z_initial (if the bottleneck is used) and the z_proj of every latent
+    DecoderBlock, each with its output map allocated at the size that block
+    sees (the skip's, or twice its input's) -- the z_proj maps channel-padded
+    to 64 when the concat before them is 64-aligned (decoder_fwd's layout).
+    Returns (consumers, per-block z_proj map or None)."""
+    f4 = feats[-1]
+    H4, W4 = f4.shape[2], f4.shape[3]
+    cons, zps = [], [None] * len(model.decoder_blocks)
+    if model.use_bottleneck:
+        cons.append(LatentConsumer(model.z_initial, M.act(N, model.z_initial[0].out_channels, H4, W4)))
+    size = (H4, W4)
+    for i, blk in enumerate(model.decoder_blocks):
+        use = i < len(feats) - 1 and (skip_always or model.use_skip)
+        skip = feats[-(i + 2)] if use else None
+        size = (skip.shape[2], skip.shape[3]) if skip is not None else (2 * size[0], 2 * size[1])
+        if blk.use_latent:
+            Lb = blk.z_proj[0].out_channels
+            lead = blk.conv1[0].in_channels - Lb
+            Lp = -(-Lb // 64) * 64
+            cpad = Lp if (lead % 64 == 0 and Lp != Lb) else Lb
+            cons.append(LatentConsumer(blk.z_proj, M.act(N, cpad, size[0], size[1])))
+            zps[i] = cons[-1].out
+    return cons, zps
+
+
+def latent_fwd(M, z, cons):
+    """Every consumer's map from z [N, L] in one launch."""
+    if not cons:
+        return
+    for c in cons:
+        K.call("vu_latent_check_job", c.conv.out_channels, c.out.shape[1], K.pstride(c.out), M.d)
+    K.call("vu_latent_fwd", _jobs(cons), len(cons), K.ptr(z), z.shape[0], z.shape[1], M.d, K.stream())
+
+
+def latent_bwd(M, model, cons, z, eps, logvar, pooled, dmu, dlogvar):
+    """Backward of the consumers (their map gradients in ``c.dmap``), of
+    reparameterize and of both heads -> dpooled [N, C4] (fp32)."""
+    N, L = z.shape
+    dev = z.device
+    arr = _jobs(cons)
+    keep = []
+    for i, c in enumerate(cons):
+        part = torch.empty(K.query("vu_latent_part_floats", N, c.conv.out_channels), dtype=torch.float32,
+                           device=dev)
+        keep.append(part)
+        arr[i].dmap, arr[i].dmap_stride, arr[i].part = c.dmap.data_ptr(), K.pstride(c.dmap), part.data_ptr()
+        gw, accw = E.grad_sink(c.conv.weight)
+        gb, accb = E.grad_sink(c.conv.bias) if c.conv.bias is not None else (None, accw)
+        gg, gbe, accn = E.bn_grad_sinks(c.bn)
+        accs = {a for g, a in ((gw, accw), (gb, accb), (gg, accn)) if g is not None}
+        if len(accs) > 1:
+            raise RuntimeError("latent consumer: inconsistent gradient state")
+        arr[i].grad_acc = 1 if accs == {True} else 0
+        arr[i].dw, arr[i].dbias = K.ptr(gw), K.ptr(gb)
+        arr[i].dgamma, arr[i].dbeta = K.ptr(gg), K.ptr(gbe)
+    if cons:
+        K.call("vu_latent_bwd_sums", arr, len(cons), N, K.dcode(cons[0].dmap.dtype), K.stream())
+    hm, hl = model.mu_head[0], model.logvar_head[0]
+    h = _lib.VuLatentHeads()
+    dpooled = torch.empty_like(pooled)
+    dmu_c = dmu.float().contiguous() if dmu is not None else None
+    dlv_c = dlogvar.float().contiguous() if dlogvar is not None else None
+    h.z, h.eps, h.logvar = z.data_ptr(), K.ptr(eps), logvar.data_ptr()
+    h.dmu_in, h.dlv_in = K.ptr(dmu_c), K.ptr(dlv_c)
+    h.pooled, h.w_mu, h.w_lv = pooled.data_ptr(), hm.weight.data_ptr(), hl.weight.data_ptr()
+    sinks = [E.grad_sink(p) for p in (hm.weight, hm.bias, hl.weight, hl.bias)]
+    accs = {a for g, a in sinks if g is not None}
+    if len(accs) > 1:
+        raise RuntimeError("VAE heads: inconsistent gradient state")
+    h.dw_mu, h.db_mu, h.dw_lv, h.db_lv = (K.ptr(g) for g, _ in sinks)
+    h.dpooled, h.C, h.grad_acc = dpooled.data_ptr(), pooled.shape[1], 1 if accs == {True} else 0
+    sum_co = sum(c.conv.out_channels for c in cons)
+    ws = K.workspace_f32(K.query("vu_latent_bwd_workspace_bytes", N, L, sum_co), dev)
+    K.call("vu_latent_bwd", arr, len(cons), C.byref(h), N, L, K.ptr(ws), K.stream())
+    ps = [hm.weight, hm.bias, hl.weight, hl.bias]
+    for c in cons:
+        ps += [c.conv.weight, c.conv.bias, c.bn.weight, c.bn.bias]
+    M.notify(ps)
+    return dpooled
 
 
 # ---------------------------------------------------------------------------
@@ -406,38 +594,48 @@ def vae_tail_fwd(M, model, feats, Hin, Win, eps):
     N = f4.shape[0]
     dev = f4.device
     H4, W4 = f4.shape[2], f4.shape[3]
-    pooled = sample_sum(M, f4, 1.0 / (H4 * W4))
     L = model.latent_dim
-    mu = torch.empty((N, L), dtype=torch.float32, device=dev)
-    logvar = torch.empty_like(mu)
-    for head, out in ((model.mu_head[0], mu), (model.logvar_head[0], logvar)):
-        K.call("vu_linear_small_fwd", K.ptr(pooled), N, f4.shape[1], K.ptr(head.weight),
-               K.ptr(head.bias), L, K.ptr(out), K.stream())
     sampling = model.latent_injection not in ("none", "inject_no_bottleneck")
     if not sampling:
         eps = None
-    z = torch.empty_like(mu)
-    K.call("vu_reparam_fwd", K.ptr(mu), K.ptr(logvar), K.ptr(eps), N * L, K.ptr(z), K.stream())
+    vec = latent_vectors_ok(M, model, N)
+    cons, zps = [], [None] * len(model.decoder_blocks)
+    if vec:
+        pooled, mu, logvar, z = heads_fwd(M, model, f4, eps)
+        cons, zps = latent_consumers(M, model, feats, N)
+        latent_fwd(M, z, cons)
+    else:
+        pooled = sample_sum(M, f4, 1.0 / (H4 * W4))
+        mu = torch.empty((N, L), dtype=torch.float32, device=dev)
+        logvar = torch.empty_like(mu)
+        for head, out in ((model.mu_head[0], mu), (model.logvar_head[0], logvar)):
+            K.call("vu_linear_small_fwd", K.ptr(pooled), N, f4.shape[1], K.ptr(head.weight),
+                   K.ptr(head.bias), L, K.ptr(out), K.stream())
+        z = torch.empty_like(mu)
+        K.call("vu_reparam_fwd", K.ptr(mu), K.ptr(logvar), K.ptr(eps), N * L, K.ptr(z), K.stream())
     szi = None
     if model.use_bottleneck:
-        h, szi = cbr1x1_fwd(M, model.z_initial, latent_map(M, z, N, H4, W4))
+        if vec:
+            h = cons[0].out
+        else:
+            h, szi = cbr1x1_fwd(M, model.z_initial, latent_map(M, z, N, H4, W4))
     else:
         h = f4
     sdec = []
     for i, blk in enumerate(model.decoder_blocks):
         skip = feats[-(i + 2)] if (i < len(feats) - 1 and model.use_skip) else None
-        h, s = decoder_fwd(M, blk, h, skip, z)
+        h, s = decoder_fwd(M, blk, h, skip, z, zp_vec=zps[i])
         sdec.append(s)
     small, sfc = E.outconv_fwd(M, model.final_conv, h)
     out = torch.empty((N, small.shape[1], Hin, Win), dtype=torch.float32, device=dev,
                       memory_format=torch.channels_last)
     K.upsample_fwd(small, out, Hin, Win, 0, 0, F32)
-    return out, mu, logvar, (feats, pooled, eps, logvar, szi, sdec, sfc, small)
+    return out, mu, logvar, (feats, pooled, eps, logvar, szi, sdec, sfc, small, (cons, z) if vec else None)
 
 
 def vae_tail_bwd(M, model, state, dout, dmu, dlogvar):
     """-> gradients of the five encoder features (None where none flows)."""
-    feats, pooled, eps, logvar, szi, sdec, sfc, small = state
+    feats, pooled, eps, logvar, szi, sdec, sfc, small, lat = state
     N = small.shape[0]
     dsmall = torch.empty_like(small)
     if dout is not None:
@@ -447,8 +645,36 @@ def vae_tail_bwd(M, model, state, dout, dmu, dlogvar):
         dsmall.zero_()
     dh = E.outconv_bwd(M, model.final_conv, sfc, dsmall)
     L = model.latent_dim
-    dz = torch.zeros((N, L), dtype=torch.float32, device=small.device)
     dfeats = [None] * len(feats)
+    f4 = feats[-1]
+    C4, HW4 = f4.shape[1], f4.shape[2] * f4.shape[3]
+    if lat is not None:
+        cons, z = lat
+        byblk = {}
+        k = 1 if model.use_bottleneck else 0
+        for i, blk in enumerate(model.decoder_blocks):
+            if blk.use_latent:
+                byblk[i] = cons[k]
+                k += 1
+        for i in range(len(model.decoder_blocks) - 1, -1, -1):
+            dh, dskip, dzi = decoder_bwd(M, model.decoder_blocks[i], sdec[i], dh)
+            if dskip is not None:
+                dfeats[len(feats) - 2 - i] = dskip
+            if dzi is not None:
+                byblk[i].dmap = dzi[1]
+        df4 = None
+        if model.use_bottleneck:
+            cons[0].dmap = dh
+        else:
+            df4 = dh
+        dpooled = latent_bwd(M, model, cons, z, eps, logvar, pooled, dmu, dlogvar)
+        if df4 is None:
+            df4 = M.act(N, C4, f4.shape[2], f4.shape[3])
+        K.call("vu_sample_broadcast", K.ptr(dpooled), N, HW4, C4, 1.0 / HW4, K.ptr(df4),
+               K.pstride(df4), 0 if df4 is not dh else 1, M.d, K.stream())
+        dfeats[-1] = df4
+        return dfeats
+    dz = torch.zeros((N, L), dtype=torch.float32, device=small.device)
     for i in range(len(model.decoder_blocks) - 1, -1, -1):
         dh, dskip, dzi = decoder_bwd(M, model.decoder_blocks[i], sdec[i], dh)
         if dskip is not None:
@@ -466,8 +692,6 @@ def vae_tail_bwd(M, model, state, dout, dmu, dlogvar):
     dlv_t = dlogvar.float().contiguous().clone() if dlogvar is not None else torch.zeros_like(dz)
     K.call("vu_reparam_bwd", K.ptr(logvar), K.ptr(eps), K.ptr(dz), N * L, K.ptr(dmu_t),
            K.ptr(dlv_t), 1, K.stream())
-    f4 = feats[-1]
-    C4, HW4 = f4.shape[1], f4.shape[2] * f4.shape[3]
     dpooled = torch.empty((N, C4), dtype=torch.float32, device=f4.device)
     first = True
     for head, dh_ in ((model.mu_head[0], dmu_t), (model.logvar_head[0], dlv_t)):
