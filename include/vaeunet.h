@@ -123,7 +123,7 @@ int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype);
 /* the kernel the dispatcher picks for this problem (tests): 1 generic, 2 v2
  * LDS-DMA tiles, 3 v3 halo, 4 v4 ping-pong, 5 v5 persistent short-K, 6 v6
  * resident weights, 7 v7 small-grid, 8 1x1 stream, 9 image conv, 10 7x7 stem,
- * 12 v2 small-grid mode */
+ * 12 v2 small-grid mode, 13 v2 tail (small grids no other rule admits) */
 int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype);
 int vu_gemm_wgrad(const VuGemmWgrad* args, int dtype, void* stream);
 /* output tile (BI x BJ) the dispatcher picks for this problem (split-K sizing) */
@@ -214,6 +214,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     immediate-offset fragment reads and incremental tile addressing, 0 the
  *     round-3 loop, 2 the round-4 loop without s_setprio (A/B runs) */
 #define VU_TUNE_W3_FAST 26
+/*   VU_TUNE_PP_FULL: 1 = the ping-pong 3x3 kernel runs one read segment and
+ *     one 32-MFMA segment per step (2 barriers) instead of two halves (A/B) */
+#define VU_TUNE_PP_FULL 27
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was
@@ -231,6 +234,19 @@ int vu_amax(const void* x, int64_t xs, int64_t P, int C, float* amax,
 int vu_quant_fp8(const void* x, int64_t xs, int64_t P, int C,
                  const float* amax, uint8_t* y, int64_t ys, float* dq,
                  int dtype, void* stream);
+/* BatchNorm apply (+ReLU) fused with e4m3 quantisation, delayed scaling
+ * (fp8 DoubleConv: BN1's output is conv2's fp8 input, and only that):
+ *   z = relu?(x * scale[c] + shift[c])   (scale == NULL: z = relu?(x))
+ *   y = e4m3(clamp(z * s, +-448)), s = 448 / amax_ring[slot] (1 if 0),
+ *   *dq = 1/s; max|z| is max-accumulated into amax_ring[(slot+1)%3] (the
+ *   next step's scale) and amax_ring[(slot+2)%3] is cleared.  calibrate != 0:
+ *   only max-accumulate max|z| into amax_ring[slot] (first step), y unused.
+ * C = 8 * 2^k <= 2048, strides multiples of 8.  Replaces the bf16 apply +
+ * vu_amax + vu_quant_fp8 sequence (unet_parts.py:41-43 BN -> ReLU -> conv). */
+int vu_bn_apply_fp8(const void* x, int64_t xs, uint8_t* y, int64_t ys,
+                    int64_t P, int C, const float* scale, const float* shift,
+                    int relu, float* amax_ring, int slot, int calibrate,
+                    float* dq, int dtype, void* stream);
 /* per-row version for weights: fp32 [rows][cols] -> e4m3 [rows][ldy] (zero
  * padded), dq[r] = 1/s_r with s_r = 448 / max_k |x[r][k]| */
 int vu_quant_rows_fp8(const float* x, int rows, int64_t cols, uint8_t* y,

@@ -228,3 +228,79 @@ def test_conv3x3_fp8_split_matches_unsplit():
     for st, ref in ((sa, a), (sb, b)):
         mean = st.psum.double().sum(0).cpu() / st.rows
         torch.testing.assert_close(mean.float(), ref.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+
+
+def _q8_ref(x, sc, sh, relu, am_prev):
+    """CPU restatement of vu_bn_apply_fp8: z = x*sc + sh (two fp32 roundings),
+    relu, q = e4m3(clamp(z * 448/am_prev, +-448))."""
+    xf = x.float().cpu()
+    z = xf if sc is None else xf * sc.cpu()[None, :, None, None] + sh.cpu()[None, :, None, None]
+    if relu:
+        z = z.clamp_min(0.0)
+    s = torch.tensor(448.0) / torch.tensor(am_prev) if am_prev > 0 else torch.tensor(1.0)
+    return z, (z * s).clamp(-448, 448).to(torch.float8_e4m3fn), s
+
+
+@pytest.mark.parametrize("C_,dtype,slot", [(64, torch.bfloat16, 0), (128, torch.bfloat16, 2),
+                                            (512, torch.float32, 1), (8, torch.bfloat16, 1)])
+def test_bn_apply_fp8_bit_exact(C_, dtype, slot):
+    """Fused BN apply + ReLU + e4m3 quantise with the delayed scale: bytes equal
+    the unfused restatement; the next slot receives max |z| exactly, the one
+    after is cleared, dq = 1/s; values above the stale amax saturate."""
+    from vaeunet_amd import fp8
+    g = torch.Generator().manual_seed(C_)
+    x = torch.randn(2, C_, 9, 23, generator=g) * 2
+    sc = torch.randn(C_, generator=g)
+    sh = torch.randn(C_, generator=g) * 0.3
+    xd = _act(x, dtype)
+    ds = fp8.DelayedScale(DEV)
+    ds.t = slot
+    for relu, am_prev in ((True, 1.7), (False, 40.0)):      # 1.7: far below max|z| -> saturation
+        ring = torch.tensor([5.0, 5.0, 5.0])
+        ring[slot] = am_prev
+        ds.ring.copy_(ring)
+        q, dq = fp8.bn_apply_quant(xd, (sc.to(DEV), sh.to(DEV)), relu, ds)
+        z, qr, s = _q8_ref(xd, sc, sh, relu, am_prev)
+        assert torch.equal(_bytes(q), _bytes(qr))
+        assert dq.item() == (1.0 / s).item()
+        r = ds.ring.cpu()
+        assert r[slot].item() == am_prev
+        assert r[(slot + 1) % 3].item() == max(5.0, z.abs().max().item())   # max-accumulated
+        assert r[(slot + 2) % 3].item() == 0.0
+    # calibration: max|z| into the read slot only, nothing stored
+    ds.ring.zero_()
+    fp8.calibrate(xd, None, False, ds)
+    assert ds.ring.cpu()[slot].item() == xd.float().abs().max().item()
+    assert ds.ring.cpu().count_nonzero().item() == 1
+
+
+def test_bn_apply_fp8_rejects_unserved_channels():
+    from vaeunet_amd import _lib, fp8
+    xd = _act(torch.randn(1, 24, 4, 4))                       # 24 / 8 = 3: not a power of two
+    with pytest.raises(Exception):
+        fp8.bn_apply_quant(xd, None, True, fp8.DelayedScale(DEV))
+    assert _lib is not None
+
+
+@pytest.mark.parametrize("up", [False, True])
+def test_double_conv_fp8_delayed_scaling(up):
+    """Delayed-scaling fp8 DoubleConv over three steps of the same batch
+    (train-mode BN: same batch statistics, so the recorded amax is the one
+    the just-in-time path computes): close to the just-in-time fp8 path and
+    to the bf16 path every step; the rings carry amax(x) and max BN1 output."""
+    from vaeunet_amd import DoubleConv, fp8
+    torch.manual_seed(4)
+    cins = [64, 64] if up else [64]
+    mod = DoubleConv(sum(cins), 128).to(DEV)
+    xs = [_act(torch.randn(2, c, 32, 48).relu()) for c in cins]
+    yj = fp8.double_conv_forward(mod, xs, delayed=False).float()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = mod(torch.cat(xs, 1)).float()
+    for step in range(3):
+        yd = fp8.double_conv_forward(mod, xs).float()
+        assert ((yd - yj).abs().max() / yj.abs().max()).item() < 0.03, step
+        assert ((yd - yb).abs().max() / yb.abs().max()).item() < 0.15, step
+        ds_in, ds_mid = mod._vu_fp8_scales
+        assert ds_in.t == step + 1
+        assert ds_in.ring[ds_in.slot].item() == max(float(t.float().abs().max()) for t in xs)
+        assert ds_mid.ring[ds_mid.slot].item() > 0

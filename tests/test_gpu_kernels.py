@@ -235,6 +235,37 @@ def test_conv3x3_pingpong_kernel(case):
         _tune(*TUNE_DEFAULTS)
 
 
+TUNE_PP_FULL = 27
+
+
+@pytest.mark.parametrize("case", [c for c in V4_CASES if c[4] % 128 == 0])
+def test_conv3x3_pingpong_full_phase(case):
+    """the one-phase-per-step schedule (VU_TUNE_PP_FULL): the same MFMAs into
+    the same accumulators in the same order as the two-phase schedule, so the
+    output is bit-identical; plus the full parity check on it."""
+    K, E = _k()
+    N, cins, H, W, co = case[:5]
+    g = torch.Generator().manual_seed(9)
+    srcs = [_act(torch.randn(N, c, H, W, generator=g), "bf16") for c in cins]
+    w = torch.randn(co, sum(cins), 3, 3, generator=g) / (3 * sum(cins) ** 0.5)
+    d = _code("bf16")
+    outs = []
+    _tune((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 0))
+    try:
+        for full in (0, 1):
+            _tune((TUNE_PP_FULL, full))
+            out = K.empty_act(N, co, H, W, torch.bfloat16, DEV)
+            st = K.gemm_fwd(K.gather3x3(srcs), E.w3x3_fwd(w.to(DEV), d), co, out, d, stats=True)
+            torch.cuda.synchronize()
+            outs.append((out, st))
+        assert torch.equal(outs[0][0], outs[1][0])
+        assert torch.equal(outs[0][1].psum, outs[1][1].psum) and torch.equal(outs[0][1].pm2, outs[1][1].pm2)
+        _tune((TUNE_PP_FULL, 1))
+        _check_halo_conv(case, (128,))
+    finally:
+        _tune(*TUNE_DEFAULTS, (TUNE_PP_FULL, 0))
+
+
 @pytest.mark.parametrize("case", SPLITK_CASES)
 def test_conv3x3_pingpong_splitk(case):
     """split-K: blocks walk chunk ranges, fp32 slabs, deterministic finish."""

@@ -187,7 +187,7 @@ def test_attn_gate_ops_vs_torch():
     """AttentionGate (unet_parts.py:7-30), train-mode BatchNorms: output, psi
     map, running statistics and every input / parameter gradient."""
     g = torch.Generator().manual_seed(13)
-    F_g, F_l, F_int = 16, 24, 8
+    F_g, F_l, F_int = 16, 32, 8      # (the gate kernels take C = 8 * 2^k channels)
     gt = torch.randn(2, F_g, 12, 10, generator=g)
     xt = torch.randn(2, F_l, 12, 10, generator=g)
     params = _gate_params(g, F_g, F_l, F_int)
@@ -266,8 +266,8 @@ def test_opcheck_round4_ops():
     x = _act(torch.randn(2, 8, 6, 6, generator=g)).requires_grad_(True)
     w = (torch.randn(8, 8, 2, 2, generator=g) * 0.1).to(DEV).requires_grad_(True)
     gt = _act(torch.randn(2, 16, 6, 6, generator=g)).requires_grad_(True)
-    xt = _act(torch.randn(2, 24, 6, 6, generator=g)).requires_grad_(True)
-    params = [p.to(DEV).requires_grad_(True) for p in _gate_params(g, 16, 24, 8)]
+    xt = _act(torch.randn(2, 32, 6, 6, generator=g)).requires_grad_(True)
+    params = [p.to(DEV).requires_grad_(True) for p in _gate_params(g, 16, 32, 8)]
     running = [torch.zeros(8, device=DEV), torch.ones(8, device=DEV), torch.zeros(8, device=DEV),
                torch.ones(8, device=DEV), torch.zeros(1, device=DEV), torch.ones(1, device=DEV)]
     f4 = _act(torch.randn(2, 64, 2, 2, generator=g)).requires_grad_(True)

@@ -87,6 +87,7 @@ def test_unet_config2_every_gemm_per_element():
     # weights (6), v4 ping-pong incl. split-K (4), 1x1 streams (8), halo wgrad (3)
     assert {9, 6, 4, 8} <= _kernels(audit, "fwd"), _kernels(audit, "fwd")
     assert 3 in _kernels(audit, "wgrad"), _kernels(audit, "wgrad")
+    assert 1 not in _kernels(audit, "fwd") and 1 not in _kernels(audit, "wgrad"), audit.summary()
     assert any(r["acc"] for r in wg) and any(r["acc"] for r in fwd)
 
 
@@ -110,3 +111,5 @@ def test_unetresnet_config3_every_gemm_per_element():
     # stem (10), v7 small-grid encoder levels (7), v4 / v6 decoder levels
     assert {10, 7} <= _kernels(audit, "fwd"), _kernels(audit, "fwd")
     assert 3 in _kernels(audit, "wgrad"), _kernels(audit, "wgrad")
+    # no launch of a bf16 step falls to the generic register-staged kernels
+    assert 1 not in _kernels(audit, "fwd") and 1 not in _kernels(audit, "wgrad"), audit.summary()

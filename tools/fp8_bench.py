@@ -4,7 +4,13 @@ inc.0 at the 1024^2 layer shapes (1,472.5 GFLOP/img of 3x3
 forward), timed per layer with HIP events, against the bf16 halo kernels on
 the same shapes; error vs the unquantised fp32 conv reported per layer.
 
-usage: python tools/fp8_bench.py [--batch 2] [--reps 20] [--layers inc.2,...] [--json out.json]
+--double: the DoubleConv blocks instead (conv -> BN -> ReLU, twice, train-mode
+BatchNorm), timed end to end INCLUDING every activation quantisation: the
+delayed-scaling fp8 path (fp8.double_conv_forward: one-pass input quantise,
+BN1 apply fused with the e4m3 quantise) and the just-in-time fp8 path
+against the bf16 engine path (engine.double_conv_fwd) on the same module.
+
+usage: python tools/fp8_bench.py [--batch 2] [--reps 20] [--layers inc.2,...] [--double] [--json out.json]
 """
 import argparse
 import json
@@ -20,6 +26,59 @@ from vaeunet_amd import kernels as K  # noqa: E402
 from vaeunet_amd.engine import w3x3_fwd  # noqa: E402
 
 PEAK_FP8, PEAK_BF16 = 5000.0, 2500.0
+# (name, cin sources, cout, H) of the DoubleConv blocks of UNet(3,2) at 1024^2
+# (inc: 3 input channels, not an fp8 shape; its conv2 is inc.2 above)
+BLOCKS = [
+    ("down1", [64], 128, 512), ("down2", [128], 256, 256), ("down3", [256], 512, 128),
+    ("down4", [512], 1024, 64), ("up1", [512, 512], 512, 128), ("up2", [256, 256], 256, 256),
+    ("up3", [128, 128], 128, 512), ("up4", [64, 64], 64, 1024),
+]
+
+
+def double_main(args):
+    from vaeunet_amd import DoubleConv
+    from vaeunet_amd import engine as E
+    dev = torch.device("cuda")
+    B = args.batch
+    rows, tot = [], {"bf16": 0.0, "fp8": 0.0, "fp8_jit": 0.0, "fl": 0.0}
+    for name, cins, co, H in BLOCKS:
+        if args.layers and name not in args.layers.split(","):
+            continue
+        ci = sum(cins)
+        mod = DoubleConv(ci, co).to(dev).train()
+        srcs = [torch.randn(B, c, H, H, device=dev).relu().to(torch.bfloat16).contiguous(memory_format=K.CL)
+                for c in cins]
+        fl = 2.0 * B * H * H * co * 9 * (ci + co)
+        M = E.Mode(_lib.BF16, dev)
+
+        def bf16():
+            E.double_conv_fwd(M, mod.double_conv, srcs)
+        msb = timeit(bf16, args.reps)
+        ms8 = timeit(lambda: fp8.double_conv_forward(mod, srcs), args.reps)
+        msj = timeit(lambda: fp8.double_conv_forward(mod, srcs, delayed=False), args.reps)
+        with torch.no_grad():
+            yb = E.double_conv_fwd(M, mod.double_conv, srcs)[0].float()
+            y8 = fp8.double_conv_forward(mod, srcs).float()
+        row = {"block": name, "cin": ci, "cout": co, "hw": H, "bf16_us": round(msb * 1e3, 1),
+               "fp8_us": round(ms8 * 1e3, 1), "fp8_jit_us": round(msj * 1e3, 1),
+               "speedup": round(msb / ms8, 3), "speedup_jit": round(msb / msj, 3),
+               "rel_err_vs_bf16": round(((y8 - yb).abs().max() / yb.abs().max()).item(), 4)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+        tot["bf16"] += msb
+        tot["fp8"] += ms8
+        tot["fp8_jit"] += msj
+        tot["fl"] += fl
+        del srcs, mod
+        torch.cuda.empty_cache()
+    summ = {"batch": B, "image": "3x1024x1024", "blocks": len(rows), "bf16_ms": round(tot["bf16"], 3),
+            "fp8_ms": round(tot["fp8"], 3), "fp8_jit_ms": round(tot["fp8_jit"], 3),
+            "speedup": round(tot["bf16"] / tot["fp8"], 3), "speedup_jit": round(tot["bf16"] / tot["fp8_jit"], 3),
+            "fp8_block_tflops": round(tot["fl"] / tot["fp8"] / 1e9, 1)}
+    print("SUMMARY " + json.dumps(summ), flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump({"blocks": rows, "summary": summ}, f, indent=1)
 # (name, cin sources, cout, H) of the 3x3 convs of UNet(3,2) at 1024^2 (inc.0 excluded)
 LAYERS = [
     ("inc.2", [64], 64, 1024), ("down1.1", [64], 128, 512), ("down1.2", [128], 128, 512),
@@ -52,13 +111,16 @@ def main():
     ap.add_argument("--layers", default="")
     ap.add_argument("--no-bf16", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--double", action="store_true", help="time whole DoubleConv blocks (see above)")
     ap.add_argument("--tune", default="", help="KEY=VAL,... vu_gemm_set_tuning before the run (A/B)")
     args = ap.parse_args()
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
         _lib.call("vu_gemm_set_tuning", int(k), int(v))
-    dev = torch.device("cuda")
     torch.manual_seed(0)
+    if args.double:
+        return double_main(args)
+    dev = torch.device("cuda")
     B = args.batch
     rows = []
     tot = {"fp8": [0.0, 0.0], "bf16": [0.0, 0.0], "quant": [0.0, 0.0]}

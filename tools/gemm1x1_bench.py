@@ -57,7 +57,8 @@ def main():
         wf = w1x1_fwd(w, d)
         ms = timeit(lambda: K.gemm_fwd(K.gather1x1([x]), wf, Fi, u, d, bias=b, stats=True), args.reps)
         byts = B * S * S * (C + Fi) * 2
-        line = f"{name} attn fwd  {C:4d}->{Fi:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s"
+        fl = 2.0 * B * S * S * C * Fi
+        line = f"{name} attn fwd  {C:4d}->{Fi:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s {fl / ms / 1e9:6.0f}TF"
         if args.check:
             line += f" err {err(u, F.conv2d(x.float(), w.bfloat16().float(), b)):.1e}"
         tot += ms
@@ -72,7 +73,7 @@ def main():
             e1 = err(dx, ref)
         ms = timeit(lambda: K.gemm_fwd(K.gather1x1([du]), wd, C, dx, d, accumulate=True), args.reps)
         byts = B * S * S * (Fi + 2 * C) * 2
-        line = f"{name} attn dgrad {Fi:4d}->{C:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s"
+        line = f"{name} attn dgrad {Fi:4d}->{C:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s {fl / ms / 1e9:6.0f}TF"
         if args.check:
             line += f" err {e1:.1e}"
         tot += ms
@@ -87,7 +88,8 @@ def main():
         fn = lambda: K.gemm_fwd(K.gather1x1([x1]), wtf, 4 * co, uo, d, bias=bt, convT=(S, S, 0, 0, co))  # noqa
         ms = timeit(fn, args.reps)
         byts = B * (h * h * ci + S * S * co) * 2
-        line = f"{name} convT fwd {ci:4d}->{co:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s"
+        fl = 2.0 * B * h * h * ci * 4 * co
+        line = f"{name} convT fwd {ci:4d}->{co:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s {fl / ms / 1e9:6.0f}TF"
         if args.check:
             line += f" err {err(uo, F.conv_transpose2d(x1.float(), wt.bfloat16().float(), bt, stride=2)):.1e}"
         tot += ms
@@ -97,13 +99,22 @@ def main():
         wtd = wT_dgrad(wt, d)
         fn = lambda: K.gemm_fwd(K.gather_convT(duo, B, h, h), wtd, ci, dx1, d)  # noqa
         ms = timeit(fn, args.reps)
-        line = f"{name} convT dgrad {co:4d}->{ci:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s"
+        line = f"{name} convT dgrad {co:4d}->{ci:4d} @{S:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s {fl / ms / 1e9:6.0f}TF"
         if args.check:
             ref = torch.nn.grad.conv2d_weight  # placeholder to keep flake quiet
             xr = x1.float().requires_grad_(True)
             yr = F.conv_transpose2d(xr, wt.bfloat16().float(), None, stride=2)
             yr.backward(duo.float())
             line += f" err {err(dx1, xr.grad):.1e}"
+        tot += ms
+        print(line, flush=True)
+        # ConvTranspose2d weight gradient: x1^T x gather(du) (split-K slabs + reduce)
+        gw = torch.empty(ci, co, 2, 2, device=dev)
+        from vaeunet_amd.engine import convT_layout
+        fn = lambda: K.gemm_wgrad(K.gather1x1([x1]), K.gather_convT(duo, B, h, h), ci, 4 * co, gw,  # noqa: E731
+                                  convT_layout(gw), d, False)
+        ms = timeit(fn, args.reps)
+        line = f"{name} convT wgrad {ci:4d}x{4 * co:4d} @{h:3d}: {ms * 1e3:7.1f}us {byts / ms / 1e9:5.2f}TB/s {fl / ms / 1e9:6.0f}TF"
         tot += ms
         print(line, flush=True)
     print(f"TOTAL {tot:.3f} ms")

@@ -100,6 +100,7 @@ _SIGS = {
     "vu_amax": (_i, [_p, _l, _l, _i, _p, _i, _i, _p]),
     "vu_quant_fp8": (_i, [_p, _l, _l, _i, _p, _p, _l, _p, _i, _p]),
     "vu_quant_rows_fp8": (_i, [_p, _i, _l, _p, _l, _p, _p]),
+    "vu_bn_apply_fp8": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _i, _p, _i, _i, _p, _i, _p]),
     "vu_conv3x3_fp8_row_tile": (_l, [C.POINTER(VuConvFp8)]),
     "vu_conv3x3_fp8": (_i, [C.POINTER(VuConvFp8), _p]),
     "vu_conv3x3_fp8_workspace_bytes": (_l, [C.POINTER(VuConvFp8)]),

@@ -1183,6 +1183,82 @@ int nblocks(int64_t n, int per) {
   return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
 }
 
+// ---- BatchNorm apply (+ReLU) fused with e4m3 quantisation, delayed scaling --
+// z = relu?(x * scale[c] + shift[c]) (two roundings, no FMA contraction, so
+// the result is the unfused apply's fp32 value), q = e4m3(clamp(z * s)),
+// s = 448 / ring[slot] -- the amax RECORDED BY THE PREVIOUS STEP -- while
+// this step's max |z| is max-accumulated into ring[(slot+1)%3] for the next
+// one, and ring[(slot+2)%3] (last step's scale slot, read by no one this
+// step) is cleared for the step after.  One read of the bf16 conv output,
+// one 1-byte write: the bf16 activation, its amax pass and its quantise pass
+// of the three-launch path never touch HBM.  scale == nullptr: identity
+// affine (quantise a bf16 activation with the delayed scale).
+// CALIB: only max-accumulate max |z| into ring[slot] (first step: no
+// history), nothing stored.
+constexpr int Q8_UNR = 4;
+
+template <typename T, bool CALIB>
+__global__ __launch_bounds__(256) void bn_apply_q8_kernel(const T* x, int64_t xs, uint8_t* y, int64_t ys, int64_t P,
+                                                          int C, const float* scale, const float* shift, int relu,
+                                                          float* ring, int slot, float* dq) {
+  const int V = C >> 3;
+  const int R = 256 / V;
+  const int c = (threadIdx.x & (V - 1)) * 8;
+  const int row = threadIdx.x / V;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale ? scale[c + i] : 1.f;
+    sh[i] = scale ? shift[c + i] : 0.f;
+  }
+  float s = 1.f;
+  if (!CALIB) {
+    s = qscale(ring[slot]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      if (dq) dq[0] = 1.f / s;
+      ring[(slot + 2) % 3] = 0.f;
+    }
+  }
+  float m = 0.f;
+  const int64_t step = (int64_t)gridDim.x * R * Q8_UNR;
+  for (int64_t p0 = (int64_t)blockIdx.x * R * Q8_UNR + row; p0 < P; p0 += step) {
+    Vec8<T> v[Q8_UNR];
+#pragma unroll
+    for (int u = 0; u < Q8_UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * R;
+      if (p < P) v[u].load(x + p * xs + c);
+    }
+#pragma unroll
+    for (int u = 0; u < Q8_UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * R;
+      if (p >= P) continue;
+      float f[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float z = scale ? __fadd_rn(__fmul_rn(v[u].get(i), sc[i]), sh[i]) : v[u].get(i);
+        if (relu) z = fmaxf(z, 0.f);
+        m = fmaxf(m, fabsf(z));
+        f[i] = clamp448(z * s);
+      }
+      if (!CALIB) {
+        u32x2 o;
+        o[0] = e4m3x4(f[0], f[1], f[2], f[3]);
+        o[1] = e4m3x4(f[4], f[5], f[6], f[7]);
+        *reinterpret_cast<u32x2*>(y + p * ys + c) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float shm[4];
+  if ((threadIdx.x & 63) == 0) shm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float r = fmaxf(fmaxf(shm[0], shm[1]), fmaxf(shm[2], shm[3]));
+    atomicMax(reinterpret_cast<unsigned*>(ring + (CALIB ? slot : (slot + 1) % 3)), __float_as_uint(r));
+  }
+}
+
 }  // namespace
 
 int conv_fp8_tune(int key, int value) {
@@ -1285,6 +1361,33 @@ extern "C" int vu_quant_fp8(const void* x, int64_t xs, int64_t P, int C, const f
     hipLaunchKernelGGL(quant_kernel<bf16_t>, dim3(nb), dim3(256), 0, st, (const bf16_t*)x, xs, P, C, amax, y, ys, dq);
   else
     hipLaunchKernelGGL(quant_kernel<float>, dim3(nb), dim3(256), 0, st, (const float*)x, xs, P, C, amax, y, ys, dq);
+  VU_CHECK_LAUNCH();
+}
+
+extern "C" int vu_bn_apply_fp8(const void* x, int64_t xs, uint8_t* y, int64_t ys, int64_t P, int C,
+                               const float* scale, const float* shift, int relu, float* amax_ring, int slot,
+                               int calibrate, float* dq, int dtype, void* stream) {
+  const int V = C / 8;
+  if (C % 8 != 0 || V < 1 || V > 256 || (V & (V - 1)) != 0 || xs % 8 != 0 || P < 0 || slot < 0 || slot > 2 ||
+      !amax_ring || (!calibrate && (ys % 8 != 0 || !y)) || (scale && !shift) || (dtype != VU_BF16 && dtype != VU_F32))
+    return (int)hipErrorInvalidValue;
+  if (P == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t R = 256 / V;
+  int64_t g = (P + R * 16 - 1) / (R * 16);          // ~16 pixel rows per thread
+  const int64_t g1 = (P + R * Q8_UNR - 1) / (R * Q8_UNR);
+  if (g < 256) g = g1 < 256 ? g1 : 256;               // small tensors: >= one CU sweep
+  if (g > 8192) g = 8192;
+  const dim3 grid((unsigned)g);
+#define VU_Q8_LAUNCH(T, CAL)                                                                                  \
+  hipLaunchKernelGGL((bn_apply_q8_kernel<T, CAL>), grid, dim3(256), 0, st, (const T*)x, xs, y, ys, P, C, scale, \
+                     shift, relu, amax_ring, slot, dq)
+  if (dtype == VU_BF16) {
+    if (calibrate) VU_Q8_LAUNCH(bf16_t, true); else VU_Q8_LAUNCH(bf16_t, false);
+  } else {
+    if (calibrate) VU_Q8_LAUNCH(float, true); else VU_Q8_LAUNCH(float, false);
+  }
+#undef VU_Q8_LAUNCH
   VU_CHECK_LAUNCH();
 }
 

@@ -325,6 +325,8 @@ int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v2_launch(const VuGemmFwd& p, hipStream_t st);
 int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v2_small_launch(const VuGemmFwd& p, hipStream_t st);
+int gemm_fwd_v2_tail(const VuGemmFwd& p, int dtype);
+int gemm_fwd_v2_tail_launch(const VuGemmFwd& p, hipStream_t st);
 int64_t gemm_fwd_v2_small_workspace(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_bm(const VuGemmFwd& p, int dtype);
 int gemm_fwd_v3_launch(const VuGemmFwd& p, hipStream_t st);
@@ -381,6 +383,8 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
     if (bm) return bm;
     bm = gemm_fwd_v2_bm(*args, dtype);
     if (bm) return bm;
+    bm = gemm_fwd_v2_tail(*args, dtype);
+    if (bm) return bm;
   }
   return pick_bm(*args);
 }
@@ -408,7 +412,8 @@ extern "C" int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype) {
 // Which kernel the dispatcher below picks (mirrors its order; tests assert the
 // path they mean to cover): 1 generic, 2 v2 LDS-DMA tiles, 3 v3 halo, 4 v4
 // ping-pong, 5 v5 persistent short-K, 6 v6 resident weights, 7 v7 small-grid,
-// 8 1x1 stream, 9 image conv, 10 7x7 stem, 12 v2 small-grid mode.
+// 8 1x1 stream, 9 image conv, 10 7x7 stem, 12 v2 small-grid mode, 13 v2
+// tail (small grids nothing else admits).
 extern "C" int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype) {
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return 9;
   if (use_v2(dtype) && conv_stem_bm(*args, dtype)) return 10;
@@ -420,6 +425,7 @@ extern "C" int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype) {
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return 3;
   if (use_v2(dtype) && gemm_fwd_v5_bm(*args, dtype)) return 5;
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return 2;
+  if (use_v2(dtype) && gemm_fwd_v2_tail(*args, dtype)) return 13;
   return 1;
 }
 
@@ -443,6 +449,7 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
   if (use_v3(dtype) && gemm_fwd_v3_bm(*args, dtype)) return gemm_fwd_v3_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v5_bm(*args, dtype)) return gemm_fwd_v5_launch(*args, st);
   if (use_v2(dtype) && gemm_fwd_v2_bm(*args, dtype)) return gemm_fwd_v2_launch(*args, st);
+  if (use_v2(dtype) && gemm_fwd_v2_tail(*args, dtype)) return gemm_fwd_v2_tail_launch(*args, st);
   return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);
 }
 

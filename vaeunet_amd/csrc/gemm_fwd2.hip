@@ -323,21 +323,27 @@ int v2_cfg(const VuGemmFwd& p) {
 // (fp32, channel groups not 64-aligned — a single 1x1 source may end on a
 // 32-channel boundary —, ragged column counts, or too few tiles to fill the
 // chip).
-int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
+static bool v2_shape_ok(const VuGemmFwd& p, int dtype) {
   const VuGather& g = p.a;
-  if (dtype != VU_BF16) return 0;
+  if (dtype != VU_BF16) return false;
   const bool one = g.R == 1 && g.S == 1;
   for (int t = 0; t < g.nsrc; ++t) {
     const bool last = t == g.nsrc - 1;
-    if (g.stride[t] % 8 != 0) return 0;
-    if (g.cend[t] % 64 != 0 && !(one && last && g.cend[t] % 32 == 0)) return 0;
+    if (g.stride[t] % 8 != 0) return false;
+    if (g.cend[t] % 64 != 0 && !(one && last && g.cend[t] % 32 == 0)) return false;
   }
-  if (p.ncol % 8 != 0 || p.ldb % 8 != 0) return 0;
+  if (p.ncol % 8 != 0 || p.ldb % 8 != 0) return false;
   if (p.out_mode == 1) {
-    if (p.cout % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0) return 0;
+    if (p.cout % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0) return false;
   } else if (p.out_stride % 8 != 0 || p.out_coff % 8 != 0) {
-    return 0;
+    return false;
   }
+  return (int64_t)g.N * g.H * g.W > 0;
+}
+
+int gemm_fwd_v2_bm(const VuGemmFwd& p, int dtype) {
+  const VuGather& g = p.a;
+  if (!v2_shape_ok(p, dtype)) return 0;
   int64_t M = (int64_t)g.N * g.H * g.W;
   int bn = p.ncol <= 64 ? 64 : 128;
   int64_t tiles = ((M + 255) / 256) * ((p.ncol + bn - 1) / bn);
@@ -393,6 +399,19 @@ int gemm_fwd_v2_small_launch(const VuGemmFwd& p, hipStream_t st) {
   hipLaunchKernelGGL((gemm_fwd_v2_kernel<128, 64, 2, 2, 3, true>), dim3((unsigned)nblk), dim3(256), 0, st, q);
   return splitk_finish_launch(q, st);
 }
+
+// Every other bf16 GEMM the v2 gather serves -- the ones no tile-count rule
+// above admits: the ResNet34 decoder's attention-gate 1x1 convs (F_int = 32
+// columns) and the downsample shortcuts' stride-2 input gradients at the 64^2
+// .. 16^2 levels (out_mode 2), K of one or a few 64-steps.  One 128 x 64
+// tile per block (4 waves), no split: these are latency-bound launches of a
+// few microseconds, and the generic register-staged kernel they fell to took
+// ~11 us each (round-3 config-3 profile).  VU_TUNE_V2_SMALL = 0 turns it off.
+int gemm_fwd_v2_tail(const VuGemmFwd& p, int dtype) {
+  return g_small && v2_shape_ok(p, dtype) ? 128 : 0;
+}
+
+int gemm_fwd_v2_tail_launch(const VuGemmFwd& p, hipStream_t st) { return launch_ns<128, 64, 2, 2>(p, st); }
 
 int gemm_fwd_v2_tune(int key, int value) {
   if (key == VU_TUNE_V2_SMALL) {

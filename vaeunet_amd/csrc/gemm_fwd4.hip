@@ -80,7 +80,11 @@ VU_DEV float ror_add(float v) {
 }
 VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
 
-template <int BN, bool SPLIT, bool BNB, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
+// RELU: epilogue ReLU (VuGemmFwd.relu).  FULL: one read segment + one
+// 32-MFMA segment per step (2 barriers) instead of two 16-MFMA halves (4
+// barriers): twice the matrix work per barrier interval, 16 more fragment
+// registers (VU_TUNE_PP_FULL, A/B).
+template <int BN, bool SPLIT, bool BNB, bool RELU = false, bool FULL = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -242,6 +246,38 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       const int pt = t + PD < 9 ? t + PD : t + PD - 9;
       const bool pref = t + PD < 9 || next_here;      // the step two ahead exists
       const int pc = t + PD < 9 ? c : c + 1;
+      if constexpr (FULL) {
+        // -- one read segment: weights + all 8 pixel fragments; half 0
+        //    prefetches the weights two steps ahead and waits for the next
+        //    step's, half 1 streams the next chunk's halo (waits at tap 8)
+        u32x4 bq[4], aq[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[j] = *reinterpret_cast<const u32x4*>(Bw + brow + j * 16 * 64);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) aq[i] = *reinterpret_cast<const u32x4*>(A + arow(i));
+        if (!grp) {
+          if (pref) {
+            wstage(pc, pt, pslot, 0, LB0);
+            wait_vm_c<(PD - 1) * LB0>();
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        } else {
+          if (t == 0 && next_here) halo_chunk(c + 1, hb ^ 1);
+          if (t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        pp_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bq[j]),
+                                                                __builtin_bit_cast(bf16x8, aq[i]), acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+        continue;
+      }
       u32x4 bf[4], af[4];
       // -- phase 1: weights + pixel fragments 0..3; half 0 prefetches the
       //    weights two steps ahead
@@ -638,6 +674,7 @@ bool tiles_ok(const VuGemmFwd& p) {
 
 int g_min_blocks = 256;  // vu_gemm_set_tuning(VU_TUNE_V4_MIN_BLOCKS, ...)
 int g_splitk = 1;        // vu_gemm_set_tuning(VU_TUNE_V4_SPLITK, ...): 0 off, 1 auto, k >= 2 forced
+int g_pp_full = 0;       // VU_TUNE_PP_FULL: one phase per step (conv3x3_pp_kernel FULL)
 
 // Output-column tile the ping-pong kernel uses for this problem (0 = not served).
 int pick_bn(const VuGemmFwd& p) {
@@ -724,6 +761,9 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     else if (p.relu)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+    else if (BN != 64 && g_pp_full)  // (BN = 64 spills with the extra fragments)
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64>), dim3((unsigned)tiles), dim3(512), 0,
+                         st, q);
     else
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     return (int)hipGetLastError();
@@ -818,6 +858,10 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
   }
   if (key == VU_TUNE_V4_SPLITK) {
     g_splitk = value;
+    return 0;
+  }
+  if (key == VU_TUNE_PP_FULL) {
+    g_pp_full = value;
     return 0;
   }
   if (key == VU_TUNE_V4_SPLIT_CHUNKS) {

@@ -280,7 +280,9 @@ int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
     for (int t = 0; t < g->nsrc; ++t)
       if (g->cend[t] % 8 || g->stride[t] % 8) return 0;
   int64_t M = (int64_t)p.p.N * p.p.H * p.p.W;
-  if (M < 4096) return 0;
+  // (round 4: was 4096, which sent the ResNet34 16^2 level (M = 2048 at
+  // batch 8) to the generic register-staged kernel at ~90 TFLOP/s)
+  if (M < 512) return 0;
   // small outputs (the attention gates' 1x1 convs) get a tile that fits them
   // instead of streaming zero columns through a 256-wide one
   if (p.ni <= 32 && p.nj <= 64) { *bi = 32; *bj = 64; return 1; }

@@ -49,6 +49,55 @@ def quantize(x, am):
     return q, dq
 
 
+class DelayedScale:
+    """Delayed (previous-step) per-tensor scaling of one fp8 activation site.
+
+    ``ring`` holds three fp32 amax slots on the device: step t quantises with
+    s = 448 / ring[t % 3] (the amax step t-1 recorded), max-accumulates its
+    own max |x| into ring[(t+1) % 3] and clears ring[(t+2) % 3] -- all inside
+    the quantising kernel (vu_bn_apply_fp8), so the step adds no launch and
+    no host sync.  The first step has no history: a calibration pass of the
+    same kernel measures max |x| into ring[0] first.  Values above the stale
+    amax saturate at +-448 (standard delayed-scaling behaviour)."""
+
+    def __init__(self, device):
+        self.ring = torch.zeros(3, dtype=torch.float32, device=device)
+        self.t = 0
+
+    @property
+    def slot(self):
+        return self.t % 3
+
+    def advance(self):
+        self.t += 1
+
+
+def _q8_args(x, coef, relu, ds):
+    N, Cc, H, W = x.shape
+    sc = C.c_void_p(coef[0].data_ptr()) if coef is not None else None
+    sh = C.c_void_p(coef[1].data_ptr()) if coef is not None else None
+    return (N * H * W, Cc, sc, sh, 1 if relu else 0, C.c_void_p(ds.ring.data_ptr()), ds.slot)
+
+
+def calibrate(x, coef, relu, ds):
+    """First step of a site (no history): max-accumulate max |z| of this
+    source into the scale slot bn_apply_quant is about to read."""
+    call("vu_bn_apply_fp8", C.c_void_p(x.data_ptr()), K.pstride(x), None, 0, *_q8_args(x, coef, relu, ds), 1,
+         None, K.dcode(x.dtype), stream())
+
+
+def bn_apply_quant(x, coef, relu, ds):
+    """e4m3 NHWC relu?(x * coef[0] + coef[1]) (coef None: relu?(x)) with the
+    delayed scale ``ds``; returns (q, dequant scale [1]).  One pass over x;
+    the caller advances ``ds`` once per step (after every source of a site)."""
+    N, Cc, H, W = x.shape
+    q = torch.empty((N, Cc, H, W), dtype=E4M3, device=x.device, memory_format=K.CL)
+    dq = torch.empty(1, dtype=torch.float32, device=x.device)
+    call("vu_bn_apply_fp8", C.c_void_p(x.data_ptr()), K.pstride(x), C.c_void_p(q.data_ptr()), K.pstride(q),
+         *_q8_args(x, coef, relu, ds), 0, C.c_void_p(dq.data_ptr()), K.dcode(x.dtype), stream())
+    return q, dq
+
+
 def quantize_rows(m):
     """fp32 [rows][cols] -> (e4m3 [rows][cols], per-row dequant scale [rows])."""
     rows, cols = m.shape
@@ -123,17 +172,58 @@ def conv3x3_q(srcs, weight, bias=None, stats=False):
     return conv3x3(qs, dq, wq, ws, weight.shape[0], bias=bias, stats=stats)
 
 
+def _site_scales(mod, device):
+    ent = mod.__dict__.get("_vu_fp8_scales")
+    if ent is None:
+        ent = (DelayedScale(device), DelayedScale(device))
+        mod.__dict__["_vu_fp8_scales"] = ent
+    return ent
+
+
 @torch.no_grad()
-def double_conv_forward(mod, x):
+def double_conv_forward(mod, x, delayed=True):
     """DoubleConv.forward (unet_parts.py:32-49) with both 3x3 convs in fp8:
     conv -> BatchNorm (batch statistics from the fp8 conv epilogue in train
-    mode, running statistics in eval mode) -> ReLU, twice; bf16 NHWC out."""
+    mode, running statistics in eval mode) -> ReLU, twice; bf16 NHWC out.
+    x: a bf16 NHWC tensor, or the list of channel-concat sources of an Up
+    block's DoubleConv (they share one scale, as in conv3x3_q).
+
+    delayed=True (default): both activation quantisations use the amax the
+    previous call recorded (DelayedScale, one per site, kept on the module):
+    the input is quantised in one pass (no amax pass) and BN1 + ReLU is
+    applied and quantised in the same pass (vu_bn_apply_fp8), so conv2's
+    input is never stored in bf16.  delayed=False: just-in-time scaling
+    (amax pass + quantise pass of the bf16 BN1 output)."""
     conv1, bn1, _, conv2, bn2, _ = mod.double_conv
-    a = x
-    for conv, bn in ((conv1, bn1), (conv2, bn2)):
-        y, st = conv3x3_q([a], conv.weight, stats=bn.training)
-        coef = E.bn_coef(bn, st, conv.out_channels)
-        out = torch.empty_like(y)
-        K.bn_apply(y, out, coef, True, _lib.BF16)
-        a = out
-    return a
+    srcs = list(x) if isinstance(x, (list, tuple)) else [x]
+    if not delayed:
+        a = srcs
+        for conv, bn in ((conv1, bn1), (conv2, bn2)):
+            y, st = conv3x3_q(a, conv.weight, stats=bn.training)
+            coef = E.bn_coef(bn, st, conv.out_channels)
+            out = torch.empty_like(y)
+            K.bn_apply(y, out, coef, True, _lib.BF16)
+            a = [out]
+        return a[0]
+    ds_in, ds_mid = _site_scales(mod, srcs[0].device)
+    if ds_in.t == 0:
+        for t in srcs:               # every source first: they share the scale
+            calibrate(t, None, False, ds_in)
+    qs = []
+    for t in srcs:
+        q, xdq = bn_apply_quant(t, None, False, ds_in)
+        qs.append(q)
+    w1, s1 = quantize_weight(conv1.weight)
+    y1, st1 = conv3x3(qs, xdq, w1, s1, conv1.out_channels, stats=bn1.training)
+    coef1 = E.bn_coef(bn1, st1, conv1.out_channels)
+    if ds_mid.t == 0:
+        calibrate(y1, coef1, True, ds_mid)
+    aq, adq = bn_apply_quant(y1, coef1, True, ds_mid)
+    w2, s2 = quantize_weight(conv2.weight)
+    y2, st2 = conv3x3([aq], adq, w2, s2, conv2.out_channels, stats=bn2.training)
+    coef2 = E.bn_coef(bn2, st2, conv2.out_channels)
+    out = torch.empty_like(y2)
+    K.bn_apply(y2, out, coef2, True, _lib.BF16)
+    ds_in.advance()
+    ds_mid.advance()
+    return out

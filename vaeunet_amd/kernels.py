@@ -124,7 +124,8 @@ AUDIT = None
 # functions the launch runs (the roofline line names what it timed)
 FWD_KERNELS = {1: "gemm_fwd_kernel", 2: "gemm_fwd_v2_kernel", 3: "conv3x3_halo_kernel", 4: "conv3x3_pp_kernel",
                5: "gemm_fwd_v5_kernel", 6: "conv3x3_c64_kernel", 7: "conv3x3_sg_kernel", 8: "gemm_stream_kernel",
-               9: "conv3x3_image_kernel", 10: "conv_stem_kernel", 12: "gemm_fwd_v2_kernel(small-grid)"}
+               9: "conv3x3_image_kernel", 10: "conv_stem_kernel", 12: "gemm_fwd_v2_kernel(small-grid)",
+               13: "gemm_fwd_v2_kernel(tail)"}
 WGRAD_KERNELS = {1: "gemm_wgrad_kernel", 2: "gemm_wgrad_v2_kernel", 3: "wgrad3x3_halo_kernel"}
 
 

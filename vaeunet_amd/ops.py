@@ -524,7 +524,7 @@ def _gate_backward(ctx, gout, _gpsi, _grun):
     t = ctx.saved_tensors
     g, x, params, running = t[0], t[1], list(t[2:2 + ctx.np]), list(t[2 + ctx.np:])
     dg, dx, dps = attn_gate_bwd(g, x, gout, params, running, *ctx.cfg)
-    return dg, dx, dps, None, None, None
+    return dg, dx, dps, [None] * len(running), None, None
 
 
 attn_gate_fwd.register_autograd(_gate_backward, setup_context=_gate_setup)
