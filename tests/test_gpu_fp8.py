@@ -255,7 +255,7 @@ def test_bn_apply_fp8_bit_exact(C_, dtype, slot):
     xd = _act(x, dtype)
     ds = fp8.DelayedScale(DEV)
     ds.t = slot
-    for relu, am_prev in ((True, 1.7), (False, 40.0)):      # 1.7: far below max|z| -> saturation
+    for relu, am_prev in ((True, 1.75), (False, 40.0)):     # 1.75: far below max|z| -> saturation
         ring = torch.tensor([5.0, 5.0, 5.0])
         ring[slot] = am_prev
         ds.ring.copy_(ring)

@@ -45,7 +45,9 @@ def timeit(fn, reps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tune", default="")
+    ap.add_argument("--wsplit", type=int, default=0, help="cap on the weight-gradient split-K ways (A/B)")
     args = ap.parse_args()
+    K.WGRAD_SPLIT_CAP = args.wsplit
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
         _lib.call("vu_gemm_set_tuning", int(k), int(v))

@@ -45,6 +45,22 @@ VU_DEV void epi_relu(f32x4 (&a)[N]) {
     for (int r = 0; r < 4; ++r) a[i][r] = fmaxf(a[i][r], 0.f);
 }
 
+// Division by a divisor fixed for the whole launch (image width, pixels per
+// image, ConvT output channels), for dividends n < 2^31: q = (umulhi(n, m) +
+// n) >> l with l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1 (Granlund
+// & Montgomery; exact for every n < 2^31).  Built once per thread (uniform
+// arguments: scalar code); each division is then 3 VALU ops instead of the
+// ~20 of a runtime 32-bit integer division.
+struct FastDiv {
+  uint32_t m, l, d;
+  VU_DEV explicit FastDiv(uint32_t dd) : d(dd) {
+    l = 0;
+    while ((1u << l) < dd && l < 31) ++l;
+    m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - dd)) / dd) + 1u;
+  }
+  VU_DEV uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
+};
+
 // Round a float to the storage precision (identity for fp32).
 template <typename T> VU_DEV float rnd(float v);
 template <> VU_DEV float rnd<float>(float v) { return v; }

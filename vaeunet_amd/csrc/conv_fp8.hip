@@ -1235,7 +1235,16 @@ __global__ __launch_bounds__(256) void bn_apply_q8_kernel(const T* x, int64_t xs
       float f[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        float z = scale ? __fadd_rn(__fmul_rn(v[u].get(i), sc[i]), sh[i]) : v[u].get(i);
+        // z = x * scale + shift with two roundings: hipcc contracts a*b+c into
+        // an FMA (through __fmul_rn and the fp-contract pragma alike), which
+        // moved max|z| by an ulp against the two-op restatement; the empty asm
+        // makes the product opaque
+        float z = v[u].get(i);
+        if (scale) {
+          float pr = z * sc[i];
+          asm volatile("" : "+v"(pr));
+          z = pr + sh[i];
+        }
         if (relu) z = fmaxf(z, 0.f);
         m = fmaxf(m, fabsf(z));
         f[i] = clamp448(z * s);

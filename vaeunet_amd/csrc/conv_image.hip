@@ -54,12 +54,13 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
 
   u32x4 wf[4][3];
   int cur_nt = -1;
+  const FastDiv div_hw((uint32_t)HW), div_w((uint32_t)W);  // (n, h, w) decode by multiply-shift
 
   // taps of the 16 pixels of fragment i of tile base pb (one 16-byte load per k-step)
   auto load_px = [&](int m, u32x4* pf) {
-    const int n = m / HW;
+    const int n = (int)div_hw.div((uint32_t)m);
     const int rem = m - n * HW;
-    const int h = rem / W, w = rem - (rem / W) * W;
+    const int h = (int)div_w.div((uint32_t)rem), w = rem - h * W;
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) {
       const int tap = 4 * ks + gq;
@@ -70,9 +71,16 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
     }
   };
 
-  for (int tile = blockIdx.x * (NT / 64) + wid; tile < ntiles; tile += gridDim.x * (NT / 64)) {
+  // the first fragment's taps of a wave's next tile are loaded behind the
+  // current tile's last MFMAs, so only the first tile waits out a load
+  const int tstride = gridDim.x * (NT / 64);
+  u32x4 pf[3], pn[3];
+  int tile = blockIdx.x * (NT / 64) + wid;
+  if (tile < ntiles) load_px((tile / nct) * TP + r16, pf);
+  for (; tile < ntiles; tile += tstride) {
     const int mt = tile / nct, nt = tile - mt * nct;
     const int pb = mt * TP, n0 = nt * 64;
+    const int next = tile + tstride;
     if (nt != cur_nt) {
       cur_nt = nt;
 #pragma unroll
@@ -89,21 +97,20 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
     for (int i = 0; i < NF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-    u32x4 pf[3], pn[3];
-    load_px(pb + r16, pf);
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-      if (i + 1 < NF) load_px(pb + (i + 1) * 16 + r16, pn);
+      if (i + 1 < NF)
+        load_px(pb + (i + 1) * 16 + r16, pn);
+      else if (next < ntiles)
+        load_px((next / nct) * TP + r16, pn);
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[j][ks]),
                                                               __builtin_bit_cast(bf16x8, pf[ks]), acc[i][j], 0, 0, 0);
-      if (i + 1 < NF) {
 #pragma unroll
-        for (int ks = 0; ks < 3; ++ks) pf[ks] = pn[ks];
-      }
+      for (int ks = 0; ks < 3; ++ks) pf[ks] = pn[ks];
     }
     // ---- epilogue: bias, bf16 rounding, BN partials, 16-byte stores
     const int c0 = n0 + cb16;

@@ -82,6 +82,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int gq = lane >> 4, r16 = lane & 15;
   const int pchunk = lane & 7;
+  // pixel -> (n, h, w) and ConvT column -> (tap, channel) decodes: once per
+  // tile per row, by multiply-shift (runtime integer divisions were ~1/3 of
+  // the kernel's VALU instructions)
+  const FastDiv div_hw((uint32_t)HW), div_w((uint32_t)g.W), div_co((uint32_t)(p.cout > 0 ? p.cout : 1));
   const bf16_t* bmat = reinterpret_cast<const bf16_t*>(p.b);
   const void* zp = (const void*)v5_zero_page;
 
@@ -108,9 +112,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int i = 0; i < LA; ++i) {
         const int m = mt * BM + ((i * NT + tid) >> 3);
-        pa[i].n = m / HW;
+        pa[i].n = (int)div_hw.div((uint32_t)m);
         const int rem = m - pa[i].n * HW;
-        pa[i].h = rem / g.W;
+        pa[i].h = (int)div_w.div((uint32_t)rem);
         pa[i].w = rem - pa[i].h * g.W;
       }
 #pragma unroll
@@ -161,12 +165,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
   auto dst_of = [&](int m, int col0) -> bf16_t* {
     if (p.out_mode == 0) return out + (int64_t)m * p.out_stride + p.out_coff + col0;
-    const int n = m / HW;
+    const int n = (int)div_hw.div((uint32_t)m);
     const int rem = m - n * HW;
-    const int h = rem / g.W, w = rem - (rem / g.W) * g.W;
+    const int h = (int)div_w.div((uint32_t)rem), w = rem - h * g.W;
     if (p.out_mode == 2)
       return out + ((int64_t)(n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx) * p.out_stride + p.out_coff + col0;
-    const int ab = col0 / p.cout, co = col0 - ab * p.cout;
+    const int ab = (int)div_co.div((uint32_t)col0), co = col0 - ab * p.cout;
     const int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
     return out + ((int64_t)(n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
   };

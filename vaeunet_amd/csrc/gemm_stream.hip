@@ -74,6 +74,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
   const int64_t st = g.stride[0];
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
   const int HW = g.H * g.W;
+  const FastDiv div_hw((uint32_t)HW), div_w((uint32_t)g.W), div_co((uint32_t)(p.cout > 0 ? p.cout : 1));
 
   // the next tile's operands are loaded before this tile's MFMAs and stores:
   // one tile of loads always in flight per wave (latency, not bandwidth,
@@ -163,12 +164,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
     // (permlane16 + permlane32) regroup them so that each store instruction
     // writes 64 contiguous bytes per pixel (lane row q: columns 32h + 8q ..
     // +7 of the group) instead of 16-byte pieces at a 32-byte stride.
+    // ConvT pixel shuffle: the (n, h, w) decode of a pixel and the (tap,
+    // channel) split of a column by multiply-shift (runtime divisions here
+    // were ~20 VALU each, three per 16-byte store)
     auto dst_of = [&](int64_t m, int col0) -> bf16_t* {
       if (p.out_mode == 1) {
-        const int n = (int)(m / HW);
-        const int rem = (int)(m - (int64_t)n * HW);
-        const int h = rem / g.W, w = rem - (rem / g.W) * g.W;
-        const int ab = col0 / p.cout, co = col0 - ab * p.cout;
+        const int n = (int)div_hw.div((uint32_t)m);
+        const int rem = (int)m - n * HW;
+        const int h = (int)div_w.div((uint32_t)rem), w = rem - h * g.W;
+        const int ab = (int)div_co.div((uint32_t)col0), co = col0 - ab * p.cout;
         const int oy = 2 * h + (ab >> 1) + p.opy, ox = 2 * w + (ab & 1) + p.opx;
         return out + ((int64_t)(n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
       }

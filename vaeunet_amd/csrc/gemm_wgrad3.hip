@@ -192,21 +192,27 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
       q_rel[k] = q >= 0 ? (int)((int64_t)(((q & 15) - 1) * W + ((q >> 4) & 63) - 1) * xst + (q >> 10)) : INT32_MIN;
     }
   }
+  // Tiles are numbered down the columns of tiles of an image (t -> image,
+  // tile column, tile row): a split's consecutive tiles are vertically
+  // adjacent, so the two halo rows a tile shares with its predecessor are
+  // still in L2 and each tile fetches TH new x rows from HBM instead of TH + 2
+  // (raster order revisited them a whole tile row = 16 tiles later, long
+  // evicted: the 512^2 64-channel launch read 1.5x its algorithmic bytes).
+  const int tiles_h = H / TH;
   // tile walk counters (FAST): image, tile row, tile column of the next stage
   int w_img = 0, w_ty = 0, w_tx = 0;
   if constexpr (FAST) {
     w_img = t_beg / tiles_img;
     const int tr = t_beg - w_img * tiles_img;
-    w_ty = tr / tiles_w;
-    w_tx = tr - w_ty * tiles_w;
+    w_tx = tr / tiles_h;
+    w_ty = tr - w_tx * tiles_h;
   }
-  const int tiles_h = H / TH;
 
   auto stage_fast = [&](int buf) {
     const int img = w_img, y0 = w_ty * TH, x0 = w_tx * TW;
-    if (++w_tx == tiles_w) {
-      w_tx = 0;
-      if (++w_ty == tiles_h) { w_ty = 0; ++w_img; }
+    if (++w_ty == tiles_h) {
+      w_ty = 0;
+      if (++w_tx == tiles_w) { w_tx = 0; ++w_img; }
     }
     char* Pb = smem + buf * STAGE;
     char* Qb = Pb + PB;
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(512, 1) void wgrad3x3_halo_kernel(VuGemmWgrad p) {
 
   auto stage = [&](int t, int buf) {
     const int img = t / tiles_img, tr = t - img * tiles_img;
-    const int y0 = (tr / tiles_w) * TH, x0 = (tr - (tr / tiles_w) * tiles_w) * TW;
+    const int y0 = (tr - (tr / tiles_h) * tiles_h) * TH, x0 = (tr / tiles_h) * TW;
     char* Pb = smem + buf * STAGE;
     char* Qb = Pb + PB;
     const bf16_t* dtile = dsrc + (((int64_t)img * H + y0) * W + x0) * dst_;

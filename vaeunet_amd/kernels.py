@@ -250,6 +250,7 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
 
 SPLIT_PIX = 4096
 SPLIT_MAX = 1024
+WGRAD_SPLIT_CAP = 0   # A/B runs (tools/enc_bench.py --wsplit): cap on the split-K ways, 0 = none
 
 
 def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
@@ -277,6 +278,8 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
         if eff > best[0] + 1e-9:
             best = (eff, s)
     splits = best[1]
+    if WGRAD_SPLIT_CAP > 0:
+        splits = min(splits, WGRAD_SPLIT_CAP)
     # v2 (1x1 / ConvT): very long pixel ranges per block (> SPLIT_PIX) expose
     # the ring's DMA latency on every step, so a second wave of blocks measured
     # faster (512^2 attention W_x gradient: 256 splits 158 us, 512 splits
