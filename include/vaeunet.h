@@ -214,8 +214,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     immediate-offset fragment reads and incremental tile addressing, 0 the
  *     round-3 loop, 2 the round-4 loop without s_setprio (A/B runs) */
 #define VU_TUNE_W3_FAST 26
-/*   VU_TUNE_PP_FULL: 1 = the ping-pong 3x3 kernel runs one read segment and
- *     one 32-MFMA segment per step (2 barriers) instead of two halves (A/B) */
+/*   VU_TUNE_PP_FULL: 1 (default) = the ping-pong 3x3 kernel runs one read
+ *     segment and one 32-MFMA segment per step (2 barriers) instead of two
+ *     halves (0; bit-identical outputs) */
 #define VU_TUNE_PP_FULL 27
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
@@ -668,6 +669,10 @@ int vu_latent_fwd(const VuLatentJob* jobs, int njobs, const float* z, int N, int
 int64_t vu_latent_part_floats(int N, int co);
 int vu_latent_bwd_sums(const VuLatentJob* jobs, int njobs, int N, int dtype, void* stream);
 int64_t vu_latent_bwd_workspace_bytes(int N, int L, int64_t sum_co);
+/* 1 when vu_latent_bwd serves N samples, latent size L, consumers with
+ * sum_co output channels in all and C encoder channels (its one-block
+ * working set fits in LDS), else 0 (the caller takes the map path) */
+int vu_latent_bwd_supported(int N, int L, int64_t sum_co, int C);
 /* one block: every consumer's BN / ReLU / conv backward on the vectors, dz,
  * reparameterize backward, both heads' backward -> dpooled */
 int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentHeads* heads, int N, int L,

@@ -292,7 +292,7 @@ def test_double_conv_fp8_delayed_scaling(up):
     torch.manual_seed(4)
     cins = [64, 64] if up else [64]
     mod = DoubleConv(sum(cins), 128).to(DEV)
-    xs = [_act(torch.randn(2, c, 32, 48).relu()) for c in cins]
+    xs = [_act(torch.randn(2, c, 32, 64).relu()) for c in cins]
     yj = fp8.double_conv_forward(mod, xs, delayed=False).float()
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         yb = mod(torch.cat(xs, 1)).float()
@@ -304,3 +304,24 @@ def test_double_conv_fp8_delayed_scaling(up):
         assert ds_in.t == step + 1
         assert ds_in.ring[ds_in.slot].item() == max(float(t.float().abs().max()) for t in xs)
         assert ds_mid.ring[ds_mid.slot].item() > 0
+
+
+def test_double_conv_fp8_chained():
+    """Chained fp8 blocks: an e4m3 input from the producer (x_q) and an e4m3
+    output (BN2 apply fused with the quantise, its own delayed scale): the
+    dequantised output is the bf16-output block's result up to one e4m3
+    rounding (relative step 2^-3 below 448, saturation above the stale amax),
+    every step."""
+    from vaeunet_amd import DoubleConv, fp8
+    torch.manual_seed(6)
+    mod = DoubleConv(64, 64).to(DEV)
+    x = _act(torch.randn(2, 64, 32, 64).relu())
+    ds = fp8.DelayedScale(DEV)
+    fp8.calibrate(x, None, False, ds)
+    xq, xdq = fp8.bn_apply_quant(x, None, False, ds)
+    for step in range(3):
+        ref = fp8.double_conv_forward(mod, [xq.float().mul(xdq).to(torch.bfloat16).contiguous(memory_format=CL)])
+        q, dq = fp8.double_conv_forward(mod, None, x_q=([xq], xdq), out_fp8=True)
+        got = q.float() * dq
+        err = (got - ref.float()).abs()
+        assert (err <= 2.0 ** -3 * ref.float().abs() + 1e-3 * ref.float().abs().max()).all(), step

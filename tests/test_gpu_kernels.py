@@ -263,7 +263,7 @@ def test_conv3x3_pingpong_full_phase(case):
         _tune((TUNE_PP_FULL, 1))
         _check_halo_conv(case, (128,))
     finally:
-        _tune(*TUNE_DEFAULTS, (TUNE_PP_FULL, 0))
+        _tune(*TUNE_DEFAULTS, (TUNE_PP_FULL, 1))
 
 
 @pytest.mark.parametrize("case", SPLITK_CASES)

@@ -7,8 +7,11 @@ the same shapes; error vs the unquantised fp32 conv reported per layer.
 --double: the DoubleConv blocks instead (conv -> BN -> ReLU, twice, train-mode
 BatchNorm), timed end to end INCLUDING every activation quantisation: the
 delayed-scaling fp8 path (fp8.double_conv_forward: one-pass input quantise,
-BN1 apply fused with the e4m3 quantise) and the just-in-time fp8 path
-against the bf16 engine path (engine.double_conv_fwd) on the same module.
+BN1 apply fused with the e4m3 quantise), the just-in-time fp8 path and the
+chained fp8 block (e4m3 in from the producing block, BN2 apply fused with
+the e4m3 quantise of the output: the steady state of consecutive fp8
+blocks) against the bf16 engine path (engine.double_conv_fwd) on the same
+module.
 
 usage: python tools/fp8_bench.py [--batch 2] [--reps 20] [--layers inc.2,...] [--double] [--json out.json]
 """
@@ -40,7 +43,7 @@ def double_main(args):
     from vaeunet_amd import engine as E
     dev = torch.device("cuda")
     B = args.batch
-    rows, tot = [], {"bf16": 0.0, "fp8": 0.0, "fp8_jit": 0.0, "fl": 0.0}
+    rows, tot = [], {"bf16": 0.0, "fp8": 0.0, "fp8_jit": 0.0, "fp8_chain": 0.0, "fl": 0.0}
     for name, cins, co, H in BLOCKS:
         if args.layers and name not in args.layers.split(","):
             continue
@@ -56,24 +59,37 @@ def double_main(args):
         msb = timeit(bf16, args.reps)
         ms8 = timeit(lambda: fp8.double_conv_forward(mod, srcs), args.reps)
         msj = timeit(lambda: fp8.double_conv_forward(mod, srcs, delayed=False), args.reps)
+        # chained: input already e4m3 (quantised by the producing block), output e4m3
+        xq = fp8.double_conv_forward(mod, srcs)  # (warm the scales)
+        dsq = fp8.DelayedScale(dev)
+        fp8.calibrate(srcs[0], None, False, dsq)
+        qin = [fp8.bn_apply_quant(t, None, False, dsq)[0] for t in srcs]
+        qdq = fp8.bn_apply_quant(srcs[0], None, False, dsq)[1]
+        del xq
+        msc = timeit(lambda: fp8.double_conv_forward(mod, None, x_q=(qin, qdq), out_fp8=True), args.reps)
         with torch.no_grad():
             yb = E.double_conv_fwd(M, mod.double_conv, srcs)[0].float()
             y8 = fp8.double_conv_forward(mod, srcs).float()
         row = {"block": name, "cin": ci, "cout": co, "hw": H, "bf16_us": round(msb * 1e3, 1),
                "fp8_us": round(ms8 * 1e3, 1), "fp8_jit_us": round(msj * 1e3, 1),
+               "fp8_chain_us": round(msc * 1e3, 1),
                "speedup": round(msb / ms8, 3), "speedup_jit": round(msb / msj, 3),
+               "speedup_chain": round(msb / msc, 3),
                "rel_err_vs_bf16": round(((y8 - yb).abs().max() / yb.abs().max()).item(), 4)}
         rows.append(row)
         print(json.dumps(row), flush=True)
         tot["bf16"] += msb
         tot["fp8"] += ms8
         tot["fp8_jit"] += msj
+        tot["fp8_chain"] += msc
         tot["fl"] += fl
         del srcs, mod
         torch.cuda.empty_cache()
     summ = {"batch": B, "image": "3x1024x1024", "blocks": len(rows), "bf16_ms": round(tot["bf16"], 3),
             "fp8_ms": round(tot["fp8"], 3), "fp8_jit_ms": round(tot["fp8_jit"], 3),
+            "fp8_chain_ms": round(tot["fp8_chain"], 3),
             "speedup": round(tot["bf16"] / tot["fp8"], 3), "speedup_jit": round(tot["bf16"] / tot["fp8_jit"], 3),
+            "speedup_chain": round(tot["bf16"] / tot["fp8_chain"], 3),
             "fp8_block_tflops": round(tot["fl"] / tot["fp8"] / 1e9, 1)}
     print("SUMMARY " + json.dumps(summ), flush=True)
     if args.json:

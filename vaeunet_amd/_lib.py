@@ -170,6 +170,7 @@ _SIGS = {
     "vu_latent_fwd_blocks": (_l, [_i, _i, _i]),
     "vu_latent_fwd": (_i, [_p, _i, _p, _i, _i, _i, _p]),
     "vu_latent_part_floats": (_l, [_i, _i]),
+    "vu_latent_bwd_supported": (_i, [_i, _i, _l, _i]),
     "vu_latent_bwd_sums": (_i, [_p, _i, _i, _i, _p]),
     "vu_latent_bwd_workspace_bytes": (_l, [_i, _i, _l]),
     "vu_latent_bwd": (_i, [_p, _i, C.POINTER(VuLatentHeads), _i, _i, _p, _p]),

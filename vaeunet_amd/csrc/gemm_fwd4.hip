@@ -674,7 +674,7 @@ bool tiles_ok(const VuGemmFwd& p) {
 
 int g_min_blocks = 256;  // vu_gemm_set_tuning(VU_TUNE_V4_MIN_BLOCKS, ...)
 int g_splitk = 1;        // vu_gemm_set_tuning(VU_TUNE_V4_SPLITK, ...): 0 off, 1 auto, k >= 2 forced
-int g_pp_full = 0;       // VU_TUNE_PP_FULL: one phase per step (conv3x3_pp_kernel FULL)
+int g_pp_full = 1;       // VU_TUNE_PP_FULL: one phase per step (conv3x3_pp_kernel FULL; 0 = two halves)
 
 // Output-column tile the ping-pong kernel uses for this problem (0 = not served).
 int pick_bn(const VuGemmFwd& p) {

@@ -36,6 +36,7 @@ constexpr int LAT_CG = 64;      // channels per vu_latent_fwd block
 constexpr int LAT_SPLITS = 32;  // pixel splits per sample of vu_latent_bwd_sums
 constexpr int LAT_MAXN = 64;    // samples
 constexpr int LAT_MAXJ = 8;     // consumers per launch
+#define VU_LATENT_BWD_MAX_LDS (64 * 1024)
 
 // the job table travels BY VALUE in the kernel arguments (~1.7 KB): no device
 // table to upload, so a captured HIP graph replays it as is
@@ -49,26 +50,47 @@ VU_DEV float wave_sum(float v) {
   return v;
 }
 
+// one block per (sample n, group of LAT_HG latent dims): the channel mean of
+// f[-1] for sample n (every group block recomputes it: 256 KB from L2 at the
+// bottleneck; group 0 writes it), then the 2 * LAT_HG head dot products of
+// its dims (one wave per dot, lanes over the C channels, weight loads
+// unrolled), then reparameterize for those dims.  (Round 4 first version:
+// one 256-thread block per sample with a serial 64-deep load chain and 16
+// serial dots per wave -- 72 us per step.)
+constexpr int LAT_HG = 8;     // latent dims per heads block
+constexpr int LAT_HT = 512;   // heads block threads
 template <typename T>
-__global__ __launch_bounds__(256) void heads_fwd_kernel(const T* f4, int64_t fs, int HW, int C, const float* w_mu,
-                                                        const float* b_mu, const float* w_lv, const float* b_lv, int L,
-                                                        const float* eps, float* pooled, float* mu, float* logvar,
-                                                        float* z) {
-  extern __shared__ float sm[];            // [4][C] partial sums, then pooled [C]
-  const int n = blockIdx.x, tid = threadIdx.x;
+__global__ __launch_bounds__(LAT_HT) void heads_fwd_kernel(const T* f4, int64_t fs, int HW, int C, const float* w_mu,
+                                                           const float* b_mu, const float* w_lv, const float* b_lv,
+                                                           int L, const float* eps, float* pooled, float* mu,
+                                                           float* logvar, float* z) {
+  extern __shared__ float sm[];            // [rows][C] partial sums, then pooled [C], then 2*LAT_HG head outputs
+  const int n = blockIdx.x, grp = blockIdx.y, tid = threadIdx.x;
   const int V = C >> 3;                    // 8-channel vectors per pixel (C % 8 == 0)
-  const int rows = 256 / V;                // pixel rows in flight per block (V <= 256)
+  const int rows = LAT_HT / V;             // pixel rows in flight per block (V <= LAT_HT)
   const int cv = tid % V, row = tid / V;
   float s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = 0.f;
-  if (row < rows)
-    for (int p = row; p < HW; p += rows) {
+  if (row < rows) {
+    const T* base = f4 + (int64_t)n * HW * fs + cv * 8;
+    int p = row;
+    for (; p + 3 * rows < HW; p += 4 * rows) {   // 4 loads in flight per thread
+      Vec8<T> v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u].load(base + (int64_t)(p + u * rows) * fs);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += v[u].get(k);
+    }
+    for (; p < HW; p += rows) {
       Vec8<T> v;
-      v.load(f4 + ((int64_t)n * HW + p) * fs + cv * 8);
+      v.load(base + (int64_t)p * fs);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v.get(k);
     }
+  }
   float* part = sm;                        // [rows][C]
   if (row < rows)
 #pragma unroll
@@ -76,35 +98,49 @@ __global__ __launch_bounds__(256) void heads_fwd_kernel(const T* f4, int64_t fs,
   __syncthreads();
   float* pm = sm + rows * C;               // pooled mean [C]
   const float inv = 1.f / (float)HW;
-  for (int c = tid; c < C; c += 256) {
+  for (int c = tid; c < C; c += LAT_HT) {
     float t = 0.f;
     for (int q = 0; q < rows; ++q) t += part[q * C + c];
     pm[c] = t * inv;
-    pooled[(int64_t)n * C + c] = t * inv;
+    if (grp == 0) pooled[(int64_t)n * C + c] = t * inv;
   }
   __syncthreads();
-  // heads: output o < L is mu[o], else logvar[o - L]; wave w takes o = w, w+4, ...
-  const int lane = tid & 63, wv = tid >> 6;
-  for (int o = wv; o < 2 * L; o += 4) {
-    const float* w = o < L ? w_mu + (int64_t)o * C : w_lv + (int64_t)(o - L) * C;
+  // dot d < 2*LAT_HG of this group: mu[l0 + d] (d < LAT_HG) or logvar[l0 + d - LAT_HG]; wave w takes d = w, w + 8
+  float* hout = pm + C;
+  const int lane = tid & 63, wv = tid >> 6, l0 = grp * LAT_HG;
+  for (int d = wv; d < 2 * LAT_HG; d += LAT_HT / 64) {
+    const int l = l0 + (d < LAT_HG ? d : d - LAT_HG);
+    if (l >= L) continue;                  // wave-uniform
+    const float* w = d < LAT_HG ? w_mu + (int64_t)l * C : w_lv + (int64_t)l * C;
     float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += w[c] * pm[c];
+    for (int c = lane; c < C; c += 256) {  // 4 loads in flight per lane
+      float wr[4], pr[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int cc = c + 64 * u;
+        wr[u] = cc < C ? w[cc] : 0.f;
+        pr[u] = cc < C ? pm[cc] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a += wr[u] * pr[u];
+    }
     a = wave_sum(a);
     if (lane == 0) {
-      if (o < L) {
-        a += b_mu ? b_mu[o] : 0.f;
-        mu[(int64_t)n * L + o] = a;
+      if (d < LAT_HG) {
+        a += b_mu ? b_mu[l] : 0.f;
+        mu[(int64_t)n * L + l] = a;
       } else {
-        a += b_lv ? b_lv[o - L] : 0.f;
-        logvar[(int64_t)n * L + o - L] = a;
+        a += b_lv ? b_lv[l] : 0.f;
+        logvar[(int64_t)n * L + l] = a;
       }
+      hout[d] = a;
     }
   }
   __syncthreads();
-  __threadfence_block();
-  for (int j = tid; j < L; j += 256) {
-    const float m = mu[(int64_t)n * L + j];
-    z[(int64_t)n * L + j] = eps ? m + eps[(int64_t)n * L + j] * expf(0.5f * logvar[(int64_t)n * L + j]) : m;
+  if (tid < LAT_HG && l0 + tid < L) {
+    const int l = l0 + tid;
+    const float m = hout[tid];
+    z[(int64_t)n * L + l] = eps ? m + eps[(int64_t)n * L + l] * expf(0.5f * hout[LAT_HG + tid]) : m;
   }
 }
 
@@ -214,13 +250,25 @@ __global__ __launch_bounds__(256) void latent_sums_kernel(const LatentJobs jobs,
   float s[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = 0.f;
-  if (row < rows)
-    for (int p = p0 + row; p < p1; p += rows) {
+  if (row < rows) {
+    const T* base = d + (int64_t)n * J.HW * J.dmap_stride + cv * 8;
+    int p = p0 + row;
+    for (; p + 3 * rows < p1; p += 4 * rows) {   // 4 loads in flight per thread
+      Vec8<T> v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u].load(base + (int64_t)(p + u * rows) * J.dmap_stride);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] += v[u].get(k);
+    }
+    for (; p < p1; p += rows) {
       Vec8<T> v;
-      v.load(d + ((int64_t)n * J.HW + p) * J.dmap_stride + cv * 8);
+      v.load(base + (int64_t)p * J.dmap_stride);
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v.get(k);
     }
+  }
   if (row < rows)
 #pragma unroll
     for (int k = 0; k < 8; ++k) sh[row * C + cv * 8 + k] = s[k];
@@ -232,113 +280,245 @@ __global__ __launch_bounds__(256) void latent_sums_kernel(const LatentJobs jobs,
   }
 }
 
-// one block: every consumer's backward on the vectors, then the bottleneck's
-__global__ __launch_bounds__(1024) void latent_bwd_kernel(const LatentJobs jobs, int njobs, VuLatentHeads hb,
-                                                          int N, int L, float* ws) {
-  // ws: DY [sum_j N * co_j] floats, then dz [N][L], dmu [N][L], dlv [N][L]
-  const int tid = threadIdx.x;
-  int64_t off = 0;
-  for (int j = 0; j < njobs; ++j) {
+// One block (1024 threads): every consumer's backward on the vectors, then
+// the bottleneck's.  The work is ~1 MFLOP; what costs is latency, so every
+// phase runs its global loads in parallel across the block and keeps the
+// intermediate vectors in LDS (the first version walked 256-512-long
+// dependent global-load chains per thread: 510 us per step).  LDS (floats):
+//   sdy [N][CT]   map-gradient sums, then the consumers' pre-BN gradients
+//                 (CT = sum of co over the consumers, job j at column off_j)
+//   sz, sdmu, sdlv [N][L]
+//   su            [max(16 N L, N C)]: the dz partials of the 16 waves, then
+//                 pooled [N][C]
+// All sums run in a fixed order (reproducible).
+constexpr int LAT_BT = 1024;
+constexpr int LAT_RMW = 8;    // gradient elements per thread per round (phases 3a, 4)
+
+__host__ __device__ inline int64_t latent_bwd_lds_floats(int N, int L, int CT, int C) {
+  const int64_t u = (int64_t)16 * N * L > (int64_t)N * C ? (int64_t)16 * N * L : (int64_t)N * C;
+  return (int64_t)N * CT + 3LL * N * L + u;
+}
+
+__global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs jobs, int njobs, VuLatentHeads hb,
+                                                            int N, int L, float* ws) {
+  (void)ws;
+  extern __shared__ float lsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int joff[LAT_MAXJ + 1];
+  joff[0] = 0;
+  for (int j = 0; j < njobs; ++j) joff[j + 1] = joff[j] + jobs.j[j].co;
+  const int CT = joff[njobs];
+  const int C = hb.C;
+  float* sdy = lsm;
+  float* sz = sdy + (int64_t)N * CT;
+  float* sdmu = sz + N * L;
+  float* sdlv = sdmu + N * L;
+  float* su = sdlv + N * L;
+
+  // phase 1: map-gradient sums S[n][c] = sum over the LAT_SPLITS partials
+  // (all 32 loads of a thread in flight), z -> LDS
+  for (int e = tid; e < N * CT; e += LAT_BT) {
+    const int n = e / CT, cc = e - n * CT;
+    int j = 0;
+    while (j + 1 < njobs && cc >= joff[j + 1]) ++j;
     const VuLatentJob& J = jobs.j[j];
-    float* DY = ws + off;
-    off += (int64_t)N * J.co;
-    const float rM = 1.f / (float)N;   // HW / (N * HW)
-    for (int c = tid; c < J.co; c += 1024) {
-      const float scale = J.coef[c], shift = J.coef[J.co + c], mean = J.coef[2 * J.co + c],
-                  invstd = J.coef[3 * J.co + c];
-      double db = 0.0, dg = 0.0;
-      for (int n = 0; n < N; ++n) {
-        float S = 0.f;
-        for (int s = 0; s < LAT_SPLITS; ++s) S += J.part[((int64_t)n * LAT_SPLITS + s) * J.co + c];
-        const float y = J.y[(int64_t)n * J.co + c];
-        const float G = (y * scale + shift > 0.f) ? S : 0.f;
-        DY[(int64_t)n * J.co + c] = G;
+    const int c = cc - joff[j];
+    const float* pp = J.part + (int64_t)n * LAT_SPLITS * J.co + c;
+    float v[LAT_SPLITS];
+#pragma unroll
+    for (int q = 0; q < LAT_SPLITS; ++q) v[q] = pp[(int64_t)q * J.co];
+    float S = 0.f;
+#pragma unroll
+    for (int q = 0; q < LAT_SPLITS; ++q) S += v[q];
+    sdy[e] = S;
+  }
+  for (int e = tid; e < N * L; e += LAT_BT) sz[e] = hb.z[e];
+  __syncthreads();
+
+  // phase 2: BatchNorm (+ReLU) backward per consumer channel on the N vectors
+  for (int cc = tid; cc < CT; cc += LAT_BT) {
+    int j = 0;
+    while (j + 1 < njobs && cc >= joff[j + 1]) ++j;
+    const VuLatentJob& J = jobs.j[j];
+    const int c = cc - joff[j];
+    const float scale = J.coef[c], shift = J.coef[J.co + c], mean = J.coef[2 * J.co + c],
+                invstd = J.coef[3 * J.co + c];
+    float yv[LAT_MAXN > 16 ? 16 : LAT_MAXN];
+    double db = 0.0, dg = 0.0;
+    for (int n0 = 0; n0 < N; n0 += 16) {
+      const int nn = N - n0 < 16 ? N - n0 : 16;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * J.co + c];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (k >= nn) break;
+        const int n = n0 + k;
+        const float y = yv[k];
+        const float G = (y * scale + shift > 0.f) ? sdy[n * CT + cc] : 0.f;
+        sdy[n * CT + cc] = G;
         db += G;
         dg += (double)G * ((y - mean) * invstd);
       }
-      if (J.dgamma) J.dgamma[c] = J.grad_acc ? J.dgamma[c] + (float)dg : (float)dg;
-      if (J.dbeta) J.dbeta[c] = J.grad_acc ? J.dbeta[c] + (float)db : (float)db;
-      const float gi = J.gamma[c] * invstd;
-      double dbias = 0.0;
-      for (int n = 0; n < N; ++n) {
-        const float y = J.y[(int64_t)n * J.co + c];
-        const float G = DY[(int64_t)n * J.co + c];
-        const float v = J.train ? gi * (G - rM * ((float)db + (y - mean) * invstd * (float)dg)) : gi * G;
-        DY[(int64_t)n * J.co + c] = v;
-        dbias += v;
-      }
-      // the conv bias of a train-mode BatchNorm has an exactly zero gradient
-      // (the batch mean absorbs it; engine.bias_grad)
-      if (J.dbias) {
-        const float b = J.train ? 0.f : (float)dbias;
-        J.dbias[c] = J.grad_acc ? J.dbias[c] + b : b;
-      }
+    }
+    if (J.dgamma) J.dgamma[c] = J.grad_acc ? J.dgamma[c] + (float)dg : (float)dg;
+    if (J.dbeta) J.dbeta[c] = J.grad_acc ? J.dbeta[c] + (float)db : (float)db;
+    const float gi = J.gamma[c] * invstd;
+    const float rM = 1.f / (float)N;   // HW / (N * HW)
+    double dbias = 0.0;
+    for (int n = 0; n < N; ++n) {
+      const float y = J.y[(int64_t)n * J.co + c];
+      const float G = sdy[n * CT + cc];
+      const float v = J.train ? gi * (G - rM * ((float)db + (y - mean) * invstd * (float)dg)) : gi * G;
+      sdy[n * CT + cc] = v;
+      dbias += v;
+    }
+    // the conv bias of a train-mode BatchNorm has an exactly zero gradient
+    // (the batch mean absorbs it; engine.bias_grad)
+    if (J.dbias) {
+      const float b = J.train ? 0.f : (float)dbias;
+      J.dbias[c] = J.grad_acc ? J.dbias[c] + b : b;
     }
   }
   __syncthreads();
-  // conv weight gradients: dW[co][l] (+)= sum_n DY[n][co] z[n][l]
-  off = 0;
-  for (int j = 0; j < njobs; ++j) {
-    const VuLatentJob& J = jobs.j[j];
-    const float* DY = ws + off;
-    off += (int64_t)N * J.co;
-    if (!J.dw) continue;
-    for (int e = tid; e < J.co * L; e += 1024) {
-      const int c = e / L, l = e - c * L;
-      float s = 0.f;
-      for (int n = 0; n < N; ++n) s += DY[(int64_t)n * J.co + c] * hb.z[(int64_t)n * L + l];
-      J.dw[e] = J.grad_acc ? J.dw[e] + s : s;
+
+  // phase 3a: conv weight gradients dW_j[c][l] (+)= sum_n DY[n][c] z[n][l];
+  // LAT_RMW elements per thread per round so that the read-modify-write
+  // loads of a round are in flight together
+  for (int e0 = tid; e0 < CT * L; e0 += LAT_RMW * LAT_BT) {
+    float* dst[LAT_RMW];
+    float old[LAT_RMW], s[LAT_RMW];
+#pragma unroll
+    for (int u = 0; u < LAT_RMW; ++u) {
+      const int e = e0 + u * LAT_BT;
+      dst[u] = nullptr;
+      old[u] = 0.f;
+      s[u] = 0.f;
+      if (e >= CT * L) continue;
+      const int cc = e / L, l = e - cc * L;
+      int j = 0;
+      while (j + 1 < njobs && cc >= joff[j + 1]) ++j;
+      const VuLatentJob& J = jobs.j[j];
+      if (!J.dw) continue;
+      dst[u] = J.dw + (int64_t)(cc - joff[j]) * L + l;
+      if (J.grad_acc) old[u] = *dst[u];
+      for (int n = 0; n < N; ++n) s[u] += sdy[n * CT + cc] * sz[n * L + l];
+    }
+#pragma unroll
+    for (int u = 0; u < LAT_RMW; ++u)
+      if (dst[u]) *dst[u] = old[u] + s[u];
+  }
+  // phase 3b: dz[n][l] = sum_j sum_c W_j[c][l] DY_j[n][c]: wave w takes the
+  // channel slice [w CT/16, (w+1) CT/16), lane = (n-half, l) over 32 l; the
+  // 16 wave partials are summed in wave order
+  const int nw = LAT_BT / 64;
+  const int cb = (int)((int64_t)wv * CT / nw), ce = (int)((int64_t)(wv + 1) * CT / nw);
+  const int nh = lane >> 5;
+  for (int l0 = 0; l0 < L; l0 += 32)
+  for (int n0 = 0; n0 < N; n0 += 8) {       // 8 samples x 32 dims per pass: 4 accumulators per lane
+    const int l = l0 + (lane & 31);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (l < L) {
+      for (int cc0 = cb; cc0 < ce; cc0 += 8) {   // 8 weight loads in flight per lane
+        float wcl[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int cc = cc0 + u;
+          wcl[u] = 0.f;
+          if (cc < ce) {
+            int j = 0;
+            while (j + 1 < njobs && cc >= joff[j + 1]) ++j;
+            wcl[u] = jobs.j[j].w[(int64_t)(cc - joff[j]) * L + l];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (cc0 + u >= ce) break;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int n = n0 + 2 * k + nh;
+            if (n < N) acc[k] += wcl[u] * sdy[n * CT + cc0 + u];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int n = n0 + 2 * k + nh;
+      if (n < N && l < L) su[((int64_t)wv * N + n) * L + l] = acc[k];
     }
   }
-  // dz[n][l] = sum_j sum_co W_j[co][l] DY_j[n][co]
-  float* dz = ws + off;
-  float* dmu = dz + N * L;
-  float* dlv = dmu + N * L;
-  for (int e = tid; e < N * L; e += 1024) {
-    const int n = e / L, l = e - n * L;
+  __syncthreads();
+  for (int e = tid; e < N * L; e += LAT_BT) {
     float s = hb.dz_in ? hb.dz_in[e] : 0.f;
-    int64_t o2 = 0;
-    for (int j = 0; j < njobs; ++j) {
-      const VuLatentJob& J = jobs.j[j];
-      const float* DY = ws + o2;
-      o2 += (int64_t)N * J.co;
-      for (int c = 0; c < J.co; ++c) s += J.w[(int64_t)c * L + l] * DY[(int64_t)n * J.co + c];
-    }
-    dz[e] = s;
+    for (int w = 0; w < nw; ++w) s += su[(int64_t)w * N * L + e];
     // reparameterize backward (unet_resnet.py:191-194): z = mu + eps * exp(lv / 2)
     const float gm = hb.dmu_in ? hb.dmu_in[e] : 0.f;
     const float gl = hb.dlv_in ? hb.dlv_in[e] : 0.f;
-    dmu[e] = gm + s;
-    dlv[e] = gl + (hb.eps ? s * hb.eps[e] * 0.5f * expf(0.5f * hb.logvar[e]) : 0.f);
+    sdmu[e] = gm + s;
+    sdlv[e] = gl + (hb.eps ? s * hb.eps[e] * 0.5f * expf(0.5f * hb.logvar[e]) : 0.f);
   }
   __syncthreads();
-  // heads: dW[j][c] (+)= sum_n d[n][j] pooled[n][c]; db[j] (+)= sum_n d[n][j]
-  const int C = hb.C;
-  for (int e = tid; e < 2 * L * C; e += 1024) {
-    const int h = e / (L * C), r = e - h * (L * C), jj = r / C, c = r - jj * C;
-    const float* d = h ? dlv : dmu;
-    float* dw = h ? hb.dw_lv : hb.dw_mu;
-    if (!dw) continue;
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += d[n * L + jj] * hb.pooled[(int64_t)n * C + c];
-    dw[r] = hb.grad_acc ? dw[r] + s : s;
+  // pooled -> LDS (over the dz partials)
+  float* spool = su;
+  for (int e = tid; e < N * C; e += LAT_BT) spool[e] = hb.pooled[e];
+  __syncthreads();
+
+  // phase 4: heads. dW[jj][c] (+)= sum_n d[n][jj] pooled[n][c]; db[jj] (+)= sum_n d[n][jj]
+  for (int e0 = tid; e0 < 2 * L * C; e0 += LAT_RMW * LAT_BT) {
+    float* dst[LAT_RMW];
+    float old[LAT_RMW], s[LAT_RMW];
+#pragma unroll
+    for (int u = 0; u < LAT_RMW; ++u) {
+      const int e = e0 + u * LAT_BT;
+      dst[u] = nullptr;
+      old[u] = 0.f;
+      s[u] = 0.f;
+      if (e >= 2 * L * C) continue;
+      const int h = e / (L * C), r = e - h * (L * C), jj = r / C, c = r - jj * C;
+      const float* d = h ? sdlv : sdmu;
+      float* dw = h ? hb.dw_lv : hb.dw_mu;
+      if (!dw) continue;
+      dst[u] = dw + r;
+      if (hb.grad_acc) old[u] = dw[r];
+      for (int n = 0; n < N; ++n) s[u] += d[n * L + jj] * spool[n * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < LAT_RMW; ++u)
+      if (dst[u]) *dst[u] = old[u] + s[u];
   }
-  for (int e = tid; e < 2 * L; e += 1024) {
+  for (int e = tid; e < 2 * L; e += LAT_BT) {
     const int h = e / L, jj = e - h * L;
-    const float* d = h ? dlv : dmu;
+    const float* d = h ? sdlv : sdmu;
     float* db = h ? hb.db_lv : hb.db_mu;
     if (!db) continue;
     float s = 0.f;
     for (int n = 0; n < N; ++n) s += d[n * L + jj];
     db[jj] = hb.grad_acc ? db[jj] + s : s;
   }
-  // dpooled[n][c] = sum_j w_mu[j][c] dmu[n][j] + w_lv[j][c] dlv[n][j]
-  for (int e = tid; e < N * C; e += 1024) {
-    const int n = e / C, c = e - n * C;
-    float s = 0.f;
-    for (int jj = 0; jj < L; ++jj)
-      s += hb.w_mu[(int64_t)jj * C + c] * dmu[n * L + jj] + hb.w_lv[(int64_t)jj * C + c] * dlv[n * L + jj];
-    hb.dpooled[e] = s;
+  // dpooled[n][c] = sum_jj w_mu[jj][c] dmu[n][jj] + w_lv[jj][c] dlv[n][jj]:
+  // a thread per (c, 8-sample group), the 2L weight loads in flight in 8s
+  for (int e = tid; e < C * ((N + 7) / 8); e += LAT_BT) {
+    const int c = e % C, n0 = (e / C) * 8;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j0 = 0; j0 < L; j0 += 8) {
+      float wm[8], wl[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        wm[u] = j0 + u < L ? hb.w_mu[(int64_t)(j0 + u) * C + c] : 0.f;
+        wl[u] = j0 + u < L ? hb.w_lv[(int64_t)(j0 + u) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (j0 + u >= L) break;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (n0 + k < N) acc[k] += wm[u] * sdmu[(n0 + k) * L + j0 + u] + wl[u] * sdlv[(n0 + k) * L + j0 + u];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (n0 + k < N) hb.dpooled[(int64_t)(n0 + k) * C + c] = acc[k];
   }
 }
 
@@ -354,12 +534,14 @@ extern "C" int vu_vae_heads_fwd(const void* f4, int64_t fs, int N, int HW, int C
                                 float* pooled, float* mu, float* logvar, float* z, int dtype, void* stream) {
   if (!pow2_ok(C) || fs % 8 || L < 1) return (int)hipErrorInvalidValue;
   if (N == 0) return 0;
-  const int rows = 256 / (C / 8);
-  const size_t shm = (size_t)(rows + 1) * C * sizeof(float);
+  const int rows = LAT_HT / (C / 8);
+  if (rows < 1) return (int)hipErrorInvalidValue;
+  const size_t shm = ((size_t)(rows + 1) * C + 2 * LAT_HG) * sizeof(float);
   if (shm > 64 * 1024) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)N, (unsigned)((L + LAT_HG - 1) / LAT_HG));
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((heads_fwd_kernel<T>), dim3(N), dim3(256), shm, st, (const T*)f4, fs, HW, C, w_mu, b_mu, w_lv,
+    hipLaunchKernelGGL((heads_fwd_kernel<T>), grid, dim3(LAT_HT), shm, st, (const T*)f4, fs, HW, C, w_mu, b_mu, w_lv,
                        b_lv, L, eps, pooled, mu, logvar, z);
   })
   return (int)hipGetLastError();
@@ -407,6 +589,11 @@ extern "C" int vu_latent_fwd(const VuLatentJob* jobs, int njobs, const float* z,
 
 extern "C" int64_t vu_latent_part_floats(int N, int co) { return (int64_t)N * LAT_SPLITS * co; }
 
+extern "C" int vu_latent_bwd_supported(int N, int L, int64_t sum_co, int C) {
+  return N >= 1 && N <= LAT_MAXN && L >= 1 && L <= 64 && sum_co >= 0 &&
+         latent_bwd_lds_floats(N, L, (int)sum_co, C) * (int64_t)sizeof(float) <= VU_LATENT_BWD_MAX_LDS;
+}
+
 extern "C" int vu_latent_bwd_sums(const VuLatentJob* jobs, int njobs, int N, int dtype, void* stream) {
   if (N < 1 || N > LAT_MAXN) return (int)hipErrorInvalidValue;
   LatentJobs J;
@@ -435,7 +622,11 @@ extern "C" int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentH
   } else if (njobs < 0) {
     return (int)hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(latent_bwd_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, J, njobs, *heads, N, L,
-                     workspace);
+  int64_t ct = 0;
+  for (int j = 0; j < njobs; ++j) ct += J.j[j].co;
+  const int64_t shm = latent_bwd_lds_floats(N, L, (int)ct, heads->C) * (int64_t)sizeof(float);
+  if (shm > VU_LATENT_BWD_MAX_LDS) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(latent_bwd_kernel, dim3(1), dim3(LAT_BT), (size_t)shm, (hipStream_t)stream, J, njobs, *heads, N,
+                     L, workspace);
   return (int)hipGetLastError();
 }

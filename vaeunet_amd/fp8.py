@@ -175,13 +175,13 @@ def conv3x3_q(srcs, weight, bias=None, stats=False):
 def _site_scales(mod, device):
     ent = mod.__dict__.get("_vu_fp8_scales")
     if ent is None:
-        ent = (DelayedScale(device), DelayedScale(device))
+        ent = (DelayedScale(device), DelayedScale(device), DelayedScale(device))
         mod.__dict__["_vu_fp8_scales"] = ent
     return ent
 
 
 @torch.no_grad()
-def double_conv_forward(mod, x, delayed=True):
+def double_conv_forward(mod, x, delayed=True, x_q=None, out_fp8=False):
     """DoubleConv.forward (unet_parts.py:32-49) with both 3x3 convs in fp8:
     conv -> BatchNorm (batch statistics from the fp8 conv epilogue in train
     mode, running statistics in eval mode) -> ReLU, twice; bf16 NHWC out.
@@ -193,9 +193,15 @@ def double_conv_forward(mod, x, delayed=True):
     the input is quantised in one pass (no amax pass) and BN1 + ReLU is
     applied and quantised in the same pass (vu_bn_apply_fp8), so conv2's
     input is never stored in bf16.  delayed=False: just-in-time scaling
-    (amax pass + quantise pass of the bf16 BN1 output)."""
+    (amax pass + quantise pass of the bf16 BN1 output).
+
+    Chained fp8 blocks (delayed only): ``x_q = (e4m3 sources, dequant scale)``
+    is an input already quantised by the producing block, and
+    ``out_fp8=True`` applies BN2 + ReLU fused with the e4m3 quantisation of
+    the block's output (its own delayed scale) and returns ``(q, dq)`` --
+    the activations between fp8 blocks are then never stored in bf16."""
     conv1, bn1, _, conv2, bn2, _ = mod.double_conv
-    srcs = list(x) if isinstance(x, (list, tuple)) else [x]
+    srcs = list(x) if isinstance(x, (list, tuple)) else ([x] if x is not None else [])
     if not delayed:
         a = srcs
         for conv, bn in ((conv1, bn1), (conv2, bn2)):
@@ -205,14 +211,20 @@ def double_conv_forward(mod, x, delayed=True):
             K.bn_apply(y, out, coef, True, _lib.BF16)
             a = [out]
         return a[0]
-    ds_in, ds_mid = _site_scales(mod, srcs[0].device)
-    if ds_in.t == 0:
-        for t in srcs:               # every source first: they share the scale
-            calibrate(t, None, False, ds_in)
-    qs = []
-    for t in srcs:
-        q, xdq = bn_apply_quant(t, None, False, ds_in)
-        qs.append(q)
+    if x_q is not None:
+        qs, xdq = list(x_q[0]), x_q[1]
+        dev = qs[0].device
+    else:
+        dev = srcs[0].device
+    ds_in, ds_mid, ds_out = _site_scales(mod, dev)
+    if x_q is None:
+        if ds_in.t == 0:
+            for t in srcs:           # every source first: they share the scale
+                calibrate(t, None, False, ds_in)
+        qs = []
+        for t in srcs:
+            q, xdq = bn_apply_quant(t, None, False, ds_in)
+            qs.append(q)
     w1, s1 = quantize_weight(conv1.weight)
     y1, st1 = conv3x3(qs, xdq, w1, s1, conv1.out_channels, stats=bn1.training)
     coef1 = E.bn_coef(bn1, st1, conv1.out_channels)
@@ -222,8 +234,13 @@ def double_conv_forward(mod, x, delayed=True):
     w2, s2 = quantize_weight(conv2.weight)
     y2, st2 = conv3x3([aq], adq, w2, s2, conv2.out_channels, stats=bn2.training)
     coef2 = E.bn_coef(bn2, st2, conv2.out_channels)
-    out = torch.empty_like(y2)
-    K.bn_apply(y2, out, coef2, True, _lib.BF16)
-    ds_in.advance()
-    ds_mid.advance()
+    if out_fp8:
+        if ds_out.t == 0:
+            calibrate(y2, coef2, True, ds_out)
+        out = bn_apply_quant(y2, coef2, True, ds_out)
+    else:
+        out = torch.empty_like(y2)
+        K.bn_apply(y2, out, coef2, True, _lib.BF16)
+    for ds in (ds_in, ds_mid, ds_out):
+        ds.advance()
     return out

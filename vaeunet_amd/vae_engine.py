@@ -428,6 +428,9 @@ def latent_vectors_ok(M, model, N):
         return False
     seqs = ([model.z_initial] if model.use_bottleneck else []) + \
         [b.z_proj for b in model.decoder_blocks if b.use_latent]
+    sum_co = sum(s[0].out_channels for s in seqs)
+    if not K.query("vu_latent_bwd_supported", N, model.latent_dim, sum_co, c4):
+        return False
     return all(_consumer_ok(M, s) for s in seqs)
 
 
