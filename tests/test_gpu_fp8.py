@@ -300,7 +300,7 @@ def test_double_conv_fp8_delayed_scaling(up):
         yd = fp8.double_conv_forward(mod, xs).float()
         assert ((yd - yj).abs().max() / yj.abs().max()).item() < 0.03, step
         assert ((yd - yb).abs().max() / yb.abs().max()).item() < 0.15, step
-        ds_in, ds_mid = mod._vu_fp8_scales
+        ds_in, ds_mid, _ = mod._vu_fp8_scales
         assert ds_in.t == step + 1
         assert ds_in.ring[ds_in.slot].item() == max(float(t.float().abs().max()) for t in xs)
         assert ds_mid.ring[ds_mid.slot].item() > 0
@@ -320,7 +320,7 @@ def test_double_conv_fp8_chained():
     fp8.calibrate(x, None, False, ds)
     xq, xdq = fp8.bn_apply_quant(x, None, False, ds)
     for step in range(3):
-        ref = fp8.double_conv_forward(mod, [xq.float().mul(xdq).to(torch.bfloat16).contiguous(memory_format=CL)])
+        ref = fp8.double_conv_forward(mod, None, x_q=([xq], xdq))          # same input, bf16 output
         q, dq = fp8.double_conv_forward(mod, None, x_q=([xq], xdq), out_fp8=True)
         got = q.float() * dq
         err = (got - ref.float()).abs()

@@ -213,6 +213,9 @@ def test_attn_gate_ops_vs_torch():
         if i in (1, 5):   # conv biases feeding a train-mode BN: exactly zero here, rounding noise in torch
             assert float(a.grad.abs().max()) == 0.0 and float(b_.grad.abs().max()) < 1e-5
             continue
+        if i == 9:        # the psi conv bias (also feeding a train-mode BN): zero up to fp32 summation noise
+            assert float(a.grad.abs().max()) < 1e-4 and float(b_.grad.abs().max()) < 1e-4
+            continue
         _close(a.grad, b_.grad, 1e-3, f"param {i}")
 
 

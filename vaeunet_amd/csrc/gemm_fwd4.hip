@@ -772,7 +772,10 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
   if (!p.workspace) return (int)hipErrorInvalidValue;
   VuGemmFwd q = p;
   q.ksplit = ks;
-  hipLaunchKernelGGL((conv3x3_pp_kernel<BN, true, false>), grid, dim3(512), 0, st, q);
+  if (BN == 256 && g_pp_full)  // (the 128-column split variant spills with the extra fragments)
+    hipLaunchKernelGGL((conv3x3_pp_kernel<BN, true, false, false, BN == 256>), grid, dim3(512), 0, st, q);
+  else
+    hipLaunchKernelGGL((conv3x3_pp_kernel<BN, true, false>), grid, dim3(512), 0, st, q);
   const int64_t M = (int64_t)g.N * g.H * g.W;
   hipLaunchKernelGGL(splitk_finish_kernel, dim3((unsigned)((M / 128) * (p.ncol / 64))), dim3(256), 0, st, q);
   return (int)hipGetLastError();

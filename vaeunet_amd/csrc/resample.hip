@@ -429,6 +429,40 @@ __global__ void permute4_batch_kernel(const VuPermJob* jobs, int n) {
     if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
     else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
   };
+  if (j.q == 4) {
+    // 3x3 (or smaller) conv weight image: dims 1 and 2 merge into one tap dim
+    // of T = d1*d2 <= 9 (input stride s2; s1 == d2*s2), and the tap dim
+    // forms one contiguous input run with dim 0 (|s0| == T*|s2|, the input-
+    // gradient image) or with dim 3 (|s3| == T*|s2|, the forward image).  A
+    // block moves a 32 x T x 32 (dim 0 x tap x dim 3) tile: reads in runs of
+    // 32*T contiguous floats, writes 32-element rows of dim 3.
+    __shared__ float big[32 * 9 * 33];
+    const int T = d[1] * d[2];
+    const int sT = st[2];
+    const bool run0 = j.s0 == (int64_t)T * (sT < 0 ? -sT : sT);   // dim 0 pairs with the taps
+    const uint32_t t0n = (d[0] + 31) / 32, t3n = (d[3] + 31) / 32;
+    const int a0 = (int)(blk / t3n) * 32, b0 = (int)(blk - (blk / t3n) * t3n) * 32;
+    (void)t0n;
+    const int n = 32 * T * 32;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int t = e % T, r = e / T;
+      const int x = r & 31, y = r >> 5;                 // x: the run dim, y: the other
+      const int a = run0 ? x : y, bb = run0 ? y : x;    // (dim 0, dim 3) offsets in the tile
+      float v = 0.f;
+      if (a0 + a < d[0] && b0 + bb < d[3] && b0 + bb < j.d3v)
+        v = in[(a0 + a) * st[0] + t * sT + (b0 + bb) * st[3]];
+      big[(a * T + t) * 33 + bb] = v;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+      const int bb = e & 31, r = e >> 5;                // r = a * T + t
+      const int a = r / T;
+      if (a0 + a >= d[0] || b0 + bb >= d[3]) continue;
+      const uint32_t o = ((uint32_t)(a0 + a) * T + (r - a * T)) * d[3] + b0 + bb;
+      put(o, big[r * 33 + bb]);
+    }
+    return;
+  }
   if (j.q >= 3) {
     const uint32_t d1 = d[1], d2 = d[2], d3 = d[3];
     const uint32_t tot = (uint32_t)d[0] * d1 * d2 * d3;

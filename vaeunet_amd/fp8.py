@@ -241,6 +241,8 @@ def double_conv_forward(mod, x, delayed=True, x_q=None, out_fp8=False):
     else:
         out = torch.empty_like(y2)
         K.bn_apply(y2, out, coef2, True, _lib.BF16)
-    for ds in (ds_in, ds_mid, ds_out):
-        ds.advance()
+    # a site's step counter counts its own quantisations
+    for ds, used in ((ds_in, x_q is None), (ds_mid, True), (ds_out, out_fp8)):
+        if used:
+            ds.advance()
     return out

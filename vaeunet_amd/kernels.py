@@ -367,6 +367,23 @@ class record_permutes:
         return False
 
 
+def perm_mode(strides, dims):
+    """vu_permute4_batch job mode: 3 = stream (output-fast dim is the
+    input-fast one), 0-2 = 32x32 tile transpose between that dim and dim 3,
+    4 = 3x3 weight image (dims 1, 2 merge into <= 9 taps forming one
+    contiguous input run with dim 0 or dim 3): 32 x T x 32 tile transpose."""
+    # input-fastest dim (among those of extent > 1); a transpose if not dim 3
+    cand = [k for k in range(4) if dims[k] > 1] or [3]
+    q = min(cand, key=lambda k: (abs(strides[k]), k != cand[-1]))
+    if q == cand[-1] or dims[3] == 1:
+        return 3  # output-fast == input-fast: stream
+    T = dims[1] * dims[2]
+    if (q in (1, 2) and dims[1] > 1 and dims[2] > 1 and T <= 9 and strides[1] == dims[2] * strides[2]
+            and abs(strides[2]) == 1 and T * abs(strides[2]) in (abs(strides[0]), abs(strides[3]))):
+        return 4
+    return q
+
+
 def job_table(jobs):
     """Device VuPermJob table of permute4 jobs -> (table tensor, total blocks)."""
     chunk = query("vu_permute4_chunk")
@@ -381,14 +398,12 @@ def job_table(jobs):
         e.d3v, e.dtype = d3v, dtype
         e.out = out.data_ptr()
         e.chunk0 = c0
-        # input-fastest dim (among those of extent > 1); a transpose if not dim 3
-        cand = [k for k in range(4) if dims[k] > 1] or [3]
-        q = min(cand, key=lambda k: (abs(strides[k]), k != cand[-1]))
-        if q == cand[-1] or dims[3] == 1:
-            q = 3  # output-fast == input-fast: stream
+        q = perm_mode(strides, dims)
         e.q = q
         if q == 3:
             c0 += -(-out.numel() // chunk)
+        elif q == 4:
+            c0 += (-(-dims[0] // 32)) * (-(-dims[3] // 32))
         else:
             a, cc = [k for k in range(3) if k != q]
             c0 += dims[a] * dims[cc] * (-(-dims[q] // 32)) * (-(-dims[3] // 32))
