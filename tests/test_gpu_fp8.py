@@ -151,7 +151,7 @@ def test_double_conv_fp8_close_to_bf16_path():
 TUNE_FP8_C64 = 23
 
 
-@pytest.mark.parametrize("shape", [(1, 1024, 1024), (2, 256, 512), (3, 256, 384)])
+@pytest.mark.parametrize("shape", [(1, 1024, 1024), (2, 256, 512), (3, 256, 384), (2, 256, 512, 2), (1, 512, 512, 1)])
 def test_conv3x3_fp8_c64_matches_step_loop(shape):
     """64 -> 64 fp8 conv on the resident-weight tile-stream kernel (default for
     these shapes; LDS-staged (2) and direct (1) output stores) vs the
@@ -159,20 +159,26 @@ def test_conv3x3_fp8_c64_matches_step_loop(shape):
     the same 32x32x64 MFMA fragments, so the bf16 outputs are bit-identical;
     the BN partials (64- vs 128-pixel tiles) combine to the same moments."""
     from vaeunet_amd import _lib, fp8
-    N, H, W = shape
+    # (N, H, W[, k]): k = 2 -> 128 input channels as two 64-channel sources,
+    # k = 1 -> one 128-channel source (the two-chunk resident-weight variant)
+    N, H, W = shape[:3]
+    cins = [64] if len(shape) == 3 else ([64, 64] if shape[3] == 2 else [128])
     g = torch.Generator().manual_seed(11)
-    x = torch.randn(N, 64, H, W, generator=g)
-    w = torch.randn(64, 64, 3, 3, generator=g) / 24.0
+    xs = [torch.randn(N, c, H, W, generator=g) for c in cins]
+    w = torch.randn(64, sum(cins), 3, 3, generator=g) / (3 * sum(cins) ** 0.5)
     b = torch.randn(64, generator=g)
-    xa = _act(x)
-    am = fp8.amax([xa])
-    q, dq = fp8.quantize(xa, am)
+    xa = [_act(x) for x in xs]
+    am = fp8.amax(xa)
+    qs = []
+    for t in xa:
+        q, dq = fp8.quantize(t, am)
+        qs.append(q)
     wq, ws = fp8.quantize_weight(w.to(DEV))
     res = {}
     for c64 in (2, 1, 0):
         _lib.call("vu_gemm_set_tuning", TUNE_FP8_C64, c64)
         try:
-            out, st = fp8.conv3x3([q], dq, wq, ws, 64, bias=b.to(DEV), stats=True)
+            out, st = fp8.conv3x3(qs, dq, wq, ws, 64, bias=b.to(DEV), stats=True)
             torch.cuda.synchronize()
             res[c64] = (out, st)
         finally:

@@ -787,20 +787,28 @@ constexpr int C64_NWR = (C64_WPIECES + 511) / 512;
 constexpr int C64_SP = 144, C64_STRIP = 32 * C64_SP;
 constexpr int C64_LDS = C64_WBYTES + 2 * C64_HALO + 2 * 64 * 4 + 8 * C64_STRIP;
 static_assert(C64_LDS <= 163840, "LDS");
+// NCH = 2 (round 4): 128 input channels (two 64-channel chunks, e.g. the
+// up4.1 concat of skip + upsampled sources) -> 64: both chunks' weights
+// resident (72 KiB), the (tile, chunk) steps share the halo double buffer,
+// direct stores (the staging strips do not fit beside the second chunk)
+template <int NCH, bool STG>
+constexpr int c64_lds() { return NCH * C64_WBYTES + 2 * C64_HALO + 2 * 64 * 4 + (STG ? 8 * C64_STRIP : 0); }
+static_assert(c64_lds<2, false>() <= 163840, "LDS");
 
 // STG: the bf16 output goes through a private LDS strip per wave and leaves
 // as whole 128-byte pixel rows (1 KiB contiguous per store instruction)
 // instead of 16-byte pieces at a 128-byte pixel stride
 // XM (A/B timing only, results wrong): 1 no MFMAs, 2 no loop halo DMA, 3 no output stores,
 // 4 no statistics
-template <bool STATS, bool STG, int XM = 0>
+template <bool STATS, bool STG, int XM = 0, int NCH = 1>
 __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
-  __shared__ __attribute__((aligned(16))) char smem[C64_LDS];
+  static_assert(NCH == 1 || !STG, "LDS: no staging strips beside two weight chunks");
+  __shared__ __attribute__((aligned(16))) char smem[c64_lds<NCH, STG>()];
   char* const wl = smem;
-  char* const hl0 = smem + C64_WBYTES;
-  float* const ssc = reinterpret_cast<float*>(smem + C64_WBYTES + 2 * C64_HALO);  // x_scale * w_scale[c]
-  float* const sbi = ssc + 64;                                                     // bias[c]
-  char* const strip = smem + C64_WBYTES + 2 * C64_HALO + 2 * 64 * 4 + (threadIdx.x >> 6) * C64_STRIP;
+  char* const hl0 = smem + NCH * C64_WBYTES;
+  float* const ssc = reinterpret_cast<float*>(smem + NCH * C64_WBYTES + 2 * C64_HALO);  // x_scale * w_scale[c]
+  float* const sbi = ssc + 64;                                                           // bias[c]
+  char* const strip = smem + NCH * C64_WBYTES + 2 * C64_HALO + 2 * 64 * 4 + (threadIdx.x >> 6) * C64_STRIP;
 
   const VuGather& g = p.a;
   const int H = g.H, W = g.W;
@@ -811,31 +819,42 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
   const int ntile_blk = (T - lb + G - 1) / G;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint8_t* const src = reinterpret_cast<const uint8_t*>(g.src[0]);
-  const int64_t st = g.stride[0];
+  // 64-channel chunk ch -> its source tensor and channel offset
+  auto chunk_src = [&](int ch, const uint8_t*& s, int64_t& stv) {
+    const int cb = 64 * ch;
+    const int q = (cb >= g.cend[0]) + (g.nsrc > 2 && cb >= g.cend[1]);
+    s = reinterpret_cast<const uint8_t*>(g.src[q]) + (cb - (q == 0 ? 0 : g.cend[q - 1]));
+    stv = g.stride[q];
+  };
   const void* const zp = (const void*)vu_zero_page8;
 
-  // resident weights: tap block t = 64 rows (output channels) of 64 bytes,
-  // piece q of row n holding logical piece q ^ ((n>>2)&3) (pswz)
+  // resident weights: chunk ch, tap block t = 64 rows (output channels) of 64
+  // bytes, piece q of row n holding logical piece q ^ ((n>>2)&3) (pswz)
   {
     const uint8_t* bm = reinterpret_cast<const uint8_t*>(p.w);
 #pragma unroll
-    for (int i = 0; i < C64_NWR; ++i) {
-      if (i * 512 + wid * 64 >= C64_WPIECES) continue;  // wave-uniform
-      const int s = i * 512 + tid;
-      const int tap = s >> 8, row = (s >> 2) & 63;
-      const void* gp = (const void*)(bm + (int64_t)row * p.ldw + tap * 64 + pswz(row, s & 3));
-      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(wl + (i * 512 + wid * 64) * 16), 16, 0, 0);
-    }
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int i = 0; i < C64_NWR; ++i) {
+        if (i * 512 + wid * 64 >= C64_WPIECES) continue;  // wave-uniform
+        const int s = i * 512 + tid;
+        const int tap = s >> 8, row = (s >> 2) & 63;
+        const void* gp = (const void*)(bm + (int64_t)row * p.ldw + tap * 64 * NCH + 64 * ch + pswz(row, s & 3));
+        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(wl + ch * C64_WBYTES + (i * 512 + wid * 64) * 16), 16, 0,
+                                         0);
+      }
   }
   if (tid < 64) {
     ssc[tid] = *p.x_scale * p.w_scale[tid];
     sbi[tid] = p.bias ? p.bias[tid] : 0.f;
   }
-  auto halo = [&](int t, int b) {
+  auto halo = [&](int t, int ch, int b) {
     const int img = t / per_img, r = t - (t / per_img) * per_img;
     const int ty = r / txn, tx = r - (r / txn) * txn;
     const int y0 = ty * C64_TH - 1, x0 = tx * C64_TW - 1;
+    const uint8_t* src;
+    int64_t st;
+    chunk_src(ch, src, st);
     const uint8_t* s0 = src + (int64_t)img * H * W * st;
     char* dst = hl0 + b * C64_HALO;
 #pragma unroll
@@ -853,7 +872,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
     }
   };
 
-  if (ntile_blk > 0) halo(lb, 0);
+  if (ntile_blk > 0) halo(lb, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -866,20 +885,27 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
 
   f32x16 acc[2][2];
   int t = lb, b = 0;
-  for (int ti = 0; ti < ntile_blk; ++ti, t += G) {
-    if (XM != 2 && ti + 1 < ntile_blk) halo(t + G, b ^ 1);
+  for (int ti = 0; ti < ntile_blk; ++ti, t += G)
+  for (int ch = 0; ch < NCH; ++ch) {
+    // the next (tile, chunk) step's halo lands in the other buffer meanwhile
+    if (XM != 2) {
+      if (ch + 1 < NCH) halo(t, ch + 1, b ^ 1);
+      else if (ti + 1 < ntile_blk) halo(t + G, 0, b ^ 1);
+    }
     const char* hb = hl0 + (XM == 2 ? 0 : b) * C64_HALO;
+    if (ch == 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    }
     // rolled: unrolled, the compiler hoists the nine taps' fragment reads
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int toff = (tap / 3) * C64_HW + tap % 3;
-      const char* wb = wl + tap * 4096;
+      const char* wb = wl + ch * C64_WBYTES + tap * 4096;
       i32x8 wf[2], pf[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) wf[j] = frag32(wb, wrow + 32 * j, hl);
@@ -893,6 +919,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
             acc[i][j][0] += __builtin_bit_cast(float, wf[j][0] ^ pf[i][1]);
           else
             acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[j], pf[i], acc[i][j], 0, 0, 0, 0, 0, 0);
+    }
+    if (NCH > 1 && ch + 1 < NCH) {
+      // more chunks of this tile: only the next step's halo is in flight
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();
+      b ^= 1;
+      continue;
     }
     // ---- epilogue: acc[i][j][r] = pixel (row 2*wid + i, column rho), channel cb16 + 32j + r
 #pragma unroll
@@ -992,6 +1025,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_fp8_c64_kernel(VuConvFp8 p) {
 
 int g_c64 = 2;  // VU_TUNE_FP8_C64: 2 (default) resident-weight kernel, staged stores; 1 direct stores; 0 off
 
+// 64-channel chunks the resident-weight kernel walks per tile (1 or 2), 0 = not served
+int c64_nch(const VuConvFp8& p) {
+  const VuGather& g = p.a;
+  if (!g_c64 || p.ncol != 64 || (g.C != 64 && g.C != 128)) return 0;
+  for (int t = 0; t < g.nsrc; ++t)
+    if (g.cend[t] % 64) return 0;
+  if (g.H % C64_TH != 0 || g.W % C64_TW != 0) return 0;
+  const int64_t T = (int64_t)g.N * (g.H / C64_TH) * (g.W / C64_TW);
+  if (T < 2 * (int64_t)cu_count()) return 0;  // a tile stream per block
+  return g.C / 64;
+}
+
 bool c64_ok(const VuConvFp8& p) {
   const VuGather& g = p.a;
   if (!g_c64 || g.nsrc != 1 || g.C != 64 || g.cend[0] != 64 || p.ncol != 64) return false;
@@ -1042,7 +1087,7 @@ int64_t bn_tiles(const VuConvFp8& p) {
 // channels, 129 -> 117 us; down4.1 with 512 would be 73 -> 87 us -- the slab
 // round trip costs more than the idle half of the chip there)
 int fp8_ksplit(const VuConvFp8& p) {
-  if (!g_split || !g_pp || g_grid != 0 || c64_ok(p)) return 1;
+  if (!g_split || !g_pp || g_grid != 0 || c64_nch(p)) return 1;
   const int bn = pick_bn(p);
   const int64_t tiles = bn == 256 ? bn_tiles<256>(p) : bn == 128 ? bn_tiles<128>(p) : bn_tiles<64>(p);
   const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
@@ -1296,7 +1341,7 @@ int conv_fp8_tune(int key, int value) {
 
 extern "C" int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args) {
   if (!served(*args)) return 0;
-  return c64_ok(*args) ? 64 : 128;
+  return c64_nch(*args) ? 64 : 128;
 }
 
 extern "C" int64_t vu_conv3x3_fp8_workspace_bytes(const VuConvFp8* args) {
@@ -1308,6 +1353,16 @@ extern "C" int64_t vu_conv3x3_fp8_workspace_bytes(const VuConvFp8* args) {
 extern "C" int vu_conv3x3_fp8(const VuConvFp8* args, void* stream) {
   if (!served(*args)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (c64_nch(*args) == 2) {
+    const VuGather& g = args->a;
+    const int64_t T = (int64_t)g.N * (g.H / C64_TH) * (g.W / C64_TW);
+    const int64_t grid = T < cu_count() ? T : cu_count();
+    if (args->stat_sum)
+      hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<true, false, 0, 2>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+    else
+      hipLaunchKernelGGL((conv3x3_fp8_c64_kernel<false, false, 0, 2>), dim3((unsigned)grid), dim3(512), 0, st, *args);
+    return (int)hipGetLastError();
+  }
   if (c64_ok(*args)) {
     const VuGather& g = args->a;
     const int64_t T = (int64_t)g.N * (g.H / C64_TH) * (g.W / C64_TW);

@@ -71,16 +71,11 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
     }
   };
 
-  // the first fragment's taps of a wave's next tile are loaded behind the
-  // current tile's last MFMAs, so only the first tile waits out a load
-  const int tstride = gridDim.x * (NT / 64);
-  u32x4 pf[3], pn[3];
-  int tile = blockIdx.x * (NT / 64) + wid;
-  if (tile < ntiles) load_px((tile / nct) * TP + r16, pf);
-  for (; tile < ntiles; tile += tstride) {
+  // (a cross-tile prefetch of the next tile's first fragment measured slower:
+  // its registers cost the third wave per SIMD, 88 -> 102 us)
+  for (int tile = blockIdx.x * (NT / 64) + wid; tile < ntiles; tile += gridDim.x * (NT / 64)) {
     const int mt = tile / nct, nt = tile - mt * nct;
     const int pb = mt * TP, n0 = nt * 64;
-    const int next = tile + tstride;
     if (nt != cur_nt) {
       cur_nt = nt;
 #pragma unroll
@@ -97,20 +92,21 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_image_kernel(VuGemmFwd p) {
     for (int i = 0; i < NF; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+    u32x4 pf[3], pn[3];
+    load_px(pb + r16, pf);
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
-      if (i + 1 < NF)
-        load_px(pb + (i + 1) * 16 + r16, pn);
-      else if (next < ntiles)
-        load_px((next / nct) * TP + r16, pn);
+      if (i + 1 < NF) load_px(pb + (i + 1) * 16 + r16, pn);
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[j][ks]),
                                                               __builtin_bit_cast(bf16x8, pf[ks]), acc[i][j], 0, 0, 0);
+      if (i + 1 < NF) {
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) pf[ks] = pn[ks];
+        for (int ks = 0; ks < 3; ++ks) pf[ks] = pn[ks];
+      }
     }
     // ---- epilogue: bias, bf16 rounding, BN partials, 16-byte stores
     const int c0 = n0 + cb16;

@@ -378,7 +378,7 @@ def perm_mode(strides, dims):
     if q == cand[-1] or dims[3] == 1:
         return 3  # output-fast == input-fast: stream
     T = dims[1] * dims[2]
-    if (q in (1, 2) and dims[1] > 1 and dims[2] > 1 and T <= 9 and strides[1] == dims[2] * strides[2]
+    if (q in (1, 2) and dims[1] > 1 and dims[2] > 1 and T in (4, 9) and strides[1] == dims[2] * strides[2]
             and abs(strides[2]) == 1 and T * abs(strides[2]) in (abs(strides[0]), abs(strides[3]))):
         return 4
     return q
