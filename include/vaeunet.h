@@ -308,6 +308,14 @@ typedef struct VuPermJob {
 int64_t vu_permute4_chunk(void);
 int vu_permute4_batch(const VuPermJob* jobs, int njobs, int64_t nchunks,
                       void* stream);
+/* Round 4: the same with the 3x3 / 2x2 weight images (q = 4: dims 1, 2
+ * merge into T = 9 or 4 taps that form one contiguous input run with dim 0
+ * or dim 3; 32 x T x 32 tile transpose, ceil(d0/32) * ceil(d3/32) blocks) in
+ * a launch of their own: jobs[0, ntap) are the q = 4 jobs (chunk0 prefix from
+ * 0, tap_blocks in all), jobs[ntap, njobs) the others (chunk0 prefix from 0
+ * again, rest_blocks in all). */
+int vu_permute4_batch2(const VuPermJob* jobs, int njobs, int ntap,
+                       int64_t tap_blocks, int64_t rest_blocks, void* stream);
 
 /* ---- BatchNorm (nn.BatchNorm2d train mode, unet_parts.py:41,44) -------- */
 /* combine per-tile (sum, M2) partials; counts: tile t has

@@ -451,25 +451,10 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
   const int st[4] = {(int)j.s0, (int)j.s1, (int)j.s2, (int)j.s3};
   const float* in = j.in + j.base;
   const uint32_t blk = (uint32_t)(chunk - j.chunk0);
-  __shared__ float big[32 * 9 * 33];
   auto put = [&](uint32_t e, float v) {
     if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
     else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
   };
-  if (j.q == 4) {
-    // 3x3 (or 2x2) conv weight image: dims 1 and 2 merge into one tap dim
-    // of T = d1*d2 (9 or 4; input stride s2, s1 == d2*s2), and the tap dim
-    // forms one contiguous input run with dim 0 (|s0| == T*|s2|, the input-
-    // gradient image) or with dim 3 (|s3| == T*|s2|, the forward image).  A
-    // block moves a 32 x T x 32 (dim 0 x tap x dim 3) tile: lanes read
-    // consecutive (run index, tap) elements, writes are 32-element rows of
-    // dim 3.  T is a template constant (the per-element divisions by it were
-    // runtime divisions: the first version was 2x slower than the 3 x 32 tiles
-    // it replaced).
-    if (d[1] * d[2] == 9) tap_tile<9>(j, in, d, st, blk, big, put);
-    else tap_tile<4>(j, in, d, st, blk, big, put);
-    return;
-  }
   if (j.q >= 3) {
     const uint32_t d1 = d[1], d2 = d[2], d3 = d[3];
     const uint32_t tot = (uint32_t)d[0] * d1 * d2 * d3;
@@ -513,9 +498,45 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
     put(e, tile[tx][ty + 8 * k]);
   }
 }
+// The 3x3 / 2x2 weight images (q = 4, see tap_tile) in a launch of their own:
+// the 38 KB tile would cap every block of the generic kernel at 4 per CU
+// (the first round-4 version, one kernel for all jobs, ran the refresh in
+// 287 us instead of 156).
+__global__ __launch_bounds__(256) void permute4_tap_kernel(const VuPermJob* jobs, int n) {
+  __shared__ float big[32 * 9 * 33];
+  const int64_t chunk = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].chunk0 <= chunk) lo = mid; else hi = mid - 1;
+  }
+  const VuPermJob& j = jobs[lo];
+  const int d[4] = {j.d0, j.d1, j.d2, j.d3};
+  const int st[4] = {(int)j.s0, (int)j.s1, (int)j.s2, (int)j.s3};
+  const float* in = j.in + j.base;
+  const uint32_t blk = (uint32_t)(chunk - j.chunk0);
+  auto put = [&](uint32_t e, float v) {
+    if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
+    else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
+  };
+  if (d[1] * d[2] == 9) tap_tile<9>(j, in, d, st, blk, big, put);
+  else tap_tile<4>(j, in, d, st, blk, big, put);
+}
 }  // namespace
 
 extern "C" int64_t vu_permute4_chunk(void) { return PERM_CHUNK; }
+
+extern "C" int vu_permute4_batch2(const VuPermJob* jobs, int njobs, int ntap, int64_t tap_blocks,
+                                  int64_t rest_blocks, void* stream) {
+  if (njobs < 0 || ntap < 0 || ntap > njobs) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (ntap > 0 && tap_blocks > 0)
+    hipLaunchKernelGGL(permute4_tap_kernel, dim3((unsigned)tap_blocks), dim3(256), 0, st, jobs, ntap);
+  if (njobs > ntap && rest_blocks > 0)
+    hipLaunchKernelGGL(permute4_batch_kernel, dim3((unsigned)rest_blocks), dim3(256), 0, st, jobs + ntap,
+                       njobs - ntap);
+  return (int)hipGetLastError();
+}
 
 extern "C" int vu_permute4_batch(const VuPermJob* jobs, int njobs, int64_t nchunks, void* stream) {
   if (njobs <= 0 || nchunks <= 0) return 0;

@@ -173,7 +173,7 @@ def _cached(p, key, build):
 
 class StaticRefresh:
     """Every derived weight image of ``params`` rebuilt IN PLACE by one
-    prebuilt vu_permute4_batch launch (no allocation, no host upload): what a
+    prebuilt vu_permute4_batch2 call (no allocation, no host upload): what a
     captured HIP graph of the training step replays at its start.  Built
     after a warm-up step, when every image the step uses exists."""
 
@@ -197,11 +197,11 @@ class StaticRefresh:
                     rec.jobs[n0] = (src, base, strides, dims, d3v, img.view(-1)[:out.numel()], dtype)
                     self.entries.append((p, cache, key))
         self.jobs = rec.jobs
-        self.table, self.nchunks = K.job_table(self.jobs) if self.jobs else (None, 0)
+        self.table, self.ntap, self.ctap, self.crest = K.job_table(self.jobs) if self.jobs else (None, 0, 0, 0)
 
     def launch(self):
         if self.jobs:
-            K.call("vu_permute4_batch", K.ptr(self.table), len(self.jobs), self.nchunks, K.stream())
+            K.permute_launch(self.table, len(self.jobs), self.ntap, self.ctap, self.crest)
         for p, cache, key in self.entries:
             cache[key] = ((p._version, p.data_ptr()), cache[key][1])
 

@@ -345,8 +345,8 @@ class permute_batch:
         jobs, _PBATCH = _PBATCH, None
         if not jobs or exc[0] is not None:
             return False
-        table, c0 = job_table(jobs)
-        call("vu_permute4_batch", ptr(table), len(jobs), c0, stream())
+        table, ntap, ctap, crest = job_table(jobs)
+        permute_launch(table, len(jobs), ntap, ctap, crest)
         return False
 
 
@@ -370,7 +370,7 @@ class record_permutes:
 def perm_mode(strides, dims):
     """vu_permute4_batch job mode: 3 = stream (output-fast dim is the
     input-fast one), 0-2 = 32x32 tile transpose between that dim and dim 3,
-    4 = 3x3 weight image (dims 1, 2 merge into <= 9 taps forming one
+    4 = 3x3 or 2x2 weight image (dims 1, 2 merge into 9 or 4 taps forming one
     contiguous input run with dim 0 or dim 3): 32 x T x 32 tile transpose."""
     # input-fastest dim (among those of extent > 1); a transpose if not dim 3
     cand = [k for k in range(4) if dims[k] > 1] or [3]
@@ -385,12 +385,21 @@ def perm_mode(strides, dims):
 
 
 def job_table(jobs):
-    """Device VuPermJob table of permute4 jobs -> (table tensor, total blocks)."""
+    """Device VuPermJob table of permute4 jobs for vu_permute4_batch2 ->
+    (table tensor, ntap, tap blocks, other blocks): the 3x3 / 2x2 weight
+    images (mode 4) first, each group with its own block prefix."""
     chunk = query("vu_permute4_chunk")
+    modes = [perm_mode(j[2], j[3]) for j in jobs]
+    order = [i for i in range(len(jobs)) if modes[i] == 4] + [i for i in range(len(jobs)) if modes[i] != 4]
+    ntap = sum(1 for m in modes if m == 4)
     arr = (_lib.VuPermJob * len(jobs))()
-    c0 = 0
-    for i, (src, base, strides, dims, d3v, out, dtype) in enumerate(jobs):
-        e = arr[i]
+    c0, ctap = 0, 0
+    for k, i in enumerate(order):
+        src, base, strides, dims, d3v, out, dtype = jobs[i]
+        q = modes[i]
+        if k == ntap:
+            ctap, c0 = c0, 0          # the other jobs' prefix restarts at 0
+        e = arr[k]
         e.inp = src.data_ptr()
         e.base = base
         e.s0, e.s1, e.s2, e.s3 = strides
@@ -398,18 +407,23 @@ def job_table(jobs):
         e.d3v, e.dtype = d3v, dtype
         e.out = out.data_ptr()
         e.chunk0 = c0
-        q = perm_mode(strides, dims)
         e.q = q
         if q == 3:
             c0 += -(-out.numel() // chunk)
         elif q == 4:
             c0 += (-(-dims[0] // 32)) * (-(-dims[3] // 32))
         else:
-            a, cc = [k for k in range(3) if k != q]
+            a, cc = [k2 for k2 in range(3) if k2 != q]
             c0 += dims[a] * dims[cc] * (-(-dims[q] // 32)) * (-(-dims[3] // 32))
+    if ntap == len(jobs):
+        ctap, c0 = c0, 0
     dev = jobs[0][5].device
     host = torch.frombuffer(bytearray(arr), dtype=torch.uint8).pin_memory()
-    return host.to(dev, non_blocking=True), c0
+    return host.to(dev, non_blocking=True), ntap, ctap, c0
+
+
+def permute_launch(table, njobs, ntap, ctap, crest):
+    call("vu_permute4_batch2", ptr(table), njobs, ntap, ctap, crest, stream())
 
 
 def bn_finalize(st, C_, gamma, beta, rmean, rvar, nbt, momentum, eps):
