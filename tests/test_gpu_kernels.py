@@ -911,18 +911,19 @@ def test_permute_batch_matches_single_launches():
     ws = [torch.randn(64, 32, 3, 3, generator=g).to(DEV), torch.randn(16, 8, 1, 1, generator=g).to(DEV),
           torch.randn(32, 16, 2, 2, generator=g).to(DEV),
           torch.randn(64, 3, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL),
-          torch.randn(72, 40, 3, 3, generator=g).to(DEV)]   # ragged 32-tiles of the tap-merged transpose
+          torch.randn(72, 40, 3, 3, generator=g).to(DEV),   # ragged 32-tiles of the tap-merged transpose
+          torch.randn(40, 24, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL)]  # converting copy
     for d in (0, 1):
         single = [E.w3x3_fwd(ws[0], d), E.w3x3_dgrad(ws[0], d), E.w1x1_fwd(ws[1], d), E.w1x1_dgrad(ws[1], d),
                   E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8),
-                  E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64)]
+                  E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64), E.w3x3_fwd(ws[5], d), E.w3x3_dgrad(ws[5], d)]
         single = [t.clone() for t in single]
         for w in ws:
             w.mul_(1.0)  # bump the version: every image is stale
         E.refresh_weights(ws)
         batched = [E.w3x3_fwd(ws[0], d), E.w3x3_dgrad(ws[0], d), E.w1x1_fwd(ws[1], d), E.w1x1_dgrad(ws[1], d),
                    E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8),
-                   E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64)]
+                   E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64), E.w3x3_fwd(ws[5], d), E.w3x3_dgrad(ws[5], d)]
         for a, b in zip(single, batched):
             assert torch.equal(a, b)
     # the round-4 tap-merged path is the one taken for the 3x3 images (and the ConvT input-gradient image)
@@ -932,8 +933,9 @@ def test_permute_batch_matches_single_launches():
             w.mul_(1.0)
         E.refresh_weights(ws)
         jobs = rec.jobs
-    modes = [K.perm_mode(j[2], j[3]) for j in jobs]
+    modes = [K.perm_mode(j[2], j[3], j[4]) for j in jobs]
     assert modes.count(4) >= 5, modes   # w3x3 fwd / dgrad of ws[0], ws[4] and the wT dgrad image
+    assert modes.count(5) >= 1, modes   # the channels_last weight's forward image without padding
 
 
 @pytest.mark.parametrize("case", [

@@ -98,11 +98,12 @@ struct SG {
   static constexpr int NJ = BN / 16;
   static constexpr int MAIN = 4 * HALO + NBW * SLOT;
   // epilogue: group 1's accumulators, 4 staging strips, BN statistics
-  static constexpr int RED = 4 * (2 * NJ * 4) * 64 * 4;
+  // epilogue (round 4): each of the 8 waves finalizes one 16-pixel fragment
+  static constexpr int RED = 8 * (NJ * 4) * 64 * 4;
   static constexpr int SPITCH = BN * 2 + 16;
-  static constexpr int STG = 32 * SPITCH;
-  static constexpr int STAT = 4 * BN * 2 * 4;
-  static constexpr int EPI = RED + 4 * STG + STAT;
+  static constexpr int STG = 16 * SPITCH;
+  static constexpr int STAT = 8 * BN * 2 * 4;
+  static constexpr int EPI = RED + 8 * STG + STAT;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
 };
 
@@ -267,7 +268,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
   } else {
     for (int s = 0; s < PD && s < S; ++s) wstage(0, s, s);  // PD <= 3: the tap rows of pair 0
   }
-  wait_vm<0>();
+  // group 0 waits for step 0's weights only (steps 1 .. PD-1 keep landing
+  // while step 0 runs; step 0's phase 1 waits for step 1 as every step does)
+  if (!grp && S >= PD) wait_vm<(PD - 1) * LB>();
+  else wait_vm<0>();
   sg_barrier();
   if (grp) sg_barrier();  // the stagger: group 1 runs one barrier behind
 
@@ -329,103 +333,85 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
   if (!grp) sg_barrier();  // re-align the groups
   __syncthreads();
 
-  // ---- sum the two K groups (group 1 -> LDS -> group 0) ---------------------
+  // ---- sum the two K groups; every wave finalizes one fragment -------------
+  // Wave (grp, q) owns fragment i = grp of its pixel quarter q and hands its
+  // partial of the other fragment to the partner wave (grp ^ 1, q): both
+  // groups share the epilogue (round 4: it was group 0's alone, group 1
+  // idling; part of v7's per-launch fixed cost).  The sums are the same two
+  // partials as before (fp32 addition commutes): bit-identical outputs.
   const __attribute__((address_space(4))) VuGemmFwd* ep =
       (const __attribute__((address_space(4))) VuGemmFwd*)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(ep));
   float* const red = reinterpret_cast<float*>(smem);
-  if (grp) {
+  const int w8 = grp * 4 + q, pw8 = (grp ^ 1) * 4 + q;
+  f32x4 mine[NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < NJ; ++j) {
+    const f32x4 o = grp ? acc[0][j] : acc[1][j];
+    mine[j] = grp ? acc[1][j] : acc[0][j];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((q * 2 * NJ + i * NJ + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+    for (int r = 0; r < 4; ++r) red[((w8 * NJ + j) * 4 + r) * 64 + lane] = o[r];
   }
   __syncthreads();
-  if (!grp) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((q * 2 * NJ + i * NJ + j) * 4 + r) * 64 + lane];
-  }
-  // pixel of fragment i of this wave (tile-relative row, column)
-  auto frag_pix = [&](int i, int& row, int& col) {
-    const int tp = (2 * q + i) * 16 + (lane & 15);
-    row = tp / TW;
-    col = tp - row * TW;
-  };
+    for (int r = 0; r < 4; ++r) mine[j][r] += red[((pw8 * NJ + j) * 4 + r) * 64 + lane];
+  // this wave's pixels: tile pixel (2q + grp) * 16 + (lane & 15)
+  const int tp0 = (2 * q + grp) * 16;
   const int cl = 4 * (lane >> 4);  // first of this lane's 4 channels in a 16-channel fragment
   if (SPLIT) {
-    if (!grp) {
-      const int64_t M = (int64_t)g.N * H * W;
-      float* const slab = ep->workspace + (int64_t)kidx * M * ep->ncol + n0 + cl;
+    const int64_t M = (int64_t)g.N * H * W;
+    float* const slab = ep->workspace + (int64_t)kidx * M * ep->ncol + n0 + cl;
+    const int tp = tp0 + (lane & 15), row = tp / TW, col = tp - (tp / TW) * TW;
+    float* const dst = slab + (((int64_t)img * H + y0 + row) * W + x0 + col) * ep->ncol;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        int row, col;
-        frag_pix(i, row, col);
-        float* const dst = slab + (((int64_t)img * H + y0 + row) * W + x0 + col) * ep->ncol;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) *reinterpret_cast<f32x4*>(dst + j * 16) = acc[i][j];
-      }
-    }
+    for (int j = 0; j < NJ; ++j) *reinterpret_cast<f32x4*>(dst + j * 16) = mine[j];
     return;
   }
-  __syncthreads();  // red[] consumed
-  char* const stg_base = smem + G::RED;
-  float* const stat = reinterpret_cast<float*>(smem + G::RED + 4 * G::STG);  // [4 waves][BN] sum, then m2
-  if (!grp) {
+  char* const stg = smem + G::RED + w8 * G::STG;
+  float* const stat = reinterpret_cast<float*>(smem + G::RED + 8 * G::STG);  // [8 waves][BN] sum, then m2
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float bv = ep->bias ? ep->bias[n0 + j * 16 + cl + r] : 0.f;
+      mine[j][r] = rnd<bf16_t>(mine[j][r] + bv);
+    }
+  if constexpr (RELU) epi_relu(mine);
+  if (ep->stat_sum) {
+    // per-wave (sum, centered M2) over its 16 pixels for every channel
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float bv = ep->bias ? ep->bias[n0 + j * 16 + cl + r] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i][j][r] = rnd<bf16_t>(acc[i][j][r] + bv);
-      }
-    if constexpr (RELU)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) epi_relu(acc[i]);
-    if (ep->stat_sum) {
-      // per-wave (sum, centered M2) over its 32 pixels for every channel
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float sv = row16_sum(acc[0][j][r] + acc[1][j][r]);
-          const float mean = sv * (1.f / 32);
-          const float d0 = acc[0][j][r] - mean, d1 = acc[1][j][r] - mean;
-          const float qv = row16_sum(d0 * d0 + d1 * d1);
-          if ((lane & 15) == 0) {
-            stat[q * BN + j * 16 + cl + r] = sv;
-            stat[(4 + q) * BN + j * 16 + cl + r] = qv;
-          }
+        const float sv = row16_sum(mine[j][r]);
+        const float d = mine[j][r] - sv * (1.f / 16);
+        const float qv = row16_sum(d * d);
+        if ((lane & 15) == 0) {
+          stat[w8 * BN + j * 16 + cl + r] = sv;
+          stat[(8 + w8) * BN + j * 16 + cl + r] = qv;
         }
-    }
-    // stage the wave's 32 pixels x BN channels (bf16) and store whole pixel rows
-    char* const stg = stg_base + q * G::STG;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        u32x2 v;
-        v[0] = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
-        v[1] = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
-        *reinterpret_cast<u32x2*>(stg + (i * 16 + (lane & 15)) * G::SPITCH + (j * 16 + cl) * 2) = v;
       }
   }
-  __syncthreads();
-  if (!grp) {
+  // stage the wave's 16 pixels x BN channels (bf16, a private strip) and
+  // store whole pixel rows
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    u32x2 v;
+    v[0] = (uint32_t)f2bf(mine[j][0]) | ((uint32_t)f2bf(mine[j][1]) << 16);
+    v[1] = (uint32_t)f2bf(mine[j][2]) | ((uint32_t)f2bf(mine[j][3]) << 16);
+    *reinterpret_cast<u32x2*>(stg + (lane & 15) * G::SPITCH + (j * 16 + cl) * 2) = v;
+  }
+  __syncthreads();   // the statistics of all eight waves (and each wave's strip) are in LDS
+  {
     constexpr int PPR = BN / 8;  // 16-byte pieces per pixel row
-    const char* const stg = stg_base + q * G::STG;
     bf16_t* const out = reinterpret_cast<bf16_t*>(ep->out) + ep->out_coff + n0;
 #pragma unroll
-    for (int e0 = 0; e0 < 32 * PPR; e0 += 64) {
+    for (int e0 = 0; e0 < 16 * PPR; e0 += 64) {
       const int e = e0 + lane;
       const int pl = e / PPR, pc = e - (e / PPR) * PPR;
-      const int tp = q * 32 + pl;
+      const int tp = tp0 + pl;
       const int row = tp / TW, col = tp - (tp / TW) * TW;
       u32x4 v = *reinterpret_cast<const u32x4*>(stg + pl * G::SPITCH + pc * 16);
       bf16_t* const dst = out + (((int64_t)img * H + y0 + row) * W + x0 + col) * ep->out_stride + pc * 8;
@@ -442,19 +428,19 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
     }
   }
   if (ep->stat_sum && tid < BN) {
-    // combine the four waves' 32-pixel statistics (Chan, fixed order)
-    float sw[4], tot = 0.f;
+    // combine the eight waves' 16-pixel statistics (Chan, fixed order)
+    float sw[8], tot = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < 8; ++w) {
       sw[w] = stat[w * BN + tid];
       tot += sw[w];
     }
     const float mean = tot * (1.f / 128);
     float m2 = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const float d = sw[w] * (1.f / 32) - mean;
-      m2 += stat[(4 + w) * BN + tid] + 32.f * d * d;
+    for (int w = 0; w < 8; ++w) {
+      const float d = sw[w] * (1.f / 16) - mean;
+      m2 += stat[(8 + w) * BN + tid] + 16.f * d * d;
     }
     ep->stat_sum[(int64_t)mt * ep->ncol + n0 + tid] = tot;
     ep->stat_m2[(int64_t)mt * ep->ncol + n0 + tid] = m2;

@@ -292,6 +292,18 @@ __global__ __launch_bounds__(256) void latent_sums_kernel(const LatentJobs jobs,
 //                 pooled [N][C]
 // All sums run in a fixed order (reproducible).
 constexpr int LAT_BT = 1024;
+struct LJob {   // the fields of a VuLatentJob the backward reads, in LDS
+  const float* part;
+  const float* coef;
+  const float* y;
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  float* dbias;
+  float* dw;
+  const float* w;
+  int co, grad_acc, train;
+};
 constexpr int LAT_RMW = 8;    // gradient elements per thread per round (phases 3a, 4)
 
 __host__ __device__ inline int64_t latent_bwd_lds_floats(int N, int L, int CT, int C) {
@@ -315,80 +327,94 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   float* sdlv = sdmu + N * L;
   float* su = sdlv + N * L;
 
-  // The job loops below are wave-uniform (a job's fields indexed by a
-  // per-lane job number would be per-lane loads from the kernel-argument
-  // segment, one dependent memory round trip before every address).
+  // The consumers' fields live in an LDS job table so that the loops below
+  // can run over the concatenated (job, channel) space -- all consumers'
+  // work in one round instead of one latency-bound round per consumer -- with
+  // a per-lane job lookup that costs an LDS read, not a per-lane load from
+  // the kernel-argument segment (one memory round trip before every address:
+  // the first version's 510 us).
+  __shared__ LJob lj[LAT_MAXJ];
+  __shared__ int loff[LAT_MAXJ + 1];
+  if (tid < njobs) {
+    const VuLatentJob& J = jobs.j[tid];
+    lj[tid] = LJob{J.part, J.coef, J.y, J.gamma, J.dgamma, J.dbeta, J.dbias, J.dw, J.w, J.co, J.grad_acc, J.train};
+  }
+  if (tid <= njobs) loff[tid] = joff[tid];
+  __syncthreads();
+  auto job_of = [&](int cc) {
+    int j = 0;
+    while (j + 1 < njobs && cc >= loff[j + 1]) ++j;
+    return j;
+  };
+
   // phase 1: map-gradient sums S[n][c] = sum over the LAT_SPLITS partials
   // (all 32 loads of a thread in flight), z -> LDS
-  for (int j = 0; j < njobs; ++j) {
-    const VuLatentJob& J = jobs.j[j];
-    const int co = J.co, o = joff[j];
-    for (int e = tid; e < N * co; e += LAT_BT) {
-      const int n = e / co, c = e - n * co;
-      const float* pp = J.part + (int64_t)n * LAT_SPLITS * co + c;
-      float v[LAT_SPLITS];
+  for (int e = tid; e < N * CT; e += LAT_BT) {
+    const int n = e / CT, cc = e - n * CT;
+    const int j = job_of(cc);
+    const int co = lj[j].co, c = cc - loff[j];
+    const float* pp = lj[j].part + (int64_t)n * LAT_SPLITS * co + c;
+    float v[LAT_SPLITS];
 #pragma unroll
-      for (int q = 0; q < LAT_SPLITS; ++q) v[q] = pp[(int64_t)q * co];
-      float S = 0.f;
+    for (int q = 0; q < LAT_SPLITS; ++q) v[q] = pp[(int64_t)q * co];
+    float S = 0.f;
 #pragma unroll
-      for (int q = 0; q < LAT_SPLITS; ++q) S += v[q];
-      sdy[n * CT + o + c] = S;
-    }
+    for (int q = 0; q < LAT_SPLITS; ++q) S += v[q];
+    sdy[e] = S;
   }
   for (int e = tid; e < N * L; e += LAT_BT) sz[e] = hb.z[e];
   __syncthreads();
 
   // phase 2: BatchNorm (+ReLU) backward per consumer channel on the N vectors
-  for (int j = 0; j < njobs; ++j) {
-    const VuLatentJob& J = jobs.j[j];
-    const int co = J.co, o = joff[j];
-    for (int c = tid; c < co; c += LAT_BT) {
-      const int cc = o + c;
-      const float scale = J.coef[c], shift = J.coef[co + c], mean = J.coef[2 * co + c], invstd = J.coef[3 * co + c];
-      float yv[16];
-      double db = 0.0, dg = 0.0;
-      for (int n0 = 0; n0 < N; n0 += 16) {
-        const int nn = N - n0 < 16 ? N - n0 : 16;
+  for (int cc = tid; cc < CT; cc += LAT_BT) {
+    const int j = job_of(cc);
+    const LJob& J = lj[j];
+    const int co = J.co, c = cc - loff[j];
+    const float scale = J.coef[c], shift = J.coef[co + c], mean = J.coef[2 * co + c], invstd = J.coef[3 * co + c];
+    const float gamma = J.gamma[c];
+    float yv[16];
+    double db = 0.0, dg = 0.0;
+    for (int n0 = 0; n0 < N; n0 += 16) {
+      const int nn = N - n0 < 16 ? N - n0 : 16;
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * co + c];
+      for (int k = 0; k < 16; ++k)
+        if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * co + c];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          if (k >= nn) break;
-          const int n = n0 + k;
-          const float y = yv[k];
-          const float G = (y * scale + shift > 0.f) ? sdy[n * CT + cc] : 0.f;
-          sdy[n * CT + cc] = G;
-          db += G;
-          dg += (double)G * ((y - mean) * invstd);
-        }
+      for (int k = 0; k < 16; ++k) {
+        if (k >= nn) break;
+        const int n = n0 + k;
+        const float y = yv[k];
+        const float G = (y * scale + shift > 0.f) ? sdy[n * CT + cc] : 0.f;
+        sdy[n * CT + cc] = G;
+        db += G;
+        dg += (double)G * ((y - mean) * invstd);
       }
-      if (J.dgamma) J.dgamma[c] = J.grad_acc ? J.dgamma[c] + (float)dg : (float)dg;
-      if (J.dbeta) J.dbeta[c] = J.grad_acc ? J.dbeta[c] + (float)db : (float)db;
-      const float gi = J.gamma[c] * invstd;
-      const float rM = 1.f / (float)N;   // HW / (N * HW)
-      double dbias = 0.0;
-      for (int n0 = 0; n0 < N; n0 += 16) {
-        const int nn = N - n0 < 16 ? N - n0 : 16;
+    }
+    if (J.dgamma) J.dgamma[c] = J.grad_acc ? J.dgamma[c] + (float)dg : (float)dg;
+    if (J.dbeta) J.dbeta[c] = J.grad_acc ? J.dbeta[c] + (float)db : (float)db;
+    const float gi = gamma * invstd;
+    const float rM = 1.f / (float)N;   // HW / (N * HW)
+    double dbias = 0.0;
+    for (int n0 = 0; n0 < N; n0 += 16) {
+      const int nn = N - n0 < 16 ? N - n0 : 16;
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * co + c];
+      for (int k = 0; k < 16; ++k)
+        if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * co + c];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          if (k >= nn) break;
-          const int n = n0 + k;
-          const float G = sdy[n * CT + cc];
-          const float v = J.train ? gi * (G - rM * ((float)db + (yv[k] - mean) * invstd * (float)dg)) : gi * G;
-          sdy[n * CT + cc] = v;
-          dbias += v;
-        }
+      for (int k = 0; k < 16; ++k) {
+        if (k >= nn) break;
+        const int n = n0 + k;
+        const float G = sdy[n * CT + cc];
+        const float v = J.train ? gi * (G - rM * ((float)db + (yv[k] - mean) * invstd * (float)dg)) : gi * G;
+        sdy[n * CT + cc] = v;
+        dbias += v;
       }
-      // the conv bias of a train-mode BatchNorm has an exactly zero gradient
-      // (the batch mean absorbs it; engine.bias_grad)
-      if (J.dbias) {
-        const float b = J.train ? 0.f : (float)dbias;
-        J.dbias[c] = J.grad_acc ? J.dbias[c] + b : b;
-      }
+    }
+    // the conv bias of a train-mode BatchNorm has an exactly zero gradient
+    // (the batch mean absorbs it; engine.bias_grad)
+    if (J.dbias) {
+      const float b = J.train ? 0.f : (float)dbias;
+      J.dbias[c] = J.grad_acc ? J.dbias[c] + b : b;
     }
   }
   __syncthreads();
@@ -396,54 +422,56 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   // phase 3a: conv weight gradients dW_j[c][l] (+)= sum_n DY[n][c] z[n][l];
   // LAT_RMW elements per thread per round so that the read-modify-write
   // loads of a round are in flight together
-  for (int j = 0; j < njobs; ++j) {
-    const VuLatentJob& J = jobs.j[j];
-    if (!J.dw) continue;
-    const int co = J.co, o = joff[j];
-    for (int e0 = tid; e0 < co * L; e0 += LAT_RMW * LAT_BT) {
-      float old[LAT_RMW], s[LAT_RMW];
+  for (int e0 = tid; e0 < CT * L; e0 += LAT_RMW * LAT_BT) {
+    float* dst[LAT_RMW];
+    float old[LAT_RMW], s[LAT_RMW];
 #pragma unroll
-      for (int u = 0; u < LAT_RMW; ++u) {
-        const int e = e0 + u * LAT_BT;
-        old[u] = (e < co * L && J.grad_acc) ? J.dw[e] : 0.f;
-        s[u] = 0.f;
-        if (e >= co * L) continue;
-        const int c = e / L, l = e - c * L;
-        for (int n = 0; n < N; ++n) s[u] += sdy[n * CT + o + c] * sz[n * L + l];
-      }
-#pragma unroll
-      for (int u = 0; u < LAT_RMW; ++u) {
-        const int e = e0 + u * LAT_BT;
-        if (e < co * L) J.dw[e] = old[u] + s[u];
-      }
+    for (int u = 0; u < LAT_RMW; ++u) {
+      const int e = e0 + u * LAT_BT;
+      dst[u] = nullptr;
+      old[u] = 0.f;
+      s[u] = 0.f;
+      if (e >= CT * L) continue;
+      const int cc = e / L, l = e - cc * L;
+      const int j = job_of(cc);
+      if (!lj[j].dw) continue;
+      dst[u] = lj[j].dw + (int64_t)(cc - loff[j]) * L + l;
+      if (lj[j].grad_acc) old[u] = *dst[u];
+      for (int n = 0; n < N; ++n) s[u] += sdy[n * CT + cc] * sz[n * L + l];
     }
+#pragma unroll
+    for (int u = 0; u < LAT_RMW; ++u)
+      if (dst[u]) *dst[u] = old[u] + s[u];
   }
   // phase 3b: dz[n][l] = sum_j sum_c W_j[c][l] DY_j[n][c]: wave w takes the
-  // channel slice [w co/16, (w+1) co/16) of every job, lane = (n-half, l)
-  // over 32 l; the 16 wave partials are summed in wave order
+  // slice [w CT/16, (w+1) CT/16) of the concatenated channels, lane =
+  // (n-half, l) over 32 l; the 16 wave partials are summed in wave order
   const int nw = LAT_BT / 64;
   const int nh = lane >> 5;
+  const int cb = (int)((int64_t)wv * CT / nw), ce = (int)((int64_t)(wv + 1) * CT / nw);
   for (int l0 = 0; l0 < L; l0 += 32)
   for (int n0 = 0; n0 < N; n0 += 8) {       // 8 samples x 32 dims per pass: 4 accumulators per lane
     const int l = l0 + (lane & 31);
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     if (l < L) {
-      for (int j = 0; j < njobs; ++j) {
-        const float* Wj = jobs.j[j].w;
-        const int co = jobs.j[j].co, o = joff[j];
-        const int cb = (int)((int64_t)wv * co / nw), ce = (int)((int64_t)(wv + 1) * co / nw);
-        for (int c0 = cb; c0 < ce; c0 += 8) {   // 8 weight loads in flight per lane
-          float wcl[8];
+      for (int c0 = cb; c0 < ce; c0 += 8) {   // 8 weight loads in flight per lane
+        float wcl[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) wcl[u] = c0 + u < ce ? Wj[(int64_t)(c0 + u) * L + l] : 0.f;
+        for (int u = 0; u < 8; ++u) {
+          const int cc = c0 + u;
+          wcl[u] = 0.f;
+          if (cc < ce) {
+            const int j = job_of(cc);
+            wcl[u] = lj[j].w[(int64_t)(cc - loff[j]) * L + l];
+          }
+        }
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            if (c0 + u >= ce) break;
+        for (int u = 0; u < 8; ++u) {
+          if (c0 + u >= ce) break;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int n = n0 + 2 * k + nh;
-              if (n < N) acc[k] += wcl[u] * sdy[n * CT + o + c0 + u];
-            }
+          for (int k = 0; k < 4; ++k) {
+            const int n = n0 + 2 * k + nh;
+            if (n < N) acc[k] += wcl[u] * sdy[n * CT + c0 + u];
           }
         }
       }

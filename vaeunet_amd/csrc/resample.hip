@@ -455,6 +455,30 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
     if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
     else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
   };
+  if (j.q == 5) {
+    // the input is row-major in the output's dim order (the forward image of a
+    // channels_last weight: [co][kh][kw][ci] on both sides): a converting
+    // copy, 4 elements per thread, no index arithmetic
+    const uint32_t tot = (uint32_t)d[0] * d[1] * d[2] * d[3];
+    const uint32_t e0 = blk * PERM_CHUNK;
+    const uint32_t e1 = e0 + PERM_CHUNK < tot ? e0 + PERM_CHUNK : tot;
+    for (uint32_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
+      if (e + 4 <= e1 && ((uintptr_t)(in + e) & 15) == 0) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(in + e);
+        if (j.dtype == VU_BF16) {
+          u32x2 o;
+          o[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(j.out) + e) = o;
+        } else {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(j.out) + e) = v;
+        }
+      } else {
+        for (uint32_t k = e; k < e + 4 && k < e1; ++k) put(k, in[k]);
+      }
+    }
+    return;
+  }
   if (j.q >= 3) {
     const uint32_t d1 = d[1], d2 = d[2], d3 = d[3];
     const uint32_t tot = (uint32_t)d[0] * d1 * d2 * d3;

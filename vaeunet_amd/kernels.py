@@ -367,16 +367,23 @@ class record_permutes:
         return False
 
 
-def perm_mode(strides, dims):
+def perm_mode(strides, dims, d3v=None):
     """vu_permute4_batch job mode: 3 = stream (output-fast dim is the
-    input-fast one), 0-2 = 32x32 tile transpose between that dim and dim 3,
+    input-fast one), 5 = the same with the input row-major in the output's
+    dim order and no padding (a converting copy: the forward image of a
+    channels_last weight), 0-2 = 32x32 tile transpose between that dim and dim 3,
     4 = 3x3 or 2x2 weight image (dims 1, 2 merge into 9 or 4 taps forming one
     contiguous input run with dim 0 or dim 3): 32 x T x 32 tile transpose."""
     # input-fastest dim (among those of extent > 1); a transpose if not dim 3
     cand = [k for k in range(4) if dims[k] > 1] or [3]
     q = min(cand, key=lambda k: (abs(strides[k]), k != cand[-1]))
     if q == cand[-1] or dims[3] == 1:
-        return 3  # output-fast == input-fast: stream
+        # output-fast == input-fast: stream; a plain converting copy when the
+        # input is row-major in the output's dim order (no padding)
+        if strides[3] == 1 and strides[2] == dims[3] and strides[1] == dims[2] * dims[3] \
+                and strides[0] == dims[1] * dims[2] * dims[3] and d3v == dims[3]:
+            return 5
+        return 3
     T = dims[1] * dims[2]
     if (q in (1, 2) and dims[1] > 1 and dims[2] > 1 and T in (4, 9) and strides[1] == dims[2] * strides[2]
             and abs(strides[2]) == 1 and T * abs(strides[2]) in (abs(strides[0]), abs(strides[3]))):
@@ -389,7 +396,7 @@ def job_table(jobs):
     (table tensor, ntap, tap blocks, other blocks): the 3x3 / 2x2 weight
     images (mode 4) first, each group with its own block prefix."""
     chunk = query("vu_permute4_chunk")
-    modes = [perm_mode(j[2], j[3]) for j in jobs]
+    modes = [perm_mode(j[2], j[3], j[4]) for j in jobs]
     order = [i for i in range(len(jobs)) if modes[i] == 4] + [i for i in range(len(jobs)) if modes[i] != 4]
     ntap = sum(1 for m in modes if m == 4)
     arr = (_lib.VuPermJob * len(jobs))()
@@ -408,7 +415,7 @@ def job_table(jobs):
         e.out = out.data_ptr()
         e.chunk0 = c0
         e.q = q
-        if q == 3:
+        if q in (3, 5):
             c0 += -(-out.numel() // chunk)
         elif q == 4:
             c0 += (-(-dims[0] // 32)) * (-(-dims[3] // 32))
