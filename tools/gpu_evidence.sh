@@ -25,3 +25,7 @@ python tools/pmc_traffic.py $O/pmc_fetch_vae $O/pmc_write_vae $O/pmc_traffic_vae
 for m in unet vae; do find $O/prof_$m -name "*kernel_stats.csv" -exec cp {} $O/${m}_kernel_stats.csv \; ; done &&
 rm -rf $O/pmc_fetch_* $O/pmc_write_* &&
 tail -1 $O/bench_unet.log | cut -c1-400 && tail -1 $O/bench_vae.log | cut -c1-400
+for m in unet vae; do python tools/replay_trace.py $O/prof_$m/p_kernel_trace.csv --list-last > $O/replay_trace_$m.txt || exit 1; done
+python tools/tail_bw.py $O/pmc_traffic.json $O/unet_kernel_stats.csv 13 45 > $O/tail_bw_unet.txt &&
+python tools/tail_bw.py $O/pmc_traffic_vae.json $O/vae_kernel_stats.csv 13 45 > $O/tail_bw_vae.txt &&
+rm -f $O/prof_unet/p_kernel_trace.csv.gz && echo evidence-done

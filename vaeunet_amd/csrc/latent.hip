@@ -221,10 +221,13 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(const LatentJobs jobs, 
   const int vpp = nch >> 3;                // vectors per pixel (cpad % 8 == 0)
   const int64_t e0 = pc * LAT_PCH, e1 = min(M, e0 + LAT_PCH);
   T* out = reinterpret_cast<T*>(J.out);
+  // (n, pixel, vector) decodes by multiply-shift: the 64-bit divisions per
+  // 16-byte store were the kernel's cost (pixel counts < 2^31: host check)
+  const FastDiv dv((uint32_t)vpp), dhw((uint32_t)J.HW);
   for (int64_t e = e0 * vpp + tid; e < e1 * vpp; e += 256) {
-    const int64_t pix = e / vpp;
+    const int64_t pix = (int64_t)dv.div((uint32_t)e);
     const int v = (int)(e - pix * vpp);
-    const int n = (int)(pix / J.HW);
+    const int n = (int)dhw.div((uint32_t)pix);
     Vec8<T> o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) o.set(k, act[n * LAT_CG + v * 8 + k]);
@@ -313,7 +316,15 @@ __host__ __device__ inline int64_t latent_bwd_lds_floats(int N, int L, int CT, i
 
 __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs jobs, int njobs, VuLatentHeads hb,
                                                             int N, int L, float* ws) {
-  (void)ws;
+  // ws (optional, A/B diagnostics only): thread 0 records the real-time
+  // counter (100 MHz) at each phase boundary into ws[0 .. 7] as uint64
+  uint64_t* const tsv = reinterpret_cast<uint64_t*>(ws);
+  int tsk = 0;
+  auto stamp = [&]() {
+    if (tsv && threadIdx.x == 0) tsv[tsk] = __builtin_amdgcn_s_memrealtime();
+    ++tsk;
+  };
+  stamp();
   extern __shared__ float lsm[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int joff[LAT_MAXJ + 1];
@@ -341,6 +352,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   }
   if (tid <= njobs) loff[tid] = joff[tid];
   __syncthreads();
+  stamp();
   auto job_of = [&](int cc) {
     int j = 0;
     while (j + 1 < njobs && cc >= loff[j + 1]) ++j;
@@ -364,6 +376,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   }
   for (int e = tid; e < N * L; e += LAT_BT) sz[e] = hb.z[e];
   __syncthreads();
+  stamp();
 
   // phase 2: BatchNorm (+ReLU) backward per consumer channel on the N vectors
   for (int cc = tid; cc < CT; cc += LAT_BT) {
@@ -418,6 +431,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     }
   }
   __syncthreads();
+  stamp();
 
   // phase 3a: conv weight gradients dW_j[c][l] (+)= sum_n DY[n][c] z[n][l];
   // LAT_RMW elements per thread per round so that the read-modify-write
@@ -483,6 +497,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     }
   }
   __syncthreads();
+  stamp();
   for (int e = tid; e < N * L; e += LAT_BT) {
     float s = hb.dz_in ? hb.dz_in[e] : 0.f;
     for (int w = 0; w < nw; ++w) s += su[(int64_t)w * N * L + e];
@@ -493,10 +508,12 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     sdlv[e] = gl + (hb.eps ? s * hb.eps[e] * 0.5f * expf(0.5f * hb.logvar[e]) : 0.f);
   }
   __syncthreads();
+  stamp();
   // pooled -> LDS (over the dz partials)
   float* spool = su;
   for (int e = tid; e < N * C; e += LAT_BT) spool[e] = hb.pooled[e];
   __syncthreads();
+  stamp();
 
   // phase 4: heads. dW[jj][c] (+)= sum_n d[n][jj] pooled[n][c]; db[jj] (+)= sum_n d[n][jj]
   for (int e0 = tid; e0 < 2 * L * C; e0 += LAT_RMW * LAT_BT) {
@@ -554,6 +571,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     for (int k = 0; k < 8; ++k)
       if (n0 + k < N) hb.dpooled[(int64_t)(n0 + k) * C + c] = acc[k];
   }
+  stamp();
 }
 
 }  // namespace
@@ -599,6 +617,7 @@ static int pack(const VuLatentJob* jobs, int njobs, int N, LatentJobs& J, int64_
     J.j[j] = jobs[j];
     VuLatentJob& q = J.j[j];
     if (vu_latent_check_job(q.co, q.cpad, q.out_stride, 0) != 0 || q.HW < 1) return (int)hipErrorInvalidValue;
+    if ((int64_t)N * q.HW * 8 >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;  // 32-bit decodes
     q.cgroups = (q.cpad + LAT_CG - 1) / LAT_CG;
     q.block0 = fblocks;
     q.sblock0 = sblocks;
