@@ -295,16 +295,24 @@ __global__ __launch_bounds__(256) void latent_sums_kernel(const LatentJobs jobs,
 //                 pooled [N][C]
 // All sums run in a fixed order (reproducible).
 constexpr int LAT_BT = 1024;
+// Global-address-space pointers: through plain (generic) pointers the
+// compiler emits flat loads / stores, which also count in lgkmcnt -- every
+// LDS wait of the loops below then waited for the outstanding global loads
+// too (99 flat memory instructions in the first builds of this kernel).
+typedef __attribute__((address_space(1))) float gfloat;
+template <typename P> VU_DEV gfloat* gf(P* p) { return (gfloat*)(float*)p; }
+template <typename P> VU_DEV const gfloat* gfc(const P* p) { return (const gfloat*)(const float*)p; }
+
 struct LJob {   // the fields of a VuLatentJob the backward reads, in LDS
-  const float* part;
-  const float* coef;
-  const float* y;
-  const float* gamma;
-  float* dgamma;
-  float* dbeta;
-  float* dbias;
-  float* dw;
-  const float* w;
+  const gfloat* part;
+  const gfloat* coef;
+  const gfloat* y;
+  const gfloat* gamma;
+  gfloat* dgamma;
+  gfloat* dbeta;
+  gfloat* dbias;
+  gfloat* dw;
+  const gfloat* w;
   int co, grad_acc, train;
 };
 constexpr int LAT_RMW = 8;    // gradient elements per thread per round (phases 3a, 4)
@@ -348,7 +356,8 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   __shared__ int loff[LAT_MAXJ + 1];
   if (tid < njobs) {
     const VuLatentJob& J = jobs.j[tid];
-    lj[tid] = LJob{J.part, J.coef, J.y, J.gamma, J.dgamma, J.dbeta, J.dbias, J.dw, J.w, J.co, J.grad_acc, J.train};
+    lj[tid] = LJob{gfc(J.part), gfc(J.coef), gfc(J.y), gfc(J.gamma), gf(J.dgamma), gf(J.dbeta), gf(J.dbias),
+                   gf(J.dw), gfc(J.w), J.co, J.grad_acc, J.train};
   }
   if (tid <= njobs) loff[tid] = joff[tid];
   __syncthreads();
@@ -365,7 +374,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     const int n = e / CT, cc = e - n * CT;
     const int j = job_of(cc);
     const int co = lj[j].co, c = cc - loff[j];
-    const float* pp = lj[j].part + (int64_t)n * LAT_SPLITS * co + c;
+    const gfloat* pp = lj[j].part + (int64_t)n * LAT_SPLITS * co + c;
     float v[LAT_SPLITS];
 #pragma unroll
     for (int q = 0; q < LAT_SPLITS; ++q) v[q] = pp[(int64_t)q * co];
@@ -374,7 +383,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     for (int q = 0; q < LAT_SPLITS; ++q) S += v[q];
     sdy[e] = S;
   }
-  for (int e = tid; e < N * L; e += LAT_BT) sz[e] = hb.z[e];
+  for (int e = tid; e < N * L; e += LAT_BT) sz[e] = gfc(hb.z)[e];
   __syncthreads();
   stamp();
 
@@ -437,7 +446,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   // LAT_RMW elements per thread per round so that the read-modify-write
   // loads of a round are in flight together
   for (int e0 = tid; e0 < CT * L; e0 += LAT_RMW * LAT_BT) {
-    float* dst[LAT_RMW];
+    gfloat* dst[LAT_RMW];
     float old[LAT_RMW], s[LAT_RMW];
 #pragma unroll
     for (int u = 0; u < LAT_RMW; ++u) {
@@ -499,25 +508,25 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   __syncthreads();
   stamp();
   for (int e = tid; e < N * L; e += LAT_BT) {
-    float s = hb.dz_in ? hb.dz_in[e] : 0.f;
+    float s = hb.dz_in ? gfc(hb.dz_in)[e] : 0.f;
     for (int w = 0; w < nw; ++w) s += su[(int64_t)w * N * L + e];
     // reparameterize backward (unet_resnet.py:191-194): z = mu + eps * exp(lv / 2)
-    const float gm = hb.dmu_in ? hb.dmu_in[e] : 0.f;
-    const float gl = hb.dlv_in ? hb.dlv_in[e] : 0.f;
+    const float gm = hb.dmu_in ? gfc(hb.dmu_in)[e] : 0.f;
+    const float gl = hb.dlv_in ? gfc(hb.dlv_in)[e] : 0.f;
     sdmu[e] = gm + s;
-    sdlv[e] = gl + (hb.eps ? s * hb.eps[e] * 0.5f * expf(0.5f * hb.logvar[e]) : 0.f);
+    sdlv[e] = gl + (hb.eps ? s * gfc(hb.eps)[e] * 0.5f * expf(0.5f * gfc(hb.logvar)[e]) : 0.f);
   }
   __syncthreads();
   stamp();
   // pooled -> LDS (over the dz partials)
   float* spool = su;
-  for (int e = tid; e < N * C; e += LAT_BT) spool[e] = hb.pooled[e];
+  for (int e = tid; e < N * C; e += LAT_BT) spool[e] = gfc(hb.pooled)[e];
   __syncthreads();
   stamp();
 
   // phase 4: heads. dW[jj][c] (+)= sum_n d[n][jj] pooled[n][c]; db[jj] (+)= sum_n d[n][jj]
   for (int e0 = tid; e0 < 2 * L * C; e0 += LAT_RMW * LAT_BT) {
-    float* dst[LAT_RMW];
+    gfloat* dst[LAT_RMW];
     float old[LAT_RMW], s[LAT_RMW];
 #pragma unroll
     for (int u = 0; u < LAT_RMW; ++u) {
@@ -528,7 +537,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
       if (e >= 2 * L * C) continue;
       const int h = e / (L * C), r = e - h * (L * C), jj = r / C, c = r - jj * C;
       const float* d = h ? sdlv : sdmu;
-      float* dw = h ? hb.dw_lv : hb.dw_mu;
+      gfloat* dw = gf(h ? hb.dw_lv : hb.dw_mu);
       if (!dw) continue;
       dst[u] = dw + r;
       if (hb.grad_acc) old[u] = dw[r];
@@ -541,7 +550,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
   for (int e = tid; e < 2 * L; e += LAT_BT) {
     const int h = e / L, jj = e - h * L;
     const float* d = h ? sdlv : sdmu;
-    float* db = h ? hb.db_lv : hb.db_mu;
+    gfloat* db = gf(h ? hb.db_lv : hb.db_mu);
     if (!db) continue;
     float s = 0.f;
     for (int n = 0; n < N; ++n) s += d[n * L + jj];
@@ -556,8 +565,8 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
       float wm[8], wl[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        wm[u] = j0 + u < L ? hb.w_mu[(int64_t)(j0 + u) * C + c] : 0.f;
-        wl[u] = j0 + u < L ? hb.w_lv[(int64_t)(j0 + u) * C + c] : 0.f;
+        wm[u] = j0 + u < L ? gfc(hb.w_mu)[(int64_t)(j0 + u) * C + c] : 0.f;
+        wl[u] = j0 + u < L ? gfc(hb.w_lv)[(int64_t)(j0 + u) * C + c] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs job
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if (n0 + k < N) hb.dpooled[(int64_t)(n0 + k) * C + c] = acc[k];
+      if (n0 + k < N) gf(hb.dpooled)[(int64_t)(n0 + k) * C + c] = acc[k];
   }
   stamp();
 }

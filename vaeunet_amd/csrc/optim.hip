@@ -16,6 +16,12 @@ namespace {
 constexpr int MT_THREADS = 256;
 constexpr int MT_CHUNK = 8192;  // elements per block (32 per thread)
 
+// the table's tensor pointers are generic (flat) pointers; cast to the global
+// address space so the element loads and stores issue as global_* (vmcnt
+// only) instead of flat_* (vmcnt + lgkmcnt)
+typedef __attribute__((address_space(1))) float gfl;
+typedef __attribute__((address_space(1))) f32x4 gf32x4;
+
 VU_DEV int find_tensor(const VuMtEntry* t, int n, int64_t chunk) {
   int lo = 0, hi = n - 1;
   while (lo < hi) {
@@ -32,7 +38,7 @@ __global__ void mt_sumsq_kernel(const VuMtEntry* t, int n, double* part) {
   const int k = find_tensor(t, n, chunk);
   const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
   const int64_t end = min(t[k].numel, off + MT_CHUNK);
-  const float* g = reinterpret_cast<const float*>(t[k].grad);
+  const gfl* g = (const gfl*)(t[k].grad);
   double a = 0;
   for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
     double v = g[i];
@@ -67,7 +73,7 @@ __global__ void mt_scale_kernel(const VuMtEntry* t, int n, const float* coef) {
   const int k = find_tensor(t, n, chunk);
   const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
   const int64_t end = min(t[k].numel, off + MT_CHUNK);
-  float* g = reinterpret_cast<float*>(t[k].grad);
+  gfl* g = (gfl*)(t[k].grad);
   const float c = *coef;
   for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) g[i] *= c;
 }
@@ -85,10 +91,10 @@ __global__ void mt_adamw_kernel(const VuMtEntry* t, int n, float decay, float w1
   const int k = find_tensor(t, n, chunk);
   const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
   const int64_t end = min(t[k].numel, off + MT_CHUNK);
-  float* p = reinterpret_cast<float*>(t[k].param);
-  const float* g = reinterpret_cast<const float*>(t[k].grad);
-  float* m = reinterpret_cast<float*>(t[k].exp_avg);
-  float* v = reinterpret_cast<float*>(t[k].exp_avg_sq);
+  gfl* p = (gfl*)(t[k].param);
+  const gfl* g = (const gfl*)(t[k].grad);
+  gfl* m = (gfl*)(t[k].exp_avg);
+  gfl* v = (gfl*)(t[k].exp_avg_sq);
   const float step_size = t[k].step_size, bc2s = t[k].bc2_sqrt;
   const float gs = gscale ? *gscale : 1.f;
   for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
@@ -121,22 +127,53 @@ __global__ void mt_adamw_dev_kernel(const VuMtEntry* t, int n, float decay, floa
   const int k = find_tensor(t, n, chunk);
   const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
   const int64_t end = min(t[k].numel, off + MT_CHUNK);
-  float* p = reinterpret_cast<float*>(t[k].param);
-  float* g = reinterpret_cast<float*>(t[k].grad);
-  float* m = reinterpret_cast<float*>(t[k].exp_avg);
-  float* v = reinterpret_cast<float*>(t[k].exp_avg_sq);
+  gfl* p = (gfl*)(t[k].param);
+  gfl* g = (gfl*)(t[k].grad);
+  gfl* m = (gfl*)(t[k].exp_avg);
+  gfl* v = (gfl*)(t[k].exp_avg_sq);
   const double sc = (double)*step;
   const float step_size = (float)(lr / (1.0 - pow(beta1d, sc)));
   const float bc2s = (float)sqrt(1.0 - pow(beta2d, sc));
-  for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
-    const float gi = g[i];
-    float pi = p[i] * decay;
-    float mi = m[i];
+  auto upd = [&](float gi, float& pi, float& mi, float& vi) {
+    pi = pi * decay;
     mi = mi + w1 * (gi - mi);
-    float vi = v[i] * beta2;
+    vi = vi * beta2;
     vi = vi + w2 * gi * gi;
     const float denom = sqrtf(vi) / bc2s + eps;
     pi = pi + (-step_size) * (mi / denom);
+  };
+  // 16-byte accesses (4 elements per thread and iteration, the four streams'
+  // loads in flight together) when the four tensors' chunk starts are
+  // 16-byte aligned; the same per-element arithmetic either way
+  const bool vec = (((uintptr_t)(p + off) | (uintptr_t)(g + off) | (uintptr_t)(m + off) | (uintptr_t)(v + off)) &
+                    15) == 0;
+  int64_t i0 = off;
+  if (vec) {
+    const int64_t nv = (end - off) / 4;
+    for (int64_t q = threadIdx.x; q < nv; q += MT_THREADS) {
+      const int64_t i = off + 4 * q;
+      const f32x4 gv = *reinterpret_cast<const gf32x4*>(g + i);
+      f32x4 pv = *reinterpret_cast<const gf32x4*>(p + i);
+      f32x4 mv = *reinterpret_cast<const gf32x4*>(m + i);
+      f32x4 vv = *reinterpret_cast<const gf32x4*>(v + i);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float pi = pv[u], mi = mv[u], vi = vv[u];
+        upd(gv[u], pi, mi, vi);
+        pv[u] = pi;
+        mv[u] = mi;
+        vv[u] = vi;
+      }
+      *reinterpret_cast<gf32x4*>(p + i) = pv;
+      *reinterpret_cast<gf32x4*>(m + i) = mv;
+      *reinterpret_cast<gf32x4*>(v + i) = vv;
+      if (zero_grad) *reinterpret_cast<gf32x4*>(g + i) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    i0 = off + 4 * nv;
+  }
+  for (int64_t i = i0 + threadIdx.x; i < end; i += MT_THREADS) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    upd(g[i], pi, mi, vi);
     p[i] = pi; m[i] = mi; v[i] = vi;
     if (zero_grad) g[i] = 0.f;
   }

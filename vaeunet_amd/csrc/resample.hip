@@ -411,9 +411,16 @@ extern "C" int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1
 // per block.  chunk0 is the prefix block count (binary search per block).
 namespace {
 constexpr int PERM_CHUNK = 4096;
+// global-address-space views of the job pointers (read from a device table:
+// through generic pointers the loads are flat instructions, which count in
+// lgkmcnt and so wait behind / hold up the tile transposes' LDS traffic)
+typedef __attribute__((address_space(1))) float gfl;
+typedef __attribute__((address_space(1))) bf16_t gbf;
+typedef __attribute__((address_space(1))) u32x2 gu32x2;
+typedef __attribute__((address_space(1))) f32x4 gf32x4;
 
 template <int T, typename Put>
-__device__ __forceinline__ void tap_tile(const VuPermJob& j, const float* in, const int* d, const int* st,
+__device__ __forceinline__ void tap_tile(const VuPermJob& j, const gfl* in, const int* d, const int* st,
                                          uint32_t blk, float* big, Put put) {
   const int sT = st[2];
   const bool run0 = j.s0 == (int64_t)T * (sT < 0 ? -sT : sT);   // dim 0 pairs with the taps
@@ -449,11 +456,11 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
   // 32-bit index math (every weight image has < 2^31 elements)
   const int d[4] = {j.d0, j.d1, j.d2, j.d3};
   const int st[4] = {(int)j.s0, (int)j.s1, (int)j.s2, (int)j.s3};
-  const float* in = j.in + j.base;
+  const gfl* in = (const gfl*)(j.in + j.base);
   const uint32_t blk = (uint32_t)(chunk - j.chunk0);
   auto put = [&](uint32_t e, float v) {
-    if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
-    else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
+    if (j.dtype == VU_BF16) ((gbf*)j.out)[e] = f2bf(v);
+    else ((gfl*)j.out)[e] = v;
   };
   if (j.q == 5) {
     // the input is row-major in the output's dim order (the forward image of a
@@ -464,14 +471,14 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
     const uint32_t e1 = e0 + PERM_CHUNK < tot ? e0 + PERM_CHUNK : tot;
     for (uint32_t e = e0 + 4 * threadIdx.x; e < e1; e += 4 * blockDim.x) {
       if (e + 4 <= e1 && ((uintptr_t)(in + e) & 15) == 0) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(in + e);
+        const f32x4 v = *(const gf32x4*)(in + e);
         if (j.dtype == VU_BF16) {
           u32x2 o;
           o[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
           o[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          *reinterpret_cast<u32x2*>(reinterpret_cast<bf16_t*>(j.out) + e) = o;
+          *(gu32x2*)((gbf*)j.out + e) = o;
         } else {
-          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(j.out) + e) = v;
+          *(gf32x4*)((gfl*)j.out + e) = v;
         }
       } else {
         for (uint32_t k = e; k < e + 4 && k < e1; ++k) put(k, in[k]);
@@ -500,7 +507,7 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
   const int iq0 = (int)(rem / t3) * 32, i30 = (int)(rem - (rem / t3) * t3) * 32;
   const int ia = (int)(b / d[c]), ic = (int)(b - (b / d[c]) * d[c]);
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const float* ib = in + ia * st[a] + ic * st[c];
+  const gfl* ib = in + ia * st[a] + ic * st[c];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int iq = iq0 + tx, i3 = i30 + ty + 8 * k;
@@ -537,11 +544,11 @@ __global__ __launch_bounds__(256) void permute4_tap_kernel(const VuPermJob* jobs
   const VuPermJob& j = jobs[lo];
   const int d[4] = {j.d0, j.d1, j.d2, j.d3};
   const int st[4] = {(int)j.s0, (int)j.s1, (int)j.s2, (int)j.s3};
-  const float* in = j.in + j.base;
+  const gfl* in = (const gfl*)(j.in + j.base);
   const uint32_t blk = (uint32_t)(chunk - j.chunk0);
   auto put = [&](uint32_t e, float v) {
-    if (j.dtype == VU_BF16) st1<bf16_t>(reinterpret_cast<bf16_t*>(j.out) + e, v);
-    else st1<float>(reinterpret_cast<float*>(j.out) + e, v);
+    if (j.dtype == VU_BF16) ((gbf*)j.out)[e] = f2bf(v);
+    else ((gfl*)j.out)[e] = v;
   };
   if (d[1] * d[2] == 9) tap_tile<9>(j, in, d, st, blk, big, put);
   else tap_tile<4>(j, in, d, st, blk, big, put);
