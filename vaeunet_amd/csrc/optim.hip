@@ -78,6 +78,21 @@ __global__ void mt_scale_kernel(const VuMtEntry* t, int n, const float* coef) {
   for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) g[i] *= c;
 }
 
+// One AdamW element update, every operation rounded on its own (no fused
+// multiply-add contraction): the eager, the capturable scalar and the
+// capturable 16-byte paths must produce identical bits whatever the compiler
+// vectorises.
+VU_DEV void adamw_elem(float gi, float& pi, float& mi, float& vi, float decay, float w1, float beta2, float w2,
+                       float eps, float step_size, float bc2s) {
+#pragma clang fp contract(off)
+  pi = pi * decay;
+  mi = mi + w1 * (gi - mi);  // lerp, weight < 0.5 branch
+  vi = vi * beta2;
+  vi = vi + w2 * gi * gi;
+  const float denom = sqrtf(vi) / bc2s + eps;
+  pi = pi + (-step_size) * (mi / denom);
+}
+
 // AdamW, the element order of torch's _multi_tensor_adamw:
 //   p *= 1 - lr*wd; m = lerp(m, g, 1-b1); v = v*b2 + (1-b2) g^2;
 //   p += -step_size * m / (sqrt(v) / bc2_sqrt + eps)
@@ -100,13 +115,8 @@ __global__ void mt_adamw_kernel(const VuMtEntry* t, int n, float decay, float w1
   for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
     float gi = g[i];
     if (gscale) gi *= gs;
-    float pi = p[i] * decay;
-    float mi = m[i];
-    mi = mi + w1 * (gi - mi);                       // lerp, weight < 0.5 branch
-    float vi = v[i] * beta2;
-    vi = vi + w2 * gi * gi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    pi = pi + (-step_size) * (mi / denom);
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(gi, pi, mi, vi, decay, w1, beta2, w2, eps, step_size, bc2s);
     p[i] = pi; m[i] = mi; v[i] = vi;
   }
 }
@@ -135,12 +145,7 @@ __global__ void mt_adamw_dev_kernel(const VuMtEntry* t, int n, float decay, floa
   const float step_size = (float)(lr / (1.0 - pow(beta1d, sc)));
   const float bc2s = (float)sqrt(1.0 - pow(beta2d, sc));
   auto upd = [&](float gi, float& pi, float& mi, float& vi) {
-    pi = pi * decay;
-    mi = mi + w1 * (gi - mi);
-    vi = vi * beta2;
-    vi = vi + w2 * gi * gi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    pi = pi + (-step_size) * (mi / denom);
+    adamw_elem(gi, pi, mi, vi, decay, w1, beta2, w2, eps, step_size, bc2s);
   };
   // 16-byte accesses (4 elements per thread and iteration, the four streams'
   // loads in flight together) when the four tensors' chunk starts are
