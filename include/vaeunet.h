@@ -678,11 +678,14 @@ int64_t vu_latent_part_floats(int N, int co);
 int vu_latent_bwd_sums(const VuLatentJob* jobs, int njobs, int N, int dtype, void* stream);
 int64_t vu_latent_bwd_workspace_bytes(int N, int L, int64_t sum_co);
 /* 1 when vu_latent_bwd serves N samples, latent size L, consumers with
- * sum_co output channels in all and C encoder channels (its one-block
- * working set fits in LDS), else 0 (the caller takes the map path) */
+ * sum_co output channels in all and C encoder channels (N <= 64, L <= 64,
+ * C % 8 == 0), else 0 (the caller takes the map path) */
 int vu_latent_bwd_supported(int N, int L, int64_t sum_co, int C);
-/* one block: every consumer's BN / ReLU / conv backward on the vectors, dz,
- * reparameterize backward, both heads' backward -> dpooled */
+/* two launches: every consumer's BN / ReLU / conv backward on the vectors
+ * (one block per 32 consumer channels; dz partials into the workspace of
+ * vu_latent_bwd_workspace_bytes, required when njobs > 0), then dz,
+ * reparameterize backward, both heads' backward -> dpooled (one block per 8
+ * encoder channels) */
 int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentHeads* heads, int N, int L,
                   float* workspace, void* stream);
 /* 0 when a consumer of this geometry is served (co = 8 * 2^k <= 2048, cpad % 8,

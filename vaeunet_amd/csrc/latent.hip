@@ -1,6 +1,6 @@
 // The VAE bottleneck of UNetResNet (unet/unet_resnet.py:140-154, 191-194,
 // 217-229) and the latent injection of its DecoderBlocks (:37-41, 93-94) as
-// four launches per training step instead of ~50.
+// five launches per training step instead of ~50.
 //
 // Everything downstream of z is spatially constant per sample: z_spatial =
 // interpolate(z[..., None, None], align_corners=True) is an exact broadcast,
@@ -21,11 +21,12 @@
 //                      the consumer's conv + BN (+running statistics) + ReLU
 //                      on the N vectors, then its map stores;
 //   vu_latent_bwd_sums per-sample partial pixel sums of the maps' gradients;
-//   vu_latent_bwd      one block: BN / ReLU / conv backward of every consumer
-//                      on the vectors (weight, bias, gamma, beta gradients),
-//                      dz, reparameterize backward, both heads' backward ->
-//                      dpooled (the caller broadcasts dpooled / HW into
-//                      d f[-1] with vu_sample_broadcast).
+//   vu_latent_bwd      two launches: BN / ReLU / conv backward of every
+//                      consumer on the vectors (weight, bias, gamma, beta
+//                      gradients, dz partials), then dz, reparameterize
+//                      backward, both heads' backward -> dpooled (the caller
+//                      broadcasts dpooled / HW into d f[-1] with
+//                      vu_sample_broadcast).
 #include "common.h"
 #include "../../include/vaeunet.h"
 
@@ -36,7 +37,6 @@ constexpr int LAT_CG = 64;      // channels per vu_latent_fwd block
 constexpr int LAT_SPLITS = 32;  // pixel splits per sample of vu_latent_bwd_sums
 constexpr int LAT_MAXN = 64;    // samples
 constexpr int LAT_MAXJ = 8;     // consumers per launch
-#define VU_LATENT_BWD_MAX_LDS (64 * 1024)
 
 // the job table travels BY VALUE in the kernel arguments (~1.7 KB): no device
 // table to upload, so a captured HIP graph replays it as is
@@ -283,304 +283,260 @@ __global__ __launch_bounds__(256) void latent_sums_kernel(const LatentJobs jobs,
   }
 }
 
-// One block (1024 threads): every consumer's backward on the vectors, then
-// the bottleneck's.  The work is ~1 MFLOP; what costs is latency, so every
-// phase runs its global loads in parallel across the block and keeps the
-// intermediate vectors in LDS (the first version walked 256-512-long
-// dependent global-load chains per thread: 510 us per step).  LDS (floats):
-//   sdy [N][CT]   map-gradient sums, then the consumers' pre-BN gradients
-//                 (CT = sum of co over the consumers, job j at column off_j)
-//   sz, sdmu, sdlv [N][L]
-//   su            [max(16 N L, N C)]: the dz partials of the 16 waves, then
-//                 pooled [N][C]
-// All sums run in a fixed order (reproducible).
-constexpr int LAT_BT = 1024;
+// The backward on the vectors, as two launches that spread over the CUs.
+// (Round 4 first: one 1024-thread block for everything -- a ~1 MFLOP job
+// whose time was all latency chains inside one CU: 510 us in its first form,
+// 95-105 us after keeping its vectors in LDS.)  Nothing here depends on
+// anything but the split sums, so each block issues every load it needs up
+// front and then works from LDS:
+//   latent_bwd_bn    one block per (consumer, 32-channel group): the split
+//                    sums of its channels, the BatchNorm (+ReLU) backward on
+//                    the N vectors (gamma / beta / bias gradients), the conv
+//                    weight gradient dW[c][l] (+)= sum_n dy[n][c] z[n][l] of
+//                    its rows, and its partial of dz[n][l] = sum_c W[c][l]
+//                    dy[n][c] into the workspace;
+//   latent_bwd_heads one block per 8 encoder channels: dz = the partials
+//                    summed in block order, reparameterize backward (every
+//                    block redoes this N x L step), the heads' weight
+//                    gradients of its channels, dpooled of its channels;
+//                    block 0 the heads' bias gradients.
+// Every sum runs in a fixed order (reproducible run to run).
+constexpr int LB_T = 256;
+constexpr int LB_CW = 32;   // consumer channels per latent_bwd_bn block
+constexpr int LB_NCH = 8;   // samples per split-sum round
+constexpr int LB_ODW = 8;   // weight-gradient rows held per thread (LB_CW * 64 / LB_T)
+constexpr int LH_CW = 8;    // encoder channels per latent_bwd_heads block
+constexpr int LH_ODW = 4;   // head weight-gradient elements per thread (2 * 64 * LH_CW / LB_T)
+
 // Global-address-space pointers: through plain (generic) pointers the
-// compiler emits flat loads / stores, which also count in lgkmcnt -- every
-// LDS wait of the loops below then waited for the outstanding global loads
-// too (99 flat memory instructions in the first builds of this kernel).
+// compiler emits flat loads / stores, which also count in lgkmcnt, so every
+// LDS wait would wait for the outstanding global loads too.
 typedef __attribute__((address_space(1))) float gfloat;
 template <typename P> VU_DEV gfloat* gf(P* p) { return (gfloat*)(float*)p; }
 template <typename P> VU_DEV const gfloat* gfc(const P* p) { return (const gfloat*)(const float*)p; }
 
-struct LJob {   // the fields of a VuLatentJob the backward reads, in LDS
-  const gfloat* part;
-  const gfloat* coef;
-  const gfloat* y;
-  const gfloat* gamma;
-  gfloat* dgamma;
-  gfloat* dbeta;
-  gfloat* dbias;
-  gfloat* dw;
-  const gfloat* w;
-  int co, grad_acc, train;
-};
-constexpr int LAT_RMW = 8;    // gradient elements per thread per round (phases 3a, 4)
-
-__host__ __device__ inline int64_t latent_bwd_lds_floats(int N, int L, int CT, int C) {
-  const int64_t u = (int64_t)16 * N * L > (int64_t)N * C ? (int64_t)16 * N * L : (int64_t)N * C;
-  return (int64_t)N * CT + 3LL * N * L + u;
+__host__ __device__ inline int lb_blocks(int co) { return (co + LB_CW - 1) / LB_CW; }
+__host__ __device__ inline int64_t lb_lds_floats(int N, int L) {
+  return (int64_t)8 * LB_NCH * LB_CW + 2LL * N * LB_CW + (int64_t)N * L + (int64_t)LB_CW * L;
+}
+__host__ __device__ inline int64_t lh_lds_floats(int N, int L) {
+  return 2LL * N * L + (int64_t)N * LH_CW + 2LL * L * LH_CW;
 }
 
-__global__ __launch_bounds__(LAT_BT) void latent_bwd_kernel(const LatentJobs jobs, int njobs, VuLatentHeads hb,
-                                                            int N, int L, float* ws) {
-  // ws (optional, A/B diagnostics only): thread 0 records the real-time
-  // counter (100 MHz) at each phase boundary into ws[0 .. 7] as uint64
-  uint64_t* const tsv = reinterpret_cast<uint64_t*>(ws);
-  int tsk = 0;
-  auto stamp = [&]() {
-    if (tsv && threadIdx.x == 0) tsv[tsk] = __builtin_amdgcn_s_memrealtime();
-    ++tsk;
-  };
-  stamp();
+__global__ __launch_bounds__(LB_T) void latent_bwd_bn_kernel(const LatentJobs jobs, int njobs, const float* z_, int N,
+                                                             int L, float* dzp_) {
   extern __shared__ float lsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  int joff[LAT_MAXJ + 1];
-  joff[0] = 0;
-  for (int j = 0; j < njobs; ++j) joff[j + 1] = joff[j] + jobs.j[j].co;
-  const int CT = joff[njobs];
-  const int C = hb.C;
-  float* sdy = lsm;
-  float* sz = sdy + (int64_t)N * CT;
-  float* sdmu = sz + N * L;
-  float* sdlv = sdmu + N * L;
-  float* su = sdlv + N * L;
-
-  // The consumers' fields live in an LDS job table so that the loops below
-  // can run over the concatenated (job, channel) space -- all consumers'
-  // work in one round instead of one latency-bound round per consumer -- with
-  // a per-lane job lookup that costs an LDS read, not a per-lane load from
-  // the kernel-argument segment (one memory round trip before every address:
-  // the first version's 510 us).
-  __shared__ LJob lj[LAT_MAXJ];
-  __shared__ int loff[LAT_MAXJ + 1];
-  if (tid < njobs) {
-    const VuLatentJob& J = jobs.j[tid];
-    lj[tid] = LJob{gfc(J.part), gfc(J.coef), gfc(J.y), gfc(J.gamma), gf(J.dgamma), gf(J.dbeta), gf(J.dbias),
-                   gf(J.dw), gfc(J.w), J.co, J.grad_acc, J.train};
+  // block -> (consumer, channel group): a wave-uniform walk of the kernarg table
+  int b = blockIdx.x, j = 0;
+  for (; j + 1 < njobs; ++j) {
+    const int nb = lb_blocks(jobs.j[j].co);
+    if (b < nb) break;
+    b -= nb;
   }
-  if (tid <= njobs) loff[tid] = joff[tid];
-  __syncthreads();
-  stamp();
-  auto job_of = [&](int cc) {
-    int j = 0;
-    while (j + 1 < njobs && cc >= loff[j + 1]) ++j;
-    return j;
-  };
+  j = __builtin_amdgcn_readfirstlane(j);
+  b = __builtin_amdgcn_readfirstlane(b);
+  const VuLatentJob& J = jobs.j[j];
+  const int co = J.co, c0 = b * LB_CW, cw = co - c0 < LB_CW ? co - c0 : LB_CW;
+  const int tid = threadIdx.x, c = tid & (LB_CW - 1), q8 = tid >> 5;
+  float* red = lsm;                          // [8][LB_NCH][LB_CW]
+  float* sy = red + 8 * LB_NCH * LB_CW;      // [N][LB_CW] BN input y
+  float* sdy = sy + N * LB_CW;               // [N][LB_CW] map-gradient sums, then pre-BN gradients
+  float* sz = sdy + N * LB_CW;               // [N][L]
+  float* sw = sz + N * L;                    // [cw][L] the conv weight rows
+  const gfloat* part = gfc(J.part);
+  const gfloat* z = gfc(z_);
+  const gfloat* W = gfc(J.w) + (int64_t)c0 * L;
+  gfloat* dw = J.dw ? gf(J.dw) + (int64_t)c0 * L : nullptr;
 
-  // phase 1: map-gradient sums S[n][c] = sum over the LAT_SPLITS partials
-  // (all 32 loads of a thread in flight), z -> LDS
-  for (int e = tid; e < N * CT; e += LAT_BT) {
-    const int n = e / CT, cc = e - n * CT;
-    const int j = job_of(cc);
-    const int co = lj[j].co, c = cc - loff[j];
-    const gfloat* pp = lj[j].part + (int64_t)n * LAT_SPLITS * co + c;
-    float v[LAT_SPLITS];
-#pragma unroll
-    for (int q = 0; q < LAT_SPLITS; ++q) v[q] = pp[(int64_t)q * co];
-    float S = 0.f;
-#pragma unroll
-    for (int q = 0; q < LAT_SPLITS; ++q) S += v[q];
-    sdy[e] = S;
+  // the loads that depend on nothing: y, z, the weight rows, the old
+  // gradients (read-modify-write when grad_acc), the BN coefficients
+  for (int e = tid; e < N * LB_CW; e += LB_T) {
+    const int n = e / LB_CW, cc = e % LB_CW;
+    if (cc < cw) sy[e] = gfc(J.y)[(int64_t)n * co + c0 + cc];
   }
-  for (int e = tid; e < N * L; e += LAT_BT) sz[e] = gfc(hb.z)[e];
-  __syncthreads();
-  stamp();
+  for (int e = tid; e < N * L; e += LB_T) sz[e] = z[e];
+  for (int e = tid; e < cw * L; e += LB_T) sw[e] = W[e];
+  float odw[LB_ODW];
+#pragma unroll
+  for (int k = 0; k < LB_ODW; ++k) {
+    const int e = tid + k * LB_T;
+    odw[k] = (dw && J.grad_acc && e < cw * L) ? dw[e] : 0.f;
+  }
+  float scale = 0.f, shift = 0.f, mean = 0.f, invstd = 0.f, gamma = 0.f, og = 0.f, ob = 0.f, obias = 0.f;
+  if (tid < cw) {
+    const gfloat* cf = gfc(J.coef) + c0 + tid;
+    scale = cf[0];
+    shift = cf[co];
+    mean = cf[2 * co];
+    invstd = cf[3 * co];
+    gamma = gfc(J.gamma)[c0 + tid];
+    if (J.grad_acc) {
+      if (J.dgamma) og = gfc(J.dgamma)[c0 + tid];
+      if (J.dbeta) ob = gfc(J.dbeta)[c0 + tid];
+      if (J.dbias) obias = gfc(J.dbias)[c0 + tid];
+    }
+  }
 
-  // phase 2: BatchNorm (+ReLU) backward per consumer channel on the N vectors
-  for (int cc = tid; cc < CT; cc += LAT_BT) {
-    const int j = job_of(cc);
-    const LJob& J = lj[j];
-    const int co = J.co, c = cc - loff[j];
-    const float scale = J.coef[c], shift = J.coef[co + c], mean = J.coef[2 * co + c], invstd = J.coef[3 * co + c];
-    const float gamma = J.gamma[c];
-    float yv[16];
-    double db = 0.0, dg = 0.0;
-    for (int n0 = 0; n0 < N; n0 += 16) {
-      const int nn = N - n0 < 16 ? N - n0 : 16;
+  // phase 1: S[n][c] = sum of the LAT_SPLITS partials: thread (q8, c) adds
+  // splits 4 q8 .. 4 q8 + 3 for LB_NCH samples (32 loads in flight), then the
+  // 8 group sums in q8 order
+  for (int n0 = 0; n0 < N; n0 += LB_NCH) {
+    const int nn = N - n0 < LB_NCH ? N - n0 : LB_NCH;
+    float v[LB_NCH][4];
 #pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * co + c];
+    for (int k = 0; k < LB_NCH; ++k)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (k >= nn) break;
-        const int n = n0 + k;
-        const float y = yv[k];
-        const float G = (y * scale + shift > 0.f) ? sdy[n * CT + cc] : 0.f;
-        sdy[n * CT + cc] = G;
-        db += G;
-        dg += (double)G * ((y - mean) * invstd);
+      for (int u = 0; u < 4; ++u)
+        v[k][u] = (k < nn && c < cw) ? part[((int64_t)(n0 + k) * LAT_SPLITS + 4 * q8 + u) * co + c0 + c] : 0.f;
+#pragma unroll
+    for (int k = 0; k < LB_NCH; ++k) red[(q8 * LB_NCH + k) * LB_CW + c] = ((v[k][0] + v[k][1]) + v[k][2]) + v[k][3];
+    __syncthreads();
+    {
+      const int k = q8;   // LB_T = LB_NCH * LB_CW
+      if (k < nn && c < cw) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += red[(q * LB_NCH + k) * LB_CW + c];
+        sdy[(n0 + k) * LB_CW + c] = s;
       }
     }
-    if (J.dgamma) J.dgamma[c] = J.grad_acc ? J.dgamma[c] + (float)dg : (float)dg;
-    if (J.dbeta) J.dbeta[c] = J.grad_acc ? J.dbeta[c] + (float)db : (float)db;
+    __syncthreads();
+  }
+
+  // phase 2: BatchNorm (+ReLU) backward per channel on the N vectors
+  if (tid < cw) {
+    double db = 0.0, dg = 0.0;
+    for (int n = 0; n < N; ++n) {
+      const float y = sy[n * LB_CW + tid];
+      const float G = (y * scale + shift > 0.f) ? sdy[n * LB_CW + tid] : 0.f;
+      sdy[n * LB_CW + tid] = G;
+      db += G;
+      dg += (double)G * ((y - mean) * invstd);
+    }
+    if (J.dgamma) gf(J.dgamma)[c0 + tid] = og + (float)dg;
+    if (J.dbeta) gf(J.dbeta)[c0 + tid] = ob + (float)db;
     const float gi = gamma * invstd;
     const float rM = 1.f / (float)N;   // HW / (N * HW)
     double dbias = 0.0;
-    for (int n0 = 0; n0 < N; n0 += 16) {
-      const int nn = N - n0 < 16 ? N - n0 : 16;
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        if (k < nn) yv[k] = J.y[(int64_t)(n0 + k) * co + c];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (k >= nn) break;
-        const int n = n0 + k;
-        const float G = sdy[n * CT + cc];
-        const float v = J.train ? gi * (G - rM * ((float)db + (yv[k] - mean) * invstd * (float)dg)) : gi * G;
-        sdy[n * CT + cc] = v;
-        dbias += v;
-      }
+    for (int n = 0; n < N; ++n) {
+      const float G = sdy[n * LB_CW + tid];
+      const float y = sy[n * LB_CW + tid];
+      const float v = J.train ? gi * (G - rM * ((float)db + (y - mean) * invstd * (float)dg)) : gi * G;
+      sdy[n * LB_CW + tid] = v;
+      dbias += v;
     }
     // the conv bias of a train-mode BatchNorm has an exactly zero gradient
     // (the batch mean absorbs it; engine.bias_grad)
-    if (J.dbias) {
-      const float b = J.train ? 0.f : (float)dbias;
-      J.dbias[c] = J.grad_acc ? J.dbias[c] + b : b;
-    }
+    if (J.dbias) gf(J.dbias)[c0 + tid] = obias + (J.train ? 0.f : (float)dbias);
   }
   __syncthreads();
-  stamp();
 
-  // phase 3a: conv weight gradients dW_j[c][l] (+)= sum_n DY[n][c] z[n][l];
-  // LAT_RMW elements per thread per round so that the read-modify-write
-  // loads of a round are in flight together
-  for (int e0 = tid; e0 < CT * L; e0 += LAT_RMW * LAT_BT) {
-    gfloat* dst[LAT_RMW];
-    float old[LAT_RMW], s[LAT_RMW];
+  // phase 3: this block's weight-gradient rows and its dz partial
+  if (dw) {
 #pragma unroll
-    for (int u = 0; u < LAT_RMW; ++u) {
-      const int e = e0 + u * LAT_BT;
-      dst[u] = nullptr;
-      old[u] = 0.f;
-      s[u] = 0.f;
-      if (e >= CT * L) continue;
+    for (int k = 0; k < LB_ODW; ++k) {
+      const int e = tid + k * LB_T;
+      if (e >= cw * L) break;
       const int cc = e / L, l = e - cc * L;
-      const int j = job_of(cc);
-      if (!lj[j].dw) continue;
-      dst[u] = lj[j].dw + (int64_t)(cc - loff[j]) * L + l;
-      if (lj[j].grad_acc) old[u] = *dst[u];
-      for (int n = 0; n < N; ++n) s[u] += sdy[n * CT + cc] * sz[n * L + l];
-    }
-#pragma unroll
-    for (int u = 0; u < LAT_RMW; ++u)
-      if (dst[u]) *dst[u] = old[u] + s[u];
-  }
-  // phase 3b: dz[n][l] = sum_j sum_c W_j[c][l] DY_j[n][c]: wave w takes the
-  // slice [w CT/16, (w+1) CT/16) of the concatenated channels, lane =
-  // (n-half, l) over 32 l; the 16 wave partials are summed in wave order
-  const int nw = LAT_BT / 64;
-  const int nh = lane >> 5;
-  const int cb = (int)((int64_t)wv * CT / nw), ce = (int)((int64_t)(wv + 1) * CT / nw);
-  for (int l0 = 0; l0 < L; l0 += 32)
-  for (int n0 = 0; n0 < N; n0 += 8) {       // 8 samples x 32 dims per pass: 4 accumulators per lane
-    const int l = l0 + (lane & 31);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (l < L) {
-      for (int c0 = cb; c0 < ce; c0 += 8) {   // 8 weight loads in flight per lane
-        float wcl[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int cc = c0 + u;
-          wcl[u] = 0.f;
-          if (cc < ce) {
-            const int j = job_of(cc);
-            wcl[u] = lj[j].w[(int64_t)(cc - loff[j]) * L + l];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (c0 + u >= ce) break;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int n = n0 + 2 * k + nh;
-            if (n < N) acc[k] += wcl[u] * sdy[n * CT + c0 + u];
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int n = n0 + 2 * k + nh;
-      if (n < N && l < L) su[((int64_t)wv * N + n) * L + l] = acc[k];
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += sdy[n * LB_CW + cc] * sz[n * L + l];
+      dw[e] = odw[k] + s;
     }
   }
-  __syncthreads();
-  stamp();
-  for (int e = tid; e < N * L; e += LAT_BT) {
+  gfloat* dzp = gf(dzp_) + (int64_t)blockIdx.x * N * L;
+  for (int e = tid; e < N * L; e += LB_T) {
+    const int n = e / L, l = e - n * L;
+    float s = 0.f;
+    for (int cc = 0; cc < cw; ++cc) s += sw[cc * L + l] * sdy[n * LB_CW + cc];
+    dzp[e] = s;
+  }
+}
+
+__global__ __launch_bounds__(LB_T) void latent_bwd_heads_kernel(VuLatentHeads hb, int N, int L, const float* dzp_,
+                                                                int nbp) {
+  extern __shared__ float lsm[];
+  const int C = hb.C, c0 = blockIdx.x * LH_CW, tid = threadIdx.x;
+  float* sdmu = lsm;                  // [N][L]
+  float* sdlv = sdmu + N * L;         // [N][L]
+  float* spool = sdlv + N * L;        // [N][LH_CW]
+  float* swm = spool + N * LH_CW;     // [L][LH_CW]
+  float* swl = swm + L * LH_CW;       // [L][LH_CW]
+  const gfloat* dzp = gfc(dzp_);
+  gfloat* dwm = gf(hb.dw_mu);
+  gfloat* dwl = gf(hb.dw_lv);
+
+  // independent loads: pooled and both heads' weights for this block's
+  // channels, the old weight gradients (grad_acc)
+  for (int e = tid; e < N * LH_CW; e += LB_T) spool[e] = gfc(hb.pooled)[(int64_t)(e / LH_CW) * C + c0 + e % LH_CW];
+  for (int e = tid; e < L * LH_CW; e += LB_T) {
+    const int64_t g = (int64_t)(e / LH_CW) * C + c0 + e % LH_CW;
+    swm[e] = gfc(hb.w_mu)[g];
+    swl[e] = gfc(hb.w_lv)[g];
+  }
+  float odw[LH_ODW];
+#pragma unroll
+  for (int k = 0; k < LH_ODW; ++k) {
+    const int e = tid + k * LB_T;
+    odw[k] = 0.f;
+    if (hb.grad_acc && e < 2 * L * LH_CW) {
+      const int h = e / (L * LH_CW), r = e - h * L * LH_CW;
+      const gfloat* d = h ? dwl : dwm;
+      if (d) odw[k] = d[(int64_t)(r / LH_CW) * C + c0 + r % LH_CW];
+    }
+  }
+  // dz = incoming + the consumers' partials (block order, 16 loads in flight),
+  // then reparameterize backward (unet_resnet.py:191-194): z = mu + eps * exp(lv / 2)
+  for (int e = tid; e < N * L; e += LB_T) {
     float s = hb.dz_in ? gfc(hb.dz_in)[e] : 0.f;
-    for (int w = 0; w < nw; ++w) s += su[(int64_t)w * N * L + e];
-    // reparameterize backward (unet_resnet.py:191-194): z = mu + eps * exp(lv / 2)
     const float gm = hb.dmu_in ? gfc(hb.dmu_in)[e] : 0.f;
     const float gl = hb.dlv_in ? gfc(hb.dlv_in)[e] : 0.f;
+    const float ep = hb.eps ? gfc(hb.eps)[e] : 0.f;
+    const float lv = hb.eps ? gfc(hb.logvar)[e] : 0.f;
+    for (int b0 = 0; b0 < nbp; b0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = b0 + u < nbp ? dzp[(int64_t)(b0 + u) * N * L + e] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (b0 + u < nbp) s += v[u];
+    }
     sdmu[e] = gm + s;
-    sdlv[e] = gl + (hb.eps ? s * gfc(hb.eps)[e] * 0.5f * expf(0.5f * gfc(hb.logvar)[e]) : 0.f);
+    sdlv[e] = gl + (hb.eps ? s * ep * 0.5f * expf(0.5f * lv) : 0.f);
   }
   __syncthreads();
-  stamp();
-  // pooled -> LDS (over the dz partials)
-  float* spool = su;
-  for (int e = tid; e < N * C; e += LAT_BT) spool[e] = gfc(hb.pooled)[e];
-  __syncthreads();
-  stamp();
 
-  // phase 4: heads. dW[jj][c] (+)= sum_n d[n][jj] pooled[n][c]; db[jj] (+)= sum_n d[n][jj]
-  for (int e0 = tid; e0 < 2 * L * C; e0 += LAT_RMW * LAT_BT) {
-    gfloat* dst[LAT_RMW];
-    float old[LAT_RMW], s[LAT_RMW];
+  // heads: dW[jj][c] (+)= sum_n d[n][jj] pooled[n][c]
 #pragma unroll
-    for (int u = 0; u < LAT_RMW; ++u) {
-      const int e = e0 + u * LAT_BT;
-      dst[u] = nullptr;
-      old[u] = 0.f;
-      s[u] = 0.f;
-      if (e >= 2 * L * C) continue;
-      const int h = e / (L * C), r = e - h * (L * C), jj = r / C, c = r - jj * C;
-      const float* d = h ? sdlv : sdmu;
-      gfloat* dw = gf(h ? hb.dw_lv : hb.dw_mu);
-      if (!dw) continue;
-      dst[u] = dw + r;
-      if (hb.grad_acc) old[u] = dw[r];
-      for (int n = 0; n < N; ++n) s[u] += d[n * L + jj] * spool[n * C + c];
-    }
-#pragma unroll
-    for (int u = 0; u < LAT_RMW; ++u)
-      if (dst[u]) *dst[u] = old[u] + s[u];
-  }
-  for (int e = tid; e < 2 * L; e += LAT_BT) {
-    const int h = e / L, jj = e - h * L;
-    const float* d = h ? sdlv : sdmu;
-    gfloat* db = gf(h ? hb.db_lv : hb.db_mu);
-    if (!db) continue;
+  for (int k = 0; k < LH_ODW; ++k) {
+    const int e = tid + k * LB_T;
+    if (e >= 2 * L * LH_CW) break;
+    const int h = e / (L * LH_CW), r = e - h * L * LH_CW, jj = r / LH_CW, cc = r % LH_CW;
+    gfloat* d = h ? dwl : dwm;
+    if (!d) continue;
+    const float* dv = h ? sdlv : sdmu;
     float s = 0.f;
-    for (int n = 0; n < N; ++n) s += d[n * L + jj];
-    db[jj] = hb.grad_acc ? db[jj] + s : s;
+    for (int n = 0; n < N; ++n) s += dv[n * L + jj] * spool[n * LH_CW + cc];
+    d[(int64_t)jj * C + c0 + cc] = odw[k] + s;
   }
-  // dpooled[n][c] = sum_jj w_mu[jj][c] dmu[n][jj] + w_lv[jj][c] dlv[n][jj]:
-  // a thread per (c, 8-sample group), the 2L weight loads in flight in 8s
-  for (int e = tid; e < C * ((N + 7) / 8); e += LAT_BT) {
-    const int c = e % C, n0 = (e / C) * 8;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int j0 = 0; j0 < L; j0 += 8) {
-      float wm[8], wl[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        wm[u] = j0 + u < L ? gfc(hb.w_mu)[(int64_t)(j0 + u) * C + c] : 0.f;
-        wl[u] = j0 + u < L ? gfc(hb.w_lv)[(int64_t)(j0 + u) * C + c] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (j0 + u >= L) break;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (n0 + k < N) acc[k] += wm[u] * sdmu[(n0 + k) * L + j0 + u] + wl[u] * sdlv[(n0 + k) * L + j0 + u];
-      }
+  // dpooled[n][c] = sum_jj w_mu[jj][c] dmu[n][jj] + w_lv[jj][c] dlv[n][jj]
+  for (int e = tid; e < N * LH_CW; e += LB_T) {
+    const int n = e / LH_CW, cc = e % LH_CW;
+    float acc = 0.f;
+    for (int jj = 0; jj < L; ++jj) acc += swm[jj * LH_CW + cc] * sdmu[n * L + jj] + swl[jj * LH_CW + cc] * sdlv[n * L + jj];
+    gf(hb.dpooled)[(int64_t)n * C + c0 + cc] = acc;
+  }
+  // db[jj] (+)= sum_n d[n][jj]
+  if (blockIdx.x == 0) {
+    for (int e = tid; e < 2 * L; e += LB_T) {
+      const int h = e / L, jj = e - h * L;
+      gfloat* db = gf(h ? hb.db_lv : hb.db_mu);
+      if (!db) continue;
+      const float* dv = h ? sdlv : sdmu;
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += dv[n * L + jj];
+      db[jj] = hb.grad_acc ? db[jj] + s : s;
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (n0 + k < N) gf(hb.dpooled)[(int64_t)(n0 + k) * C + c] = acc[k];
   }
-  stamp();
 }
 
 }  // namespace
@@ -652,8 +608,7 @@ extern "C" int vu_latent_fwd(const VuLatentJob* jobs, int njobs, const float* z,
 extern "C" int64_t vu_latent_part_floats(int N, int co) { return (int64_t)N * LAT_SPLITS * co; }
 
 extern "C" int vu_latent_bwd_supported(int N, int L, int64_t sum_co, int C) {
-  return N >= 1 && N <= LAT_MAXN && L >= 1 && L <= 64 && sum_co >= 0 &&
-         latent_bwd_lds_floats(N, L, (int)sum_co, C) * (int64_t)sizeof(float) <= VU_LATENT_BWD_MAX_LDS;
+  return N >= 1 && N <= LAT_MAXN && L >= 1 && L <= 64 && sum_co >= 0 && C >= LH_CW && C % LH_CW == 0;
 }
 
 extern "C" int vu_latent_bwd_sums(const VuLatentJob* jobs, int njobs, int N, int dtype, void* stream) {
@@ -670,13 +625,16 @@ extern "C" int vu_latent_bwd_sums(const VuLatentJob* jobs, int njobs, int N, int
   return (int)hipGetLastError();
 }
 
+// the dz partials of the latent_bwd_bn blocks: at most sum_co / 8 blocks
+// (co = 8 * 2^k: ceil(co / 32) <= co / 8)
 extern "C" int64_t vu_latent_bwd_workspace_bytes(int N, int L, int64_t sum_co) {
-  return ((int64_t)N * sum_co + 3LL * N * L) * (int64_t)sizeof(float);
+  return (sum_co / 8 + 1) * N * L * (int64_t)sizeof(float);
 }
 
 extern "C" int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentHeads* heads, int N, int L,
                              float* workspace, void* stream) {
   if (N < 1 || N > LAT_MAXN || L < 1 || L > 64) return (int)hipErrorInvalidValue;
+  if (heads->C < LH_CW || heads->C % LH_CW) return (int)hipErrorInvalidValue;
   LatentJobs J;
   int64_t fb = 0, sb = 0;
   if (njobs > 0) {
@@ -684,11 +642,14 @@ extern "C" int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentH
   } else if (njobs < 0) {
     return (int)hipErrorInvalidValue;
   }
-  int64_t ct = 0;
-  for (int j = 0; j < njobs; ++j) ct += J.j[j].co;
-  const int64_t shm = latent_bwd_lds_floats(N, L, (int)ct, heads->C) * (int64_t)sizeof(float);
-  if (shm > VU_LATENT_BWD_MAX_LDS) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(latent_bwd_kernel, dim3(1), dim3(LAT_BT), (size_t)shm, (hipStream_t)stream, J, njobs, *heads, N,
-                     L, workspace);
+  int nbp = 0;
+  for (int j = 0; j < njobs; ++j) nbp += lb_blocks(J.j[j].co);
+  if (nbp > 0 && workspace == nullptr) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (nbp > 0)
+    hipLaunchKernelGGL(latent_bwd_bn_kernel, dim3((unsigned)nbp), dim3(LB_T),
+                       (size_t)(lb_lds_floats(N, L) * sizeof(float)), st, J, njobs, heads->z, N, L, workspace);
+  hipLaunchKernelGGL(latent_bwd_heads_kernel, dim3((unsigned)(heads->C / LH_CW)), dim3(LB_T),
+                     (size_t)(lh_lds_floats(N, L) * sizeof(float)), st, *heads, N, L, workspace, nbp);
   return (int)hipGetLastError();
 }

@@ -409,7 +409,6 @@ def decoder_bwd(M, blk, saved, dout, z=None):
 # same again backwards).
 # ---------------------------------------------------------------------------
 LATENT_VECTORS = True  # A/B switch: False = the round-3 map path
-LATENT_TIMING = None  # diagnostics: int64 device tensor for vu_latent_bwd's phase timestamps
 
 
 def _consumer_ok(M, seq):
@@ -564,11 +563,9 @@ def latent_bwd(M, model, cons, z, eps, logvar, pooled, dmu, dlogvar):
     h.dw_mu, h.db_mu, h.dw_lv, h.db_lv = (K.ptr(g) for g, _ in sinks)
     h.dpooled, h.C, h.grad_acc = dpooled.data_ptr(), pooled.shape[1], 1 if accs == {True} else 0
     sum_co = sum(c.conv.out_channels for c in cons)
-    # the kernel keeps its vectors in LDS; the workspace argument is only used
-    # by the phase-timing diagnostics (LATENT_TIMING: a >= 8-element int64
-    # device tensor that receives the phase-boundary timestamps)
-    ws = LATENT_TIMING
-    K.call("vu_latent_bwd", arr, len(cons), C.byref(h), N, L, K.ptr(ws) if ws is not None else None, K.stream())
+    ws = K.workspace_f32(K.query("vu_latent_bwd_workspace_bytes", N, L, sum_co), dev)  # dz partials
+    keep.append(ws)
+    K.call("vu_latent_bwd", arr, len(cons), C.byref(h), N, L, K.ptr(ws), K.stream())
     ps = [hm.weight, hm.bias, hl.weight, hl.bias]
     for c in cons:
         ps += [c.conv.weight, c.conv.bias, c.bn.weight, c.bn.bias]
