@@ -23,8 +23,9 @@
 //     permuted order, so a lane's accumulators hold 16 consecutive output
 //     channels of one pixel, stored straight from registers (no LDS staging,
 //     no barrier; 64 contiguous bytes per pixel and store), with the BatchNorm partial
-//     statistics of each wave's 64 pixels from DPP row sums (same contract as
-//     the other kernels: per-tile sum + centered M2 of the rounded values);
+//     statistics of each wave's 64 pixels from a DPP butterfly transpose-
+//     reduce (same contract as the other kernels: per-tile sum + centered M2
+//     of the rounded values);
 //   * LDS images are conflict-free for every fragment read: weight rows XOR
 //     their 16-byte pieces with wswz(row); halo pixel P keeps its piece k at
 //     position (k + 2 * ((P >> 2) & 1)) & 3, which spreads the 16 lanes of
@@ -71,11 +72,60 @@ VU_DEV void raw_barrier() {
 // lane group touches 16 distinct 4-bank groups (checked for all j, tap, c)
 VU_DEV int wswz(int n) { return (n + (n >> 2)) & 7; }
 
-template <int R>
-VU_DEV float ror_add(float v) {
-  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xf, 0xf, false));
+
+// ---- butterfly transpose-reduce over the 16 lanes of a DPP row ----------
+// v[k] (16 slots per lane) -> lane m of the row holds the sum over the row's
+// lanes of slot m: each step pairs lanes across one lane bit and halves the
+// array (15 lane moves instead of 16 four-step rotate-add reductions, 64)
+template <int CTRL>
+VU_DEV float dmov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_add<8>(v)))); }
+VU_DEV float lx1(float v) { return dmov<0xB1>(v); }               // lane ^ 1
+VU_DEV float lx2(float v) { return dmov<0x4E>(v); }               // lane ^ 2
+VU_DEV float lx4(float v) { return dmov<0x1B>(dmov<0x141>(v)); }  // lane ^ 4
+VU_DEV float lx8(float v) { return dmov<0x128>(v); }              // lane ^ 8 (row_ror:8)
+
+VU_DEV float bfly16_reduce(const float (&v)[16], int lane) {
+  const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+  float x[8], y[4], z[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = (b3 ? v[k + 8] : v[k]) + lx8(b3 ? v[k] : v[k + 8]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) y[k] = (b2 ? x[k + 4] : x[k]) + lx4(b2 ? x[k] : x[k + 4]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) z[k] = (b1 ? y[k + 2] : y[k]) + lx2(b1 ? y[k] : y[k + 2]);
+  return (b0 ? z[1] : z[0]) + lx1(b0 ? z[0] : z[1]);
+}
+
+// inverse: lane m of a row holds the value of slot m -> every lane gets all 16
+VU_DEV void bfly16_bcast(float m, int lane, float (&out)[16]) {
+  const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4, b3 = lane & 8;
+  float z[2], y[4], x[8];
+  {
+    const float q = lx1(m);
+    z[0] = b0 ? q : m;
+    z[1] = b0 ? m : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float q = lx2(z[k]);
+    y[k] = b1 ? q : z[k];
+    y[k + 2] = b1 ? z[k] : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float q = lx4(y[k]);
+    x[k] = b2 ? q : y[k];
+    x[k + 4] = b2 ? y[k] : q;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float q = lx8(x[k]);
+    out[k] = b3 ? q : x[k];
+    out[k + 8] = b3 ? x[k] : q;
+  }
+}
 
 // RELU: the epilogue ReLU (VuGemmFwd.relu) as a separate instantiation: the
 // runtime block spilled the statistics variant (+16 % in the training step)
@@ -232,28 +282,30 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) epi_relu(acc[i]);
     if (STATS) {
-      // per-wave (sum, centered M2) of its 64 pixels; lane (kg, l16) keeps
-      // channel 16*kg + l16 = lane: one store per statistic
-      float ms = 0.f, mq = 0.f;
+      // per-wave (sum, centered M2) of its 64 pixels: slot 4j + r of a lane
+      // is channel 16*kg + 4j + r; after the butterfly lane (kg, l16) holds
+      // slot l16, i.e. channel lane: one store per statistic
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[4 * j + r] = (acc[0][j][r] + acc[1][j][r]) + (acc[2][j][r] + acc[3][j][r]);
+      const float ms = bfly16_reduce(v, lane);
+      float mb[16];
+      bfly16_bcast(ms * (1.f / 64), lane, mb);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float sv = (acc[0][j][r] + acc[1][j][r]) + (acc[2][j][r] + acc[3][j][r]);
-          sv = row16_sum(sv);
-          const float mean = sv * (1.f / 64);
           float q = 0.f;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float d = acc[i][j][r] - mean;
+            const float d = acc[i][j][r] - mb[4 * j + r];
             q += d * d;
           }
-          q = row16_sum(q);
-          if (l16 == j * 4 + r) {
-            ms = sv;
-            mq = q;
-          }
+          v[4 * j + r] = q;
         }
+      const float mq = bfly16_reduce(v, lane);
       const int64_t so = (int64_t)(t * 8 + wid) * p.ncol + lane;
       p.stat_sum[so] = ms;
       p.stat_m2[so] = mq;
