@@ -332,6 +332,14 @@ def test_conv3x3_splitk_auto_32x32_level():
     _check_halo_conv((2, [512], 32, 32, 1024), (128,))
 
 
+def test_conv3x3_splitk_auto_832_columns():
+    """the production dispatch of the UNetResNet decoder block-1 conv1 input
+    gradient (512 -> 832 padded concat channels at 32x32, B=8): 64-column
+    ping-pong tiles split over K (the 128/256-column tiles do not divide 832),
+    and its forward direction 832 -> 512 on the 256-column split."""
+    _check_halo_conv((8, [512], 32, 32, 832), (128,), kernel=4)
+
+
 IMAGE_CASES = [
     # (N, H, W, cout): the 8-channel (packed 3-channel image) conv kernel (conv_image.hip)
     (2, 16, 64, 64),

@@ -19,7 +19,9 @@ from vaeunet_amd.engine import w3x3_fwd, w3x3_dgrad  # noqa: E402
 B = 8
 LAYERS = [("layer1", 64, 64, 128), ("layer2", 128, 128, 64), ("layer3", 256, 256, 32), ("layer4", 512, 512, 16),
           # UNet(3,2) small grids: down4 conv1 / conv2, up1 conv2
-          ("unet.down4a", 512, 1024, 32), ("unet.down4b", 1024, 1024, 32), ("unet.up1b", 512, 512, 64)]
+          ("unet.down4a", 512, 1024, 32), ("unet.down4b", 1024, 1024, 32), ("unet.up1b", 512, 512, 64),
+          # UNetResNet decoder block 1 (32^2): the conv1 input gradient (512 -> 832 padded concat channels)
+          ("dec1.conv1_dgrad", 512, 832, 32)]
 
 
 def timeit(fn, reps=20):

@@ -738,6 +738,11 @@ Plan plan(const VuGemmFwd& p) {
   } else if (tiles_ok<128>(p)) {
     bn = 128;
     blocks = tile_count<128>(p);
+  } else if (p.ncol % 128 != 0 && tiles_ok<64>(p)) {
+    // 64- but not 128-multiple column counts (the 832-column decoder concat
+    // gradient at 32^2: it fell to the v2 small-grid gather, 377 TFLOP/s)
+    bn = 64;
+    blocks = tile_count<64>(p);
   } else {
     return r;
   }

@@ -361,7 +361,7 @@ int cu_count6() {
   return n;
 }
 
-int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 2 tiles per CU), k >= 2 on with the grid capped at k
+int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 1 tile per CU), k >= 2 on with the grid capped at k
 
 }  // namespace
 
@@ -379,7 +379,9 @@ int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype) {
   const int64_t M = (int64_t)g.N * g.H * g.W;
   if (M >= ((int64_t)1 << 31)) return 0;
   const int64_t T = M / (TH * TW);
-  if (g_v6 == 1 && T < 2 * (int64_t)cu_count6()) return 0;  // needs a tile stream per block
+  // one tile per block at least (the ResNet34 layer1 at 128^2: 256 tiles,
+  // 3-4 % faster than the v3 halo kernel; tools/enc_bench.py, gpurun_out/r4t)
+  if (g_v6 == 1 && T < (int64_t)cu_count6()) return 0;
   return 64;
 }
 
