@@ -218,6 +218,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     segment and one 32-MFMA segment per step (2 barriers) instead of two
  *     halves (0; bit-identical outputs) */
 #define VU_TUNE_PP_FULL 27
+/*   VU_TUNE_W2_BIG: 1 = 256 x 256 output tiles for the 1x1 / ConvT weight
+ *     gradients with both dimensions >= 256 (0 = 128 x 256) */
+#define VU_TUNE_W2_BIG 28
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was

@@ -635,7 +635,9 @@ def _row_tile_args(K, srcs, wmat, ncol, out, gather=None):
 @pytest.mark.parametrize("case", [(4, 64, 32, 32, 32), (4, 128, 32, 32, 64), (2, 256, 32, 32, 128),
                                   (1, 48, 16, 16, 24),
                                   (16, 64, 64, 64, 32),    # bf16 v2: 1-step K ring, 32-channel K tail
-                                  (16, 128, 64, 64, 64)])
+                                  (16, 128, 64, 64, 64),
+                                  (2, 64, 8, 256, 32),     # wgrad steps inside 256-wide rows (row wraps)
+                                  (2, 256, 4, 128, 128)])  # 128 x 256 wgrad tiles, 64-pixel steps, row wraps
 def test_conv1x1_fwd_dgrad_wgrad(mode, case):
     """1x1 conv (attention gate W_g / W_x, unet_parts.py:10-16): forward with
     bias + BN statistics, accumulating input gradient, weight gradient (the
@@ -707,6 +709,46 @@ def test_conv_transpose(mode, case):
     gb = torch.zeros(co, device=DEV)
     K.chan_sum(dua, gb, False, d, window=(py, px, 2 * h, 2 * w))
     _close(gb, br.grad, mode, what="convT bias grad", sabs=ba.grad, u=2.0 ** -23)
+
+
+TUNE_W2_BIG = 28
+
+
+@pytest.mark.parametrize("case", [("convT", 4, 512, 16, 16, 256), ("convT", 2, 256, 32, 32, 128),
+                                  ("1x1", 8, 512, 16, 16, 256), ("1x1", 2, 384, 24, 20, 320)])
+def test_wgrad_v2_big_tiles(case):
+    """the 256 x 256-tile, 4-slot-ring variant of the v2 weight gradient
+    (VU_TUNE_W2_BIG) on ConvTranspose2d(k2,s2) and 1x1 problems with both
+    gradient dimensions >= 256 (partial edge tiles included) vs torch fp32 of
+    the bf16 operands; the split count comes from the production heuristic."""
+    K, E = _k()
+    kind, N, ci, h, w, co = case
+    g = torch.Generator().manual_seed(29)
+    d = _code("bf16")
+    x = torch.randn(N, ci, h, w, generator=g).to(torch.bfloat16).float()
+    _tune((TUNE_W2_BIG, 1))
+    try:
+        if kind == "convT":
+            du = torch.randn(N, co, 2 * h, 2 * w, generator=g).to(torch.bfloat16).float()
+            gw = torch.zeros(ci, co, 2, 2, device=DEV)
+            K.gemm_wgrad(K.gather1x1([_act(x, "bf16")]), K.gather_convT(_act(du, "bf16"), N, h, w, 0, 0), ci, 4 * co,
+                         gw, E.convT_layout(gw), d, False)
+            xr = x.clone().requires_grad_(True)
+            wr = torch.zeros(ci, co, 2, 2, requires_grad=True)
+            F.conv_transpose2d(xr, wr, None, stride=2).backward(du)
+            xa = x.abs()
+            wa = torch.zeros(ci, co, 2, 2, requires_grad=True)
+            F.conv_transpose2d(xa, wa, None, stride=2).backward(du.abs())
+            _close(gw, wr.grad, "bf16", what="convT wgrad (256x256 tiles)", sabs=wa.grad, u=2.0 ** -23)
+        else:
+            du = torch.randn(N, co, h, w, generator=g).to(torch.bfloat16).float()
+            gw = torch.zeros(co, ci, 1, 1, device=DEV)
+            K.gemm_wgrad(K.gather1x1([_act(du, "bf16")]), K.gather1x1([_act(x, "bf16")]), co, ci, gw,
+                         E.conv_layout(gw), d, False)
+            _close(gw, torch.nn.grad.conv2d_weight(x, (co, ci, 1, 1), du), "bf16", what="1x1 wgrad (256x256 tiles)",
+                   u=2.0 ** -23, sabs=torch.nn.grad.conv2d_weight(x.abs(), (co, ci, 1, 1), du.abs()))
+    finally:
+        _tune((TUNE_W2_BIG, 0))
 
 
 @pytest.mark.parametrize("mode", ["f32", "bf16"])

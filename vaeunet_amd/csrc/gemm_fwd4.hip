@@ -853,6 +853,7 @@ int gemm_fwd_v5_tune(int key, int value);  // gemm_fwd5.hip
 int gemm_fwd_v6_tune(int key, int value);  // gemm_fwd6.hip
 int gemm_fwd_v7_tune(int key, int value);  // gemm_fwd7.hip
 int gemm_wgrad_v3_tune(int key, int value);  // gemm_wgrad3.hip
+int gemm_wgrad_v2_tune(int key, int value);  // gemm_wgrad2.hip
 int bn_tune(int key, int value);           // bn.hip
 int attn_tune(int key, int value);         // attention.hip
 extern int g_tune_gen;                     // gemm_fwd.hip
@@ -892,7 +893,7 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
   }
   if (conv_fp8_tune(key, value) == 0 || gemm_stream_tune(key, value) == 0 || gemm_fwd_v2_tune(key, value) == 0 ||
       gemm_fwd_v5_tune(key, value) == 0 || gemm_fwd_v6_tune(key, value) == 0 || gemm_fwd_v7_tune(key, value) == 0 ||
-      gemm_wgrad_v3_tune(key, value) == 0 || bn_tune(key, value) == 0 ||
+      gemm_wgrad_v3_tune(key, value) == 0 || gemm_wgrad_v2_tune(key, value) == 0 || bn_tune(key, value) == 0 ||
       attn_tune(key, value) == 0)
     return 0;
   return (int)hipErrorInvalidValue;

@@ -83,7 +83,20 @@ VU_DEV Col decode_col(const VuGather& g, int col, int ncols) {
   return d;
 }
 
-template <int BI, int BJ, int WI, int WJ, int BMR>
+// wait until at most K*NL vector-memory operations are outstanding, K the
+// number of younger ring stages in flight (a runtime 0 .. NS-1)
+template <int NL, int K>
+VU_DEV void vm_wait_stages(int k) {
+  if constexpr (K <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (k >= K) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K * NL) : "memory");
+    else vm_wait_stages<NL, K - 1>(k);
+  }
+}
+
+// NS: LDS ring slots (NS - 1 stages in flight while a step computes)
+template <int BI, int BJ, int WI, int WJ, int BMR, int NS = 3>
 __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWgrad p) {
   constexpr int NT = WI * WJ * 64;
   constexpr int RBP = BI * 2, RBQ = BJ * 2;          // LDS row bytes
@@ -92,7 +105,7 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
   constexpr int TI = BI / WI / 16, TJ = BJ / WJ / 16;
   constexpr int STAGE = BMR * (RBP + RBQ);
   static_assert(LI >= 1 && LJ >= 1, "tile too small");
-  constexpr int NSTAGE = 3;  // LDS ring, DMA two steps ahead
+  constexpr int NSTAGE = NS;  // LDS ring, DMA NS - 1 steps ahead
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
   const VuGather& gp = p.p;
@@ -157,9 +170,63 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     return d.base + (((int64_t)n * g.Hs + hs) * g.Ws + ws) * d.stride;
   };
 
+  // Linear gathers (every 1x1 and unpadded ConvT operand): no tap reads
+  // outside the source image and Hs == sy * H, with W | BMR or BMR | W and
+  // the split starting on a step boundary.  Then each DMA slot's source
+  // pointer advances per step by a fixed increment -- BMR / W source rows,
+  // or BMR pixels within a row and a row change every W / BMR steps
+  // (block-uniform) -- instead of the per-step decode + 64-bit address
+  // arithmetic + bounds branches (~290 VALU per step and wave, which left the
+  // MFMA pipe idle most of the step).
+  auto linear = [&](const VuGather& g) {
+    if (g.oy < 0 || g.ox < 0 || g.dy < 0 || g.dx < 0 || g.Hs != g.H * g.sy) return false;
+    if ((g.H - 1) * g.sy + (g.R - 1) * g.dy + g.oy >= g.Hs) return false;
+    if ((g.W - 1) * g.sx + (g.S - 1) * g.dx + g.ox >= g.Ws) return false;
+    return BMR % g.W == 0 || g.W % BMR == 0;
+  };
+  const bool lin = linear(gp) && linear(gq) && mbeg % BMR == 0;
+  const bool multirow = BMR % gp.W == 0;  // a step covers BMR / W whole rows
+  int wcnt = (int)(mbeg % gp.W);          // column of the step start (BMR | W case)
+  const bf16_t* pptr[LI];
+  const bf16_t* qptr[LJ];
+  int pinc[LI], pwrap[LI], qinc[LJ], qwrap[LJ];
+  auto lin_init = [&](const VuGather& g, const Col& d, int n, int h, int w, const bf16_t*& ptr, int& inc,
+                      int& wrap) {
+    ptr = d.ok ? d.base + (((int64_t)n * g.Hs + h * g.sy + d.r * g.dy + g.oy) * g.Ws + w * g.sx + d.s * g.dx + g.ox) *
+                               d.stride
+               : nullptr;
+    const int64_t row = (int64_t)g.sy * g.Ws;  // source pixels per grid row
+    inc = (int)((multirow ? (BMR / g.W) * row : (int64_t)BMR * g.sx) * d.stride);
+    wrap = (int)((multirow ? (BMR / g.W) * row : row - (int64_t)(g.W - BMR) * g.sx) * d.stride);
+  };
+  if (lin) {
+#pragma unroll
+    for (int k = 0; k < LI; ++k) lin_init(gp, pcd[k], pn[k], ph[k], pw[k], pptr[k], pinc[k], pwrap[k]);
+#pragma unroll
+    for (int k = 0; k < LJ; ++k) lin_init(gq, qcd[k], qn[k], qh[k], qw[k], qptr[k], qinc[k], qwrap[k]);
+  }
+
   auto stage = [&](int64_t mb, int buf) {
     char* Pb = smem + buf * STAGE;
     char* Qb = Pb + BMR * RBP;
+    if (lin) {
+      wcnt += BMR;
+      const bool wrapped = wcnt >= gp.W;  // block-uniform
+      if (wrapped) wcnt -= gp.W;
+#pragma unroll
+      for (int k = 0; k < LI; ++k) {
+        const void* s = (pptr[k] != nullptr && mb + prow[k] < mend) ? (const void*)pptr[k] : zp;
+        __builtin_amdgcn_global_load_lds(s, (lds_void*)(Pb + (k * NT + wid * 64) * 16), 16, 0, 0);
+        if (pptr[k] != nullptr) pptr[k] += wrapped ? pwrap[k] : pinc[k];
+      }
+#pragma unroll
+      for (int k = 0; k < LJ; ++k) {
+        const void* s = (qptr[k] != nullptr && mb + qrow[k] < mend) ? (const void*)qptr[k] : zp;
+        __builtin_amdgcn_global_load_lds(s, (lds_void*)(Qb + (k * NT + wid * 64) * 16), 16, 0, 0);
+        if (qptr[k] != nullptr) qptr[k] += wrapped ? qwrap[k] : qinc[k];
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < LI; ++k) {
       const void* s = src_of(gp, pcd[k], pn[k], ph[k], pw[k], mb + prow[k] < mend);
@@ -190,17 +257,17 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
   // kernels are HBM/L2-latency bound (SQ_WAIT_ANY 65 % with one stage in
   // flight at the wait), so the bytes in flight are what sets the rate.
   constexpr int NL = LI + LJ;
-  if (nsteps > 0) stage(mbeg, 0);
-  if (nsteps > 1) stage(mbeg + BMR, 1);
+#pragma unroll
+  for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
+    if (nsteps > s0) stage(mbeg + (int64_t)s0 * BMR, s0);
   const int g4 = lane >> 4, li = lane & 15, qd = li >> 2, pp = li & 3;
   for (int st = 0; st < nsteps; ++st) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    const bool more = st + 2 < nsteps;
-    if (more) stage(mbeg + (int64_t)(st + 2) * BMR, (st + 2) % NSTAGE);
-    if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL) : "memory");
-    else if (st + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (st + NSTAGE - 1 < nsteps) stage(mbeg + (int64_t)(st + NSTAGE - 1) * BMR, (st + NSTAGE - 1) % NSTAGE);
+    // stage st has landed once only the younger stages may be outstanding
+    const int younger = nsteps - 1 - st < NSTAGE - 1 ? nsteps - 1 - st : NSTAGE - 1;
+    vm_wait_stages<NL, NSTAGE - 1>(younger);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int cur = st % NSTAGE;
@@ -261,16 +328,32 @@ __global__ __launch_bounds__(WI * WJ * 64, 1) void gemm_wgrad_v2_kernel(VuGemmWg
     }
 }
 
-template <int BI, int BJ, int WI, int WJ, int BMR>
+template <int BI, int BJ, int WI, int WJ, int BMR, int NS = 3>
 int launch(const VuGemmWgrad& p, hipStream_t st) {
   int itiles = (p.ni + BI - 1) / BI, jtiles = (p.nj + BJ - 1) / BJ;
   int64_t nblk = (int64_t)itiles * jtiles * p.splits;
   if (nblk <= 0) return 0;
-  hipLaunchKernelGGL((gemm_wgrad_v2_kernel<BI, BJ, WI, WJ, BMR>), dim3((unsigned)nblk), dim3(WI * WJ * 64), 0, st, p);
+  hipLaunchKernelGGL((gemm_wgrad_v2_kernel<BI, BJ, WI, WJ, BMR, NS>), dim3((unsigned)nblk), dim3(WI * WJ * 64), 0, st,
+                     p);
   return (int)hipGetLastError();
 }
 
+// VU_TUNE_W2_BIG: 256 x 256 output tiles (32 pixels per step, 4-slot ring)
+// for the large 1x1 / ConvT weight gradients (both dims >= 256): 1.5x the
+// MFMA work per LDS byte of the 128 x 256 tile, whose blocks wait on the
+// L2 -> LDS feed (~16 GB/s per CU on the UNet ConvT gradients)
+int g_w2_big = 0;
+bool big_tile(const VuGemmWgrad& p) { return g_w2_big && p.ni >= 256 && p.nj >= 256; }
+
 }  // namespace
+
+int gemm_wgrad_v2_tune(int key, int value) {
+  if (key == VU_TUNE_W2_BIG) {
+    g_w2_big = value;
+    return 0;
+  }
+  return -1;
+}
 
 // Output tile (BI, BJ) of the v2 kernel for this problem, or 0 if it does not apply.
 int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
@@ -287,6 +370,7 @@ int gemm_wgrad_v2_tile(const VuGemmWgrad& p, int dtype, int* bi, int* bj) {
   // instead of streaming zero columns through a 256-wide one
   if (p.ni <= 32 && p.nj <= 64) { *bi = 32; *bj = 64; return 1; }
   if (p.ni <= 64 && p.nj <= 128) { *bi = 64; *bj = 128; return 1; }
+  if (big_tile(p)) { *bi = 256; *bj = 256; return 1; }
   *bi = p.ni <= 64 ? 64 : 128;
   *bj = 256;
   return 1;
@@ -296,5 +380,6 @@ int gemm_wgrad_v2_launch(const VuGemmWgrad& p, hipStream_t st) {
   if (p.ni <= 32 && p.nj <= 64) return launch<32, 64, 2, 4, 128>(p, st);
   if (p.ni <= 64 && p.nj <= 128) return launch<64, 128, 2, 4, 128>(p, st);
   if (p.ni <= 64) return launch<64, 256, 1, 8, 64>(p, st);
+  if (big_tile(p)) return launch<256, 256, 2, 4, 32, 4>(p, st);
   return launch<128, 256, 2, 4, 64>(p, st);
 }
