@@ -32,12 +32,24 @@ LAYERS = [
 
 
 def timeit(fn, reps):
+    """GPU time per call: the calls are captured in one HIP graph and replayed
+    (timed eagerly, the Python + ctypes enqueue -- the statistics buffers'
+    allocation included -- inflated the shorter launches).  Note: with
+    statistics every captured call allocates fresh partial buffers, and the
+    replay then shows inter-kernel gaps the training step does not have
+    (down3.2: kernel durations equal under rocprofv3, graph time +17 us);
+    compare kernel durations (rocprofv3 --kernel-trace) for the epilogue cost."""
     fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    g.replay()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps
@@ -72,10 +84,11 @@ def main():
         fl = 2.0 * B * H * H * co * 9 * ci
         line = f"{name:8s} {ci:5d}->{co:5d} @{H:3d}"
         for kind in kinds:
-            if kind == "fwd":
+            if kind in ("fwd", "fwdnostats"):
                 y = K.empty_act(B, co, H, H, torch.bfloat16, dev)
                 wf = w3x3_fwd(w, d)
-                fn = lambda: K.gemm_fwd(K.gather3x3(srcs), wf, co, y, d, stats=True)  # noqa: E731
+                st = kind == "fwd"
+                fn = lambda: K.gemm_fwd(K.gather3x3(srcs), wf, co, y, d, stats=st)  # noqa: E731
             elif kind == "dgrad":
                 dx = K.empty_act(B, ci, H, H, torch.bfloat16, dev)
                 wd = w3x3_dgrad(w, d)

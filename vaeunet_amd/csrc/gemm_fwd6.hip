@@ -213,6 +213,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   u32x4 pend[8];
   bf16_t* pdst = nullptr;
   bool have_pend = false;
+  // ... and its BatchNorm partials (stored after the 8 output pieces: a store
+  // issued before the next group's halo DMA would be waited for with it)
+  float pst_sum = 0.f, pst_m2 = 0.f;
+  int64_t pst_so = 0;
+  auto store_stats = [&]() {
+    p.stat_sum[pst_so] = pst_sum;
+    p.stat_m2[pst_so] = pst_m2;
+  };
   auto store_pend = [&](int q) {  // piece q = 2 * fragment + half
     bf16_t* o = pdst + ((q >> 2) * (int64_t)W + ((q >> 1) & 1) * 16) * p.out_stride + 32 * (q & 1);
     *reinterpret_cast<u32x4*>(o) = pend[q];
@@ -227,6 +235,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     for (int tap = 0; tap < 9; ++tap) {
       const int ty = tap / 3, tx = tap - (tap / 3) * 3;
       if (tap < 8 && pending) store_pend(tap);
+      if (STATS && tap == 8 && pending) store_stats();
       u32x4 bf[4], af[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(wl + (boff[j] ^ cx) + tap * 128);
@@ -255,7 +264,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     // the halo was issued before the previous tile's 8 stores
     if (have_pend) {
       have_pend = false;
-      wait_vm<8>();
+      if (STATS) wait_vm<10>(); else wait_vm<8>();
     } else {
       wait_vm<0>();
     }
@@ -306,9 +315,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
           v[4 * j + r] = q;
         }
       const float mq = bfly16_reduce(v, lane);
-      const int64_t so = (int64_t)(t * 8 + wid) * p.ncol + lane;
-      p.stat_sum[so] = ms;
-      p.stat_m2[so] = mq;
+      pst_so = (int64_t)(t * 8 + wid) * p.ncol + lane;
+      pst_sum = ms;
+      pst_m2 = mq;
     }
     // stores: a lane holds channels 16kg .. 16kg+15 of its pixel (two 16-byte
     // pieces); a permlane16 + permlane32 swap regroups them so that store h
@@ -341,14 +350,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
     // the next group's halo was issued before this tile's statistics stores
-    if (STATS) wait_vm<2>(); else wait_vm<0>();
+    wait_vm<0>();
     raw_barrier();
     b ^= 1;
     t += G;
   }
-  if (have_pend)
+  if (have_pend) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) store_pend(q);
+    if (STATS) store_stats();
+  }
 }
 
 int cu_count6() {
