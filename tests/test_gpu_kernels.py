@@ -554,6 +554,31 @@ def test_conv3x3_c64_resident(case):
         _tune((TUNE_V6, 1))
 
 
+@pytest.mark.parametrize("co", [128, 192])
+def test_conv3x3_c64_column_slices(co):
+    """64 input channels, 128/192 outputs, no statistics (the input gradient of
+    the up4.1 128 -> 64 concat conv): one resident-weight launch per 64-column
+    slice, written into channel slices of a wider output (out_coff 64)."""
+    K, E = _k()
+    N, H, W = 2, 32, 64
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(N, 64, H, W, generator=g).to(torch.bfloat16).float()
+    w = torch.randn(co, 64, 3, 3, generator=g) / 24.0
+    wq = w.to(torch.bfloat16).float()
+    d = _code("bf16")
+    xs = _act(x, "bf16")
+    wf = E.w3x3_fwd(w.to(DEV), d)
+    _tune((TUNE_V6, 256))
+    try:
+        wide = K.empty_act(N, co + 64, H, W, torch.bfloat16, DEV)
+        assert K.query("vu_gemm_fwd_kernel", *_row_tile_args(K, [xs], wf, co, wide)) == 6
+        K.gemm_fwd(K.gather3x3([xs]), wf, co, wide, d, out_coff=64)
+        _close(wide[:, 64:], F.conv2d(x, wq, padding=1), "bf16", what="v6 column slices",
+               sabs=F.conv2d(x.abs(), wq.abs(), padding=1))
+    finally:
+        _tune((TUNE_V6, 1))
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 64, 64), (1, 96, 160), (64, 13, 13)])
 def test_conv_stem_7x7s2(N, H, W):
     """ResNet34 stem (7x7, stride 2, pad 3, 8 packed channels -> 64) on the

@@ -372,7 +372,7 @@ int cu_count6() {
   return n;
 }
 
-int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 1 tile per CU), k >= 2 on with the grid capped at k
+int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 2 tiles per CU), k >= 2 on with the grid capped at k
 
 }  // namespace
 
@@ -383,16 +383,18 @@ int gemm_fwd_v6_bm(const VuGemmFwd& p, int dtype) {
   if (g.R != 3 || g.S != 3 || g.sy != 1 || g.sx != 1 || g.dy != 1 || g.dx != 1 || g.oy != -1 || g.ox != -1 ||
       g.Hs != g.H || g.Ws != g.W)
     return 0;
-  if (g.nsrc != 1 || g.C != 64 || g.cend[0] != 64 || p.ncol != 64) return 0;
+  if (g.nsrc != 1 || g.C != 64 || g.cend[0] != 64) return 0;
+  // wider outputs without statistics (the input gradient of a 128 -> 64 concat
+  // conv, up4.1: 64 -> 128 channels at 512^2) as one launch per 64-column
+  // slice: K = 576 is too short for the ping-pong tiles (922 TFLOP/s there)
+  if (p.ncol != 64 && (p.ncol % 64 != 0 || p.ncol > 256 || p.stat_sum || p.bnb_part || p.bias)) return 0;
   if (g.H % TH != 0 || g.W % TW != 0) return 0;
   if (g.stride[0] % 8 != 0 || p.out_stride % 8 != 0 || p.out_coff % 8 != 0 || p.ldb % 8 != 0 || p.ldb < 576)
     return 0;
   const int64_t M = (int64_t)g.N * g.H * g.W;
   if (M >= ((int64_t)1 << 31)) return 0;
   const int64_t T = M / (TH * TW);
-  // one tile per block at least (the ResNet34 layer1 at 128^2: 256 tiles,
-  // 3-4 % faster than the v3 halo kernel; tools/enc_bench.py, gpurun_out/r4t)
-  if (g_v6 == 1 && T < (int64_t)cu_count6()) return 0;
+  if (g_v6 == 1 && T < 2 * (int64_t)cu_count6()) return 0;  // needs a tile stream per block
   return 64;
 }
 
@@ -412,6 +414,17 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
   int64_t grid = T < cu_count6() ? T : cu_count6();
   if (g_v6 >= 2 && grid > g_v6) grid = g_v6;
   if (p.bnb_part) return (int)hipErrorInvalidValue;
+  if (p.ncol > 64) {
+    // one launch per 64-column slice: weight rows and output channels offset
+    for (int c0 = 0; c0 < p.ncol; c0 += 64) {
+      VuGemmFwd q = p;
+      q.ncol = 64;
+      q.b = reinterpret_cast<const bf16_t*>(p.b) + (int64_t)c0 * p.ldb;
+      q.out_coff = p.out_coff + c0;
+      if (int e = gemm_fwd_v6_launch(q, st)) return e;
+    }
+    return 0;
+  }
   if (p.stat_sum)
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<true, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);

@@ -200,6 +200,9 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     st = None
     if stats:
         rows = g.N * g.H * g.W
+        # the row tile depends on whether statistics are requested (kernel
+        # choice): query with the statistics pointers set (placeholders)
+        a.stat_sum = a.stat_m2 = 1
         bm = query("vu_gemm_fwd_row_tile", C.byref(a), dtype)
         tiles = (rows + bm - 1) // bm
         psum = torch.empty((tiles, ncol), dtype=torch.float32, device=out.device)
