@@ -426,6 +426,18 @@ int vu_maxpool2_bwd(const void* x, int64_t xs, const void* dy, int64_t dys,
 int vu_bn_apply_maxpool2(const void* y, int64_t ys, void* a, int64_t as, void* pool, int64_t ps,
                          int N, int H, int W, int C, const float* scale, const float* shift,
                          int relu, int dtype, void* stream);
+/* BatchNorm(+ReLU) backward THROUGH that 2x2 max-pool: y the BN input, dp
+ * the gradient of the pooled output, add the skip gradient of a (or NULL);
+ * recomputes a, its first-max argmax and a's gradient per window (as
+ * vu_bn_apply_maxpool2 / vu_maxpool2_bwd store them) in a partial pass and an
+ * apply pass -> dx (gradient of y); dgamma/dbeta as vu_bn_bwd_reduce, coef
+ * [3][C] scratch, workspace vu_reduce_workspace_bytes(N*H*W, C). */
+int vu_bn_bwd_pool_supported(int H, int W, int C, int64_t ys, int64_t dps, int64_t adds, int64_t dxs);
+int vu_bn_bwd_pool(const void* y, int64_t ys, const void* dp, int64_t dps, const void* add, int64_t adds,
+                   int N, int H, int W, int C, const float* scale, const float* shift, const float* mean,
+                   const float* invstd, const float* gamma, int relu, int train, float* dgamma,
+                   float* dbeta, int accumulate, float* coef, float* workspace, void* dx, int64_t dxs,
+                   int dtype, void* stream);
 /* bilinear, align_corners=True, (Hi,Wi) -> (Ho,Wo) placed at (py,px) inside
  * a zero (Hp,Wp) canvas (F.pad of unet_parts.py:88-89 folded in). */
 int vu_upsample_fwd(const void* x, int64_t xs, int N, int Hi, int Wi, int C,

@@ -151,3 +151,59 @@ def test_bn_bwd_fused_matches_three_launch_path(case, dt):
     torch.testing.assert_close(db1, br.grad - 0.5, rtol=1e-3, atol=2e-2)
     torch.testing.assert_close(dx1.float(), xr.grad, **(dict(rtol=3e-2, atol=3e-2) if dt == torch.bfloat16
                                                        else dict(rtol=1e-3, atol=1e-4)))
+
+
+POOL_CASES = [
+    # (N, C, H, W, relu, train, skip gradient)
+    (2, 64, 32, 48, True, True, True),
+    (2, 128, 16, 16, True, True, False),
+    (1, 64, 8, 12, False, True, True),     # no ReLU between the BN and the pool
+    (2, 64, 6, 8, True, False, True),      # eval-mode statistics
+]
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("case", POOL_CASES)
+def test_bn_bwd_through_maxpool(case, dt):
+    """vu_bn_bwd_pool (the BN(+ReLU) backward read through the following 2x2
+    max-pool: activation, argmax and pool-input gradient recomputed per window)
+    vs the materialised path: vu_bn_apply_maxpool2's activation, vu_maxpool2_bwd
+    (+ skip gradient) and the BN backward -- the BN sees bit-identical dz, so
+    dgamma / dbeta agree to the summation order and dx to one rounding."""
+    K = _k()
+    from vaeunet_amd import _lib
+    N, C, H, W, relu, train, skip = case
+    d = _lib.BF16 if dt == torch.bfloat16 else _lib.F32
+    g = torch.Generator().manual_seed(17)
+    cl = torch.channels_last
+    y = (torch.randn(N, C, H, W, generator=g) + 0.2).to(dt).to(DEV).contiguous(memory_format=cl)
+    # ties in the pooled windows: repeat some values
+    y[:, :, 1::4, :] = y[:, :, 0::4, :]
+    dp = torch.randn(N, C, H // 2, W // 2, generator=g).to(dt).to(DEV).contiguous(memory_format=cl)
+    add = torch.randn(N, C, H, W, generator=g).to(dt).to(DEV).contiguous(memory_format=cl) if skip else None
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    yf = y.float()
+    mean, var = yf.mean((0, 2, 3)), yf.var((0, 2, 3), unbiased=False)
+    invstd = 1.0 / torch.sqrt(var + 1e-5)
+    coef = torch.stack([gamma * invstd, beta - mean * gamma * invstd, mean, invstd]).contiguous()
+    # the forward: activation + pool in one pass, as the engine runs it
+    act = torch.empty_like(y)
+    pooled = torch.empty_like(dp)
+    K.bn_apply_maxpool(y, act, pooled, coef, relu, d)
+    ws8 = K.pstride(add) if add is not None else 8
+    assert K.query("vu_bn_bwd_pool_supported", H, W, C, K.pstride(y), K.pstride(dp), ws8, K.pstride(y))
+    dg1, db1 = torch.full((C,), 0.25, device=DEV), torch.full((C,), -0.5, device=DEV)
+    dx1 = torch.empty_like(y)
+    K.bn_backward_pool(dp, add, y, coef, gamma, relu, dg1, db1, True, dx1, d, train=train)
+    da = torch.empty_like(y)
+    K.maxpool_bwd(act, dp, da, add, d)
+    dg2, db2 = torch.full((C,), 0.25, device=DEV), torch.full((C,), -0.5, device=DEV)
+    dx2 = torch.empty_like(y)
+    K.bn_backward(da, y, coef, gamma, relu, dg2, db2, True, dx2, d, train=train, fused=False)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dg1, dg2, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db1, db2, rtol=1e-5, atol=1e-4)
+    scale = float(dx2.float().abs().max())
+    err = float((dx1.float() - dx2.float()).abs().max())
+    assert err <= (2.0 ** -7 if dt == torch.bfloat16 else 1e-5) * scale, (err, scale)

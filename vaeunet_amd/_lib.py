@@ -119,6 +119,9 @@ _SIGS = {
                              _p]),
     "vu_bn_fwd_fused": (_i, [_p, _p, _i, _l, _l, _i, _p, _p, _p, _p, _p, _f, _f, _p, _p, _l, _p, _l, _p, _p,
                              _p, _l, _i, _i, _p]),
+    "vu_bn_bwd_pool_supported": (_i, [_i, _i, _i, _l, _l, _l, _l]),
+    "vu_bn_bwd_pool": (_i, [_p, _l, _p, _l, _p, _l, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i, _p, _p,
+                            _p, _l, _i, _p]),
     "vu_bn_bwd_reduce": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i,
                               _p, _p, _i, _p]),
     "vu_bn_bwd_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _i, _p, _l, _i, _p]),

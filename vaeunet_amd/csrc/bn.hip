@@ -482,6 +482,134 @@ __global__ void bn_apply_maxpool_kernel(const T* y, int64_t ys, T* a, int64_t as
   }
 }
 
+// ---- BatchNorm(+ReLU) backward THROUGH the 2x2 max-pool (round 4) ----------
+// The encoder DoubleConvs' BN2 output a = relu(BN(y)) feeds the next Down's
+// max-pool and the decoder's skip concat.  Its backward used to be: max-pool
+// backward (reads a, the skip gradient and the pooled gradient, writes the
+// full-size gradient of a), then the BN backward reduce (reads that gradient
+// and y) and apply (reads both again, writes dy): 8.25 full-size passes.  Here
+// neither a nor its gradient is touched: each pass recomputes, per 2x2
+// window, a = T(relu(fma(y, scale, shift))) exactly as vu_bn_apply_maxpool2
+// stored it, its first-max argmax, and the gradient of a as the max-pool
+// backward stored it, T(skip + [argmax] pooled) -- bit-identical inputs to
+// the BN backward -- from y, the skip gradient and the pooled gradient:
+// 5.5 passes.  A thread owns 8 channels of one pooled pixel (its window).
+struct PoolBnArgs {
+  const void* y; int64_t ys;       // BN input (the conv output), full size
+  const void* dp; int64_t dps;     // gradient of the pooled output
+  const void* add; int64_t adds;   // skip-connection gradient (full size) or null
+  int N, H, W, C;
+  const float* scale; const float* shift; const float* mean; const float* invstd;
+  int relu;
+  float* part;                     // partial pass: [nblk][2][C]
+  const float* coef;               // apply pass: k1, k2, k3 [3][C] (bn_bwd_final)
+  void* dx; int64_t dxs;           // apply pass: gradient of y
+};
+
+template <typename T, bool NT>
+VU_DEV void pool_window(const PoolBnArgs& r, int64_t q, int c, const float (&sc)[8], const float (&sf)[8],
+                        float (&yv)[4][8], float (&dz)[4][8], int64_t& p00) {
+  const int Wo = r.W >> 1, Ho = r.H >> 1;
+  const int j = (int)(q % Wo);
+  const int64_t t = q / Wo;
+  const int i = (int)(t % Ho), n = (int)(t / Ho);
+  p00 = ((int64_t)n * r.H + 2 * i) * r.W + 2 * j;
+  const T* y = reinterpret_cast<const T*>(r.y);
+  const T* ad = reinterpret_cast<const T*>(r.add);
+  Vec8<T> vy[4], va[4], vg;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t pix = p00 + (k >> 1) * r.W + (k & 1);
+    if (NT) vy[k].load_nt(y + pix * r.ys + c); else vy[k].load(y + pix * r.ys + c);
+    if (ad) { if (NT) va[k].load_nt(ad + pix * r.adds + c); else va[k].load(ad + pix * r.adds + c); }
+  }
+  vg.load(reinterpret_cast<const T*>(r.dp) + q * r.dps + c);
+  float best[8];
+  int arg[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      yv[k][e] = vy[k].get(e);
+      const float z = fmaf(yv[k][e], sc[e], sf[e]);
+      const float f = rnd<T>(r.relu ? fmaxf(z, 0.f) : z);  // the stored activation
+      if (f > best[e] || isnan(f)) { best[e] = f; arg[e] = k; }
+    }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = ad ? va[k].get(e) : 0.f;
+      if (arg[e] == k) o += vg.get(e);
+      float d = rnd<T>(o);                                   // the stored pool-input gradient
+      if (r.relu && !(fmaf(yv[k][e], sc[e], sf[e]) > 0.f)) d = 0.f;
+      dz[k][e] = d;
+    }
+}
+
+template <typename T, bool NT>
+__global__ void pool_bn_partial_kernel(PoolBnArgs r) {
+  __shared__ float sh[2][256 * 8];
+  ChanMap cm(r.C);
+  const int c = cm.cv * 8;
+  float s0[8], s1[8], sc[8], sf[8], mu[8], is[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s0[e] = 0.f; s1[e] = 0.f;
+    sc[e] = r.scale[c + e]; sf[e] = r.shift[c + e]; mu[e] = r.mean[c + e]; is[e] = r.invstd[c + e];
+  }
+  const int64_t Q = (int64_t)r.N * (r.H >> 1) * (r.W >> 1);
+  for (int64_t q = (int64_t)blockIdx.x * cm.R + cm.row; q < Q; q += (int64_t)gridDim.x * cm.R) {
+    float yv[4][8], dz[4][8];
+    int64_t p00;
+    pool_window<T, NT>(r, q, c, sc, sf, yv, dz, p00);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s0[e] += dz[k][e];
+        s1[e] += dz[k][e] * ((yv[k][e] - mu[e]) * is[e]);
+      }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { sh[0][cm.row * r.C + c + e] = s0[e]; sh[1][cm.row * r.C + c + e] = s1[e]; }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < r.C; cc += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int q = 0; q < cm.R; ++q) { a0 += sh[0][q * r.C + cc]; a1 += sh[1][q * r.C + cc]; }
+    r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + cc] = a0;
+    r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + cc] = a1;
+  }
+}
+
+template <typename T, bool NT>
+__global__ void pool_bn_apply_kernel(PoolBnArgs r) {
+  ChanMap cm(r.C);
+  const int c = cm.cv * 8;
+  float sc[8], sf[8], mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = r.scale[c + e]; sf[e] = r.shift[c + e]; mu[e] = r.mean[c + e];
+    k1[e] = r.coef[c + e]; k2[e] = r.coef[r.C + c + e]; k3[e] = r.coef[2 * r.C + c + e];
+  }
+  T* dx = reinterpret_cast<T*>(r.dx);
+  const int64_t Q = (int64_t)r.N * (r.H >> 1) * (r.W >> 1);
+  for (int64_t q = (int64_t)blockIdx.x * cm.R + cm.row; q < Q; q += (int64_t)gridDim.x * cm.R) {
+    float yv[4][8], dz[4][8];
+    int64_t p00;
+    pool_window<T, NT>(r, q, c, sc, sf, yv, dz, p00);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      Vec8<T> vo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vo.set(e, k1[e] * dz[k][e] + k2[e] * (yv[k][e] - mu[e]) + k3[e]);
+      vo.store(dx + (p00 + (k >> 1) * r.W + (k & 1)) * r.dxs + c);
+    }
+  }
+}
+
 // ---- BatchNorm forward for SMALL tensors: finalize + apply in one launch ----
 // The ResNet34 encoder's 64^2-16^2 levels (and the U-Net's 32^2 level) have
 // 16-256 partial-statistics tiles; there the two finalize launches and the
@@ -1024,6 +1152,42 @@ extern "C" int vu_bn_apply_maxpool2(const void* y, int64_t ys, void* a, int64_t 
   else
     hipLaunchKernelGGL(bn_apply_maxpool_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)y, ys,
                        (float*)a, as, (float*)pool, ps, N, H, W, C, scale, shift, relu);
+  return (int)hipGetLastError();
+}
+
+// BatchNorm(+ReLU) backward through the 2x2 max-pool: partial pass, fp64
+// finish (dgamma, dbeta, k1..k3 into coef [3][C]), apply pass -> dx (the
+// gradient of y).  1 when served (even H and W, the vectorised channel map).
+extern "C" int vu_bn_bwd_pool_supported(int H, int W, int C, int64_t ys, int64_t dps, int64_t adds, int64_t dxs) {
+  return H % 2 == 0 && W % 2 == 0 && H > 0 && W > 0 && chanmap_ok(C, ys, dps, adds) && dxs % 8 == 0;
+}
+
+extern "C" int vu_bn_bwd_pool(const void* y, int64_t ys, const void* dp, int64_t dps, const void* add, int64_t adds,
+                              int N, int H, int W, int C, const float* scale, const float* shift, const float* mean,
+                              const float* invstd, const float* gamma, int relu, int train, float* dgamma,
+                              float* dbeta, int accumulate, float* coef, float* workspace, void* dx, int64_t dxs,
+                              int dtype, void* stream) {
+  if (!vu_bn_bwd_pool_supported(H, W, C, ys, dps, add ? adds : 8, dxs) || N < 1) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t P = (int64_t)N * H * W;
+  PoolBnArgs r{y, ys, dp, dps, add, adds, N, H, W, C, scale, shift, mean, invstd, relu, workspace, coef, dx, dxs};
+  const int nblk = (int)chan_grid(P, C, RED_MAXBLK);  // rows = pooled pixels: ~4 windows per thread
+  const bool nt = bn_nt(P, C, dtype == VU_BF16 ? 2 : 4);
+  const unsigned agrid = chan_grid(P, C, 8192);
+  if (dtype == VU_BF16) {
+    if (nt) hipLaunchKernelGGL((pool_bn_partial_kernel<bf16_t, true>), dim3(nblk), dim3(256), 0, st, r);
+    else hipLaunchKernelGGL((pool_bn_partial_kernel<bf16_t, false>), dim3(nblk), dim3(256), 0, st, r);
+  } else {
+    hipLaunchKernelGGL((pool_bn_partial_kernel<float, false>), dim3(nblk), dim3(256), 0, st, r);
+  }
+  hipLaunchKernelGGL(bn_bwd_final, dim3((C + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, C, P, gamma,
+                     invstd, dgamma, dbeta, accumulate, coef, train);
+  if (dtype == VU_BF16) {
+    if (nt) hipLaunchKernelGGL((pool_bn_apply_kernel<bf16_t, true>), dim3(agrid), dim3(256), 0, st, r);
+    else hipLaunchKernelGGL((pool_bn_apply_kernel<bf16_t, false>), dim3(agrid), dim3(256), 0, st, r);
+  } else {
+    hipLaunchKernelGGL((pool_bn_apply_kernel<float, false>), dim3(agrid), dim3(256), 0, st, r);
+  }
   return (int)hipGetLastError();
 }
 

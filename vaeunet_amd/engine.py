@@ -431,14 +431,51 @@ def bn_grad_sinks(bn):
     return gw, gb, accw or accb
 
 
+class PoolGrad:
+    """The gradient of a BN(+ReLU) activation that fed a 2x2 max-pool (and a
+    skip connection), kept unmaterialised: dp = gradient of the pooled output,
+    add = skip gradient (or None), act = the stored activation (fallback).
+    bn_bwd runs the BN backward straight from it (vu_bn_bwd_pool)."""
+
+    def __init__(self, dp, add, act):
+        self.dp, self.add, self.act = dp, add, act
+
+    def materialize(self, M):
+        dx = torch.empty_like(self.act)
+        K.maxpool_bwd(self.act, self.dp, dx, self.add, M.d)
+        return dx
+
+
+# BatchNorm backward through the following max-pool from (pooled gradient,
+# skip gradient, BN input) instead of the materialised pool-input gradient:
+# 5.5 instead of 8.25 full-size passes per pooled layer, but every pass
+# recomputes the activation, its argmax and the pool-input gradient per
+# window (~2x the VALU work per element of the three kernels it replaces).
+# Measured SLOWER (same-box A/B, profiles/r4af_ab_pool_bn_bwd.log: UNet
+# 523.3 -> 500.0 img/s; the two passes 154 + 190 us per launch on average):
+# these streams are VALU-bound once they compute ~25 operations per element.
+# Off by default; module-level switch for A/B runs (tested either way).
+POOL_BN_BWD = False
+
+
 def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None):
     """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
     batch statistics; eval mode (running statistics, constants) gives
     dx = gamma*invstd*dz and the same dgamma/dbeta sums.  part: the first
-    reduction stage, already emitted by the GEMM that produced dy."""
+    reduction stage, already emitted by the GEMM that produced dy.  dy may be
+    a PoolGrad (the activation fed a 2x2 max-pool)."""
     gw, gb, acc = bn_grad_sinks(bn)
     if dx is None:
         dx = torch.empty_like(x)
+    if isinstance(dy, PoolGrad):
+        add = dy.add
+        N, Cc, H, W = x.shape
+        if POOL_BN_BWD and K.query("vu_bn_bwd_pool_supported", H, W, Cc, K.pstride(x), K.pstride(dy.dp),
+                                   K.pstride(add) if add is not None else 8, K.pstride(dx)):
+            K.bn_backward_pool(dy.dp, add, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
+                               train=bn.training)
+            return dx
+        dy = dy.materialize(M)
     if part is not None and part.x is x:
         K.bn_backward_part(part, dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
                            train=bn.training)
@@ -577,16 +614,16 @@ def down_fwd(M, mod, x, pend=None, defer=False):
 
 
 def down_bwd(M, mod, saved, dout, add=None):
-    """dx = d(loss)/d(this Down's input); add = the skip gradient, summed in
-    the max-pool backward.  (A max-pool backward carrying the producing BN's
-    backward reduction streams five tensors and measured slower than the two
-    passes it replaces: DESIGN.md §4.2.)"""
+    """d(loss)/d(this Down's input) as a PoolGrad (the pooled gradient + add,
+    the skip gradient): the producing DoubleConv's BN2 backward reads it
+    through the pool (round 4).  (Round 2: a max-pool backward carrying that
+    BN's backward reduction streamed five tensors and measured slower than the
+    two passes it replaced: DESIGN.md §4.2.)"""
     x, sdc = saved
     seq = mod.maxpool_conv[1].double_conv
     dxp = double_conv_bwd(M, seq, sdc, dout, True)
-    dx = torch.empty_like(x)
-    K.maxpool_bwd(x, dxp, dx, add, M.d)
-    return dx
+    # unmaterialised: the producing DoubleConv's BN2 backward takes it (bn_bwd)
+    return PoolGrad(dxp, add, x)
 
 
 # ----------------------------------------------------------------------------

@@ -505,6 +505,21 @@ def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=T
     return dx
 
 
+def bn_backward_pool(dp, add, y, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
+    """BatchNorm(+ReLU) backward through the 2x2 max-pool that follows it
+    (vu_bn_bwd_pool): dp the pooled output's gradient, add the skip gradient
+    of the activation (or None); dx = the gradient of y (the BN input)."""
+    N, Cc, H, W = y.shape
+    P = N * H * W
+    ws = workspace_f32(query("vu_reduce_workspace_bytes", P, Cc), y.device)
+    k = torch.empty((3, Cc), dtype=torch.float32, device=y.device)
+    call("vu_bn_bwd_pool", ptr(y), pstride(y), ptr(dp), pstride(dp), ptr(add), pstride(add) if add is not None else 0,
+         N, H, W, Cc, ptr(coef[0]), ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
+         1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), ptr(dx), pstride(dx),
+         dtype, stream())
+    return dx
+
+
 def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
     """bn_backward with the first reduction stage done by the producing GEMM's
     epilogue (a BnbPart): the fp64 finish, then the apply pass."""

@@ -92,7 +92,8 @@ class Down(nn.Module):
             return E.down_fwd(M, self, E.to_act(M, inp[0]))[1:]
 
         def bwd(state, dout):
-            return (E.from_act(E.down_bwd(M, self, state, act_grad(M, dout)), x),)
+            # a standalone Down has no producing BN to hand the pooled gradient to
+            return (E.from_act(E.down_bwd(M, self, state, act_grad(M, dout)).materialize(M), x),)
         return run_block(self, fwd, bwd, (x,))
 
 
