@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 4: finalize folds with one LDS transpose + xor-shuffle trees: tests + A/B + finalize kernel times
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r4ag2
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_bn_fused.py tests/test_gpu_attention_kernels.py tests/test_gpu_ops.py tests/test_gpu_parity.py tests/test_gpu_graph.py tests/test_gpu_production_parity.py tests/test_gpu_config_parity.py > $O/tests.log 2>&1 || { echo TEST_FAIL; tail -40 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+bash tools/gpu_ab_lib.sh old new "unet vae" || exit 1
+cd /tmp
+for v in old new; do
+  cp $R/ab/lib_$v.so $R/vaeunet_amd/libvaeunet_hip.so
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$v -o p -- python -u $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-roofline > $O/prof_$v.log 2>&1 || { echo PROF_FAIL; cp $R/ab/lib_new.so $R/vaeunet_amd/libvaeunet_hip.so; exit 1; }
+  find $O/prof_$v -name "*kernel_stats.csv" -exec cp {} $O/unet_kernel_stats_$v.csv \;
+  rm -rf $O/prof_$v
+  echo "== $v"; grep -E "bn_bwd_final|chan_final_sum|bn_stats_stage2|part_final" $O/unet_kernel_stats_$v.csv | cut -d, -f1-5
+done
+cp $R/ab/lib_new.so $R/vaeunet_amd/libvaeunet_hip.so
