@@ -9,7 +9,10 @@ Workload (BASELINE.json configs[1], metric quoted on it):
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 the driver
 uses torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE from the env).
-Rank 0 prints ONE JSON line (see README / DESIGN.md §Measurement).
+Rank 0 prints ONE JSON line (see README / DESIGN.md §Measurement).  A default
+N=1 run (CPU leg on) also runs BASELINE configs[2] -- the UNetResNet VAE step,
+same steps / warmup -- as a child process and nests its line under
+"secondary.config3_vae"; the headline value is config 2's.
 """
 import argparse
 import json
@@ -57,6 +60,9 @@ def parse():
                     help="unet = BASELINE configs[1] (the metric); vae = configs[2], UNetResNet + KL")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the config-3 (VAE) secondary line that a default N=1 UNet run appends "
+                         "(--no-cpu-baseline, the A/B and profiling runs, skips it too)")
     ap.add_argument("--cpu-batch", type=int, default=8, help="CPU baseline batch (BASELINE.md §4: 8)")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps per leg after 1 warmup")
     ap.add_argument("--cpu-budget-s", type=float, default=60.0,
@@ -330,6 +336,28 @@ def gpu_parity(args, x, t, ref_out, ref_loss, dev, eps=None):
     return out
 
 
+def vae_secondary(args):
+    """BASELINE configs[2] (UNetResNet VAE train step, same batch / image) as a
+    child run of this script -- ``--model vae`` with the same steps / warmup,
+    its own 3x3 roofline, no CPU leg -- so the driver's default bench also
+    records config 3 (a child process, not an exec: this one has touched the
+    GPU).  Its JSON line is nested as-is; the headline value stays config 2."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--model", "vae", "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--batch", str(args.batch), "--size", str(args.size),
+           "--no-cpu-baseline", "--graph", args.graph]
+    if args.no_roofline:
+        cmd.append("--no-roofline")
+    _progress("secondary: config-3 VAE run")
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}"}
+    sec = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "higher_is_better", "vs_baseline", "cpu_baseline", "parity", "data", "n_gpus"):
+        sec.pop(k, None)
+    return sec
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -488,6 +516,9 @@ def main():
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline(args, dev)
+    secondary = None
+    if rank == 0 and world == 1 and not vae and not (args.no_secondary or args.no_cpu_baseline):
+        secondary = {"config3_vae": vae_secondary(args)}
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(imgs, 2),
@@ -506,6 +537,8 @@ def main():
                            "bn_bwd_reduce_in_dgrad_epilogue": bool(E.FUSE_BN_BWD_REDUCE)},
                 "loss": round(float(loss.item()), 6),
                 "roofline": roof, "cpu_baseline": cpu, "parity": parity}
+        if secondary is not None:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
