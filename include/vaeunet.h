@@ -296,8 +296,9 @@ int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1,
 
 /* Batched vu_permute4 (one launch for all derived weight images of a step).
  * jobs: device array.  q = the input-fastest dim when it is not dim 3 (the
- * job is then a batched 2-D transpose in 32x32 tiles: one block per tile,
- * prod(other dims) * ceil(d_q/32) * ceil(d3/32) blocks), or 3 (streamed,
+ * job is then a batched 2-D transpose in T x T tiles, T = vu_permute4_tile()
+ * (64; 32 before round 4): one block per tile, prod(other dims) *
+ * ceil(d_q/T) * ceil(d3/T) blocks), or 3 (streamed,
  * ceil(numel / vu_permute4_chunk()) blocks).  chunk0 = prefix block count,
  * nchunks = total blocks. */
 typedef struct VuPermJob {
@@ -309,6 +310,7 @@ typedef struct VuPermJob {
   int32_t q, pad_;
 } VuPermJob;
 int64_t vu_permute4_chunk(void);
+int64_t vu_permute4_tile(void);
 int vu_permute4_batch(const VuPermJob* jobs, int njobs, int64_t nchunks,
                       void* stream);
 /* Round 4: the same with the 3x3 / 2x2 weight images (q = 4: dims 1, 2

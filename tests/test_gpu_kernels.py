@@ -987,18 +987,21 @@ def test_permute_batch_matches_single_launches():
           torch.randn(32, 16, 2, 2, generator=g).to(DEV),
           torch.randn(64, 3, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL),
           torch.randn(72, 40, 3, 3, generator=g).to(DEV),   # ragged 32-tiles of the tap-merged transpose
-          torch.randn(40, 24, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL)]  # converting copy
+          torch.randn(40, 24, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL),  # converting copy
+          torch.randn(136, 72, 3, 3, generator=g).to(DEV).contiguous(memory_format=CL)]  # ragged 64-tile transposes
     for d in (0, 1):
         single = [E.w3x3_fwd(ws[0], d), E.w3x3_dgrad(ws[0], d), E.w1x1_fwd(ws[1], d), E.w1x1_dgrad(ws[1], d),
                   E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8),
-                  E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64), E.w3x3_fwd(ws[5], d), E.w3x3_dgrad(ws[5], d)]
+                  E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64), E.w3x3_fwd(ws[5], d), E.w3x3_dgrad(ws[5], d),
+                  E.w3x3_fwd(ws[6], d), E.w3x3_dgrad(ws[6], d)]
         single = [t.clone() for t in single]
         for w in ws:
             w.mul_(1.0)  # bump the version: every image is stale
         E.refresh_weights(ws)
         batched = [E.w3x3_fwd(ws[0], d), E.w3x3_dgrad(ws[0], d), E.w1x1_fwd(ws[1], d), E.w1x1_dgrad(ws[1], d),
                    E.wT_fwd(ws[2], d), E.wT_dgrad(ws[2], d), E.w3x3_fwd(ws[3], d, 8),
-                   E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64), E.w3x3_fwd(ws[5], d), E.w3x3_dgrad(ws[5], d)]
+                   E.w3x3_fwd(ws[4], d, 48), E.w3x3_dgrad(ws[4], d, 64), E.w3x3_fwd(ws[5], d), E.w3x3_dgrad(ws[5], d),
+                  E.w3x3_fwd(ws[6], d), E.w3x3_dgrad(ws[6], d)]
         for a, b in zip(single, batched):
             assert torch.equal(a, b)
     # the round-4 tap-merged path is the one taken for the 3x3 images (and the ConvT input-gradient image)
@@ -1011,6 +1014,27 @@ def test_permute_batch_matches_single_launches():
     modes = [K.perm_mode(j[2], j[3], j[4]) for j in jobs]
     assert modes.count(4) >= 5, modes   # w3x3 fwd / dgrad of ws[0], ws[4] and the wT dgrad image
     assert modes.count(5) >= 1, modes   # the channels_last weight's forward image without padding
+    assert modes.count(0) >= 2, modes   # the channels_last weights' input-gradient images: 64 x 64 transposes
+
+
+@pytest.mark.parametrize("shape", [(8, 3, 64, 96), (3, 3, 17, 29), (2, 1, 5, 7), (1, 8, 16, 16)])
+@pytest.mark.parametrize("cl", [True, False])
+@pytest.mark.parametrize("d", [0, 1])
+def test_input_pack_8_channels(shape, cl, d):
+    """vu_input_pack to 8 channels (the image packing of inc.0 / the ResNet
+    stem, one pixel per thread since round 4): the zero-padded NHWC copy,
+    bit-exact (bf16 by round-to-nearest-even as torch's .to(bfloat16))."""
+    K, _ = _k()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(*shape, generator=g).to(DEV)
+    if cl:
+        x = x.contiguous(memory_format=CL)
+    y = K.input_pack(x, 8, d)
+    N, C, H, W = shape
+    ref = torch.zeros(N, 8, H, W, device=DEV)
+    ref[:, :C] = x
+    ref = ref.to(torch.bfloat16 if d == 1 else torch.float32)
+    assert torch.equal(y.permute(0, 2, 3, 1).contiguous(), ref.permute(0, 2, 3, 1).contiguous())
 
 
 @pytest.mark.parametrize("case", [
@@ -1058,3 +1082,29 @@ def test_conv_stride2_input_grad_parity_classes(case, zi, acc):
     ref = torch.nn.grad.conv2d_input((N, ci, H, H), wq, dy, stride=2, padding=k // 2)
     sab = torch.nn.grad.conv2d_input((N, ci, H, H), wq.abs(), dy.abs(), stride=2, padding=k // 2)
     _close(dx, ref + base if acc else ref, "bf16", what="stride-2 dgrad", sabs=sab, acc=ref if acc else None)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 17, 23, 2), (1, 128, 9, 9, 1), (3, 64, 64, 64, 3), (1, 32, 5, 3, 4)])
+@pytest.mark.parametrize("d", [0, 1])
+def test_outconv_pointwise_fwd(shape, d):
+    """OutConv's 1x1 -> J <= 4 logits (vu_pointwise_fwd, unet_parts.py:97-103),
+    ragged pixel tails included (the round-4 clamped, unguarded row loads):
+    vs torch fp32 conv2d of the same (bf16-rounded) input, per element within
+    fp32 summation-order error."""
+    import types
+    import torch.nn.functional as F
+    from vaeunet_amd import engine as E
+    N, C, H, W, J = shape
+    g = torch.Generator().manual_seed(11)
+    conv = torch.nn.Conv2d(C, J, 1).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(J, C, 1, 1, generator=g) / C ** 0.5)
+        conv.bias.copy_(torch.randn(J, generator=g))
+    x = torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16 if d == 1 else torch.float32)
+    x = x.contiguous(memory_format=CL)
+    y, _ = E.outconv_fwd(types.SimpleNamespace(d=d), conv, x)
+    with torch.no_grad():
+        ref = F.conv2d(x.float(), conv.weight, conv.bias)
+        mag = F.conv2d(x.float().abs(), conv.weight.abs()) + conv.bias.abs()[None, :, None, None]
+    assert y.shape == ref.shape
+    assert ((y - ref).abs() <= 1e-5 * mag + 1e-6).all(), float((y - ref).abs().max())

@@ -105,6 +105,7 @@ _SIGS = {
     "vu_conv3x3_fp8": (_i, [C.POINTER(VuConvFp8), _p]),
     "vu_conv3x3_fp8_workspace_bytes": (_l, [C.POINTER(VuConvFp8)]),
     "vu_permute4_chunk": (_l, []),
+    "vu_permute4_tile": (_l, []),
     "vu_permute4_batch": (_i, [_p, _i, _l, _p]),
     "vu_permute4_batch2": (_i, [_p, _i, _i, _l, _l, _p]),
     "vu_permute4": (_i, [_p, _l, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),

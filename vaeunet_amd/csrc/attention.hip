@@ -470,15 +470,21 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
       for (int k = 0; k < 8; ++k) wr[j][k] = j < J ? w[j * C + c + k] : 0.f;
     }
     for (int64_t pb = wave * ppw * PU; pb < P; pb += nwaves * ppw * PU) {
+      // the PU loads from clamped pixel addresses, unconditionally: a guarded
+      // load per pixel sat in its own basic block with a vmcnt(0) wait after
+      // it, serialising the round trips (512^2 x 64 -> 2 at ~3 TB/s); rows
+      // past P are zeroed after the loads
       float f[PU][8];
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
         const int64_t p = pb + u * ppw + slot;
-        if (p < P) load8<T>(x + p * xs + c, f[u]);
-        else
+        load8<T>(x + (p < P ? p : P - 1) * xs + c, f[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u)
+        if (pb + u * ppw + slot >= P)
 #pragma unroll
           for (int k = 0; k < 8; ++k) f[u][k] = 0.f;
-      }
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
         const int64_t p = pb + u * ppw + slot;

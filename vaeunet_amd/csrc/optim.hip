@@ -40,9 +40,24 @@ __global__ void mt_sumsq_kernel(const VuMtEntry* t, int n, double* part) {
   const int64_t end = min(t[k].numel, off + MT_CHUNK);
   const gfl* g = (const gfl*)(t[k].grad);
   double a = 0;
-  for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
-    double v = g[i];
-    a += v * v;
+  if (end - off == MT_CHUNK) {
+    // a whole chunk: the thread's 32 loads issued before the first is used
+    // (the guarded loop below serialised them behind the fp64 chain: 2.7
+    // TB/s); the same elements summed in the same order
+    constexpr int U = MT_CHUNK / MT_THREADS;
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = g[off + threadIdx.x + u * MT_THREADS];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double d = v[u];
+      a += d * d;
+    }
+  } else {
+    for (int64_t i = off + threadIdx.x; i < end; i += MT_THREADS) {
+      double v = g[i];
+      a += v * v;
+    }
   }
   a = warp_sum_d(a);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = a;

@@ -312,6 +312,32 @@ __global__ void input_pack_kernel(const float* x, int64_t sn, int64_t sc, int64_
   }
 }
 
+// The 8-channel packing of the image (Cp == 8, C <= 8, N*H*W < 2^31): one
+// thread per pixel, the pixel decoded by multiply-shift, its C source values
+// loaded together and the 8 output channels written as ONE 16-byte (bf16) /
+// 32-byte (fp32) store.  The element-per-thread form above spent two 64-bit
+// divisions per output element: 52 us for the 512^2 batch-8 image (1.1 TB/s).
+template <typename TO>
+__global__ __launch_bounds__(256) void input_pack8_kernel(const float* x, int64_t sn, int64_t sc, int64_t sh,
+                                                          int64_t sw, int P, int C, int H, int W, TO* y) {
+  const FastDiv div_hw((uint32_t)(H * W)), div_w((uint32_t)W);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const int n = (int)div_hw.div((uint32_t)p);
+    const int rem = p - n * H * W;
+    const int h = (int)div_w.div((uint32_t)rem), w = rem - h * W;
+    const float* px = x + n * sn + h * sh + w * sw;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = px[(c < C ? c : C - 1) * sc];  // unguarded: loads issue together
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < C ? v[c] : 0.f;
+    Vec8<TO> o;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o.set(c, v[c]);
+    o.store(y + (int64_t)p * 8);
+  }
+}
+
 }  // namespace
 
 #define DISPATCH_T(dtype, ...) \
@@ -407,10 +433,10 @@ extern "C" int vu_permute4(const float* in, int64_t base, int64_t s0, int64_t s1
 // (3) is not the input-fastest one (e.g. the flipped [ci][tap][co] input-
 // gradient images: co is the slowest input dim) is a batched 2-D transpose:
 // 32x32 tiles through LDS, coalesced reads along the input-fast dim q and
-// coalesced writes along dim 3.  Other jobs are streamed PERM_CHUNK elements
+// coalesced writes along dim 3 (PERM_TILE x PERM_TILE tiles).  Other jobs are streamed PERM_CHUNK elements
 // per block.  chunk0 is the prefix block count (binary search per block).
 namespace {
-constexpr int PERM_CHUNK = 4096;
+constexpr int PERM_CHUNK = 4096, PERM_TILE = 64;
 // global-address-space views of the job pointers (read from a device table:
 // through generic pointers the loads are flat instructions, which count in
 // lgkmcnt and so wait behind / hold up the tile transposes' LDS traffic)
@@ -445,7 +471,7 @@ __device__ __forceinline__ void tap_tile(const VuPermJob& j, const gfl* in, cons
 }
 
 __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jobs, int n) {
-  __shared__ float tile[32][33];
+  __shared__ float tile[PERM_TILE][PERM_TILE + 1];
   const int64_t chunk = blockIdx.x;
   int lo = 0, hi = n - 1;
   while (lo < hi) {
@@ -499,34 +525,38 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
     }
     return;
   }
-  // tiled transpose between dim q (input-fast) and dim 3 (output-fast)
+  // tiled transpose between dim q (input-fast) and dim 3 (output-fast), 64 x
+  // 64 tiles: 256-byte fp32 reads and 128-byte bf16 writes per wave row (the
+  // 32 x 32 tiles of round 3 wrote half lines and moved 4 KB per block: the
+  // step's weight refresh ran at ~2 TB/s)
+  constexpr int TT = PERM_TILE;
   const int q = j.q;
   const int a = q == 0 ? 1 : 0, c = q == 2 ? 1 : 2;  // the two batch dims, in order
-  const uint32_t tq = (d[q] + 31) / 32, t3 = (d[3] + 31) / 32;
+  const uint32_t tq = (d[q] + TT - 1) / TT, t3 = (d[3] + TT - 1) / TT;
   const uint32_t b = blk / (tq * t3), rem = blk - b * (tq * t3);
-  const int iq0 = (int)(rem / t3) * 32, i30 = (int)(rem - (rem / t3) * t3) * 32;
+  const int iq0 = (int)(rem / t3) * TT, i30 = (int)(rem - (rem / t3) * t3) * TT;
   const int ia = (int)(b / d[c]), ic = (int)(b - (b / d[c]) * d[c]);
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const gfl* ib = in + ia * st[a] + ic * st[c];
+  float v[TT / 4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int iq = iq0 + tx, i3 = i30 + ty + 8 * k;
-    float v = 0.f;
-    if (iq < d[q] && i3 < d[3] && i3 < j.d3v) v = ib[iq * st[q] + i3 * st[3]];
-    tile[ty + 8 * k][tx] = v;
+  for (int k = 0; k < TT / 4; ++k) {
+    const int iq = iq0 + tx, i3 = i30 + ty + 4 * k;
+    v[k] = (iq < d[q] && i3 < d[3] && i3 < j.d3v) ? ib[iq * st[q] + i3 * st[3]] : 0.f;
   }
-  __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i3 = i30 + tx, iq = iq0 + ty + 8 * k;
+  for (int k = 0; k < TT / 4; ++k) tile[ty + 4 * k][tx] = v[k];
+  __syncthreads();
+  int idx[4];
+  idx[a] = ia;
+  idx[c] = ic;
+#pragma unroll
+  for (int k = 0; k < TT / 4; ++k) {
+    const int i3 = i30 + tx, iq = iq0 + ty + 4 * k;
     if (iq >= d[q] || i3 >= d[3]) continue;
-    int idx[4];
-    idx[a] = ia;
-    idx[c] = ic;
     idx[q] = iq;
-    idx[3] = i3;
     const uint32_t e = (((uint32_t)idx[0] * d[1] + idx[1]) * d[2] + idx[2]) * d[3] + i3;
-    put(e, tile[tx][ty + 8 * k]);
+    put(e, tile[tx][ty + 4 * k]);
   }
 }
 // The 3x3 / 2x2 weight images (q = 4, see tap_tile) in a launch of their own:
@@ -556,6 +586,7 @@ __global__ __launch_bounds__(256) void permute4_tap_kernel(const VuPermJob* jobs
 }  // namespace
 
 extern "C" int64_t vu_permute4_chunk(void) { return PERM_CHUNK; }
+extern "C" int64_t vu_permute4_tile(void) { return PERM_TILE; }
 
 extern "C" int vu_permute4_batch2(const VuPermJob* jobs, int njobs, int ntap, int64_t tap_blocks,
                                   int64_t rest_blocks, void* stream) {
@@ -675,6 +706,14 @@ extern "C" int vu_input_pack(const float* x, int64_t sn, int64_t sc, int64_t sh,
   hipStream_t st = (hipStream_t)stream;
   int64_t tot = (int64_t)N * H * W * Cp;
   if (tot == 0) return 0;
+  const int64_t P = (int64_t)N * H * W;
+  if (Cp == 8 && C >= 1 && C <= 8 && P < ((int64_t)1 << 31) && (int64_t)H * W < ((int64_t)1 << 31)) {
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((input_pack8_kernel<T>), dim3(ew_grid(P)), dim3(256), 0, st, x, sn, sc, sh, sw, (int)P, C,
+                         H, W, (T*)y);
+    })
+    return (int)hipGetLastError();
+  }
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL((input_pack_kernel<T>), dim3(ew_grid(tot)), dim3(256), 0, st, x, sn, sc, sh, sw, N, C, H, W,
                        Cp, (T*)y);

@@ -399,6 +399,7 @@ def job_table(jobs):
     (table tensor, ntap, tap blocks, other blocks): the 3x3 / 2x2 weight
     images (mode 4) first, each group with its own block prefix."""
     chunk = query("vu_permute4_chunk")
+    tt = query("vu_permute4_tile")
     modes = [perm_mode(j[2], j[3], j[4]) for j in jobs]
     order = [i for i in range(len(jobs)) if modes[i] == 4] + [i for i in range(len(jobs)) if modes[i] != 4]
     ntap = sum(1 for m in modes if m == 4)
@@ -424,7 +425,7 @@ def job_table(jobs):
             c0 += (-(-dims[0] // 32)) * (-(-dims[3] // 32))
         else:
             a, cc = [k2 for k2 in range(3) if k2 != q]
-            c0 += dims[a] * dims[cc] * (-(-dims[q] // 32)) * (-(-dims[3] // 32))
+            c0 += dims[a] * dims[cc] * (-(-dims[q] // tt)) * (-(-dims[3] // tt))
     if ntap == len(jobs):
         ctap, c0 = c0, 0
     dev = jobs[0][5].device
