@@ -1,12 +1,14 @@
 #!/bin/bash
 # round 4: whole-tree A/B (ab/tree = the tree before the input-pack / weight-transpose / clip-norm /
-# pointwise / scalar-BN-partial load changes) + rocprof kernel stats of both
+# pointwise / scalar-BN-partial / fused-BN-apply load changes) + rocprof kernel stats of both
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r4ai2
 mkdir -p $O
 cd $R
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_bn_fused.py tests/test_gpu_kernels.py::test_input_pack_8_channels tests/test_gpu_model.py > $O/tests.log 2>&1 || { echo TEST_FAIL; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
 for m in unet vae; do
   for i in 1 2; do
     (cd ab/tree && timeout -k 10 300 python -u bench.py --model $m --no-cpu-baseline --no-roofline --steps 40) > $O/${m}_old_$i.log 2>&1 || { echo FAIL old $m; tail -5 $O/${m}_old_$i.log; exit 1; }

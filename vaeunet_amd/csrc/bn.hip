@@ -722,8 +722,15 @@ __global__ __launch_bounds__(256) void bn_fwd_fused_kernel(BnFusedArgs a) {
   for (int i = 0; i < 8; ++i) {
     sc[i] = ssc[cv * 8 + i];
     sh[i] = ssh[cv * 8 + i];
-    rsc[i] = a.rsc ? a.rsc[c + i] : 1.f;
-    rsh[i] = a.rsc ? a.rsh[c + i] : 0.f;
+    rsc[i] = 1.f;
+    rsh[i] = 0.f;
+  }
+  if (a.rsc) {   // one uniform branch around all 16 loads: they issue together
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      rsc[i] = a.rsc[c + i];
+      rsh[i] = a.rsh[c + i];
+    }
   }
   const int64_t per = (a.P + a.split - 1) / a.split;
   const int64_t p_beg = (int64_t)sp * per, p_end = min(a.P, p_beg + per);
@@ -731,13 +738,19 @@ __global__ __launch_bounds__(256) void bn_fwd_fused_kernel(BnFusedArgs a) {
   const T* r = reinterpret_cast<const T*>(a.res);
   T* out = reinterpret_cast<T*>(a.out);
   for (int64_t p0 = p_beg + row; p0 < p_end; p0 += 64 * UNR) {
+    // clamped, unguarded loads (a guarded pair per row sat behind its own
+    // vmcnt(0): UNR serial round trips per iteration)
     Vec8<T> vy[UNR], vr[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int64_t p = p0 + (int64_t)u * 64;
-      if (p < p_end) {
-        vy[u].load(y + p * a.ys + c);
-        if (r) vr[u].load(r + p * a.rs + c);
+      const int64_t p = p0 + (int64_t)u * 64 < p_end ? p0 + (int64_t)u * 64 : p_end - 1;
+      vy[u].load(y + p * a.ys + c);
+    }
+    if (r) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int64_t p = p0 + (int64_t)u * 64 < p_end ? p0 + (int64_t)u * 64 : p_end - 1;
+        vr[u].load(r + p * a.rs + c);
       }
     }
 #pragma unroll
