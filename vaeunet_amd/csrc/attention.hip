@@ -437,12 +437,13 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
 __global__ void part_final(const float* part, int nblk, int width, float* out, int n_out, float* out2,
                            int accumulate) {
   const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const int cl = c < width ? c : width - 1;
+  float* o = cl < n_out ? (out ? out + cl : nullptr) : (out2 ? out2 + (cl - n_out) : nullptr);
+  const float o0 = (accumulate && o) ? *o : 0.f;   // loaded before the sums (bn_bwd_final)
   double s[1];
   colsum32<1>(part, nblk, width, 0, c, c < width, s);
-  if (threadIdx.x >= 32 || c >= width) return;
-  float* o = c < n_out ? (out ? out + c : nullptr) : (out2 ? out2 + (c - n_out) : nullptr);
-  if (o == nullptr) return;
-  *o = accumulate ? *o + (float)s[0] : (float)s[0];
+  if (threadIdx.x >= 32 || c >= width || o == nullptr) return;
+  *o = accumulate ? o0 + (float)s[0] : (float)s[0];
 }
 
 // ---- tiny-output pointwise conv ----

@@ -109,6 +109,13 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
   const int cl = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   const bool ok = c < C;
+  // the per-channel operands first: issued with the partial loads below, not
+  // after the trees behind the stores they may alias (4 serial round trips)
+  const int cc = ok ? c : 0;
+  const float g = gamma ? gamma[cc] : 1.f, b = beta ? beta[cc] : 0.f;
+  const bool upd = rmean && momentum != 0.f;
+  const float rm0 = upd ? rmean[cc] : 0.f, rv0 = upd ? rvar[cc] : 0.f;
+  const int64_t nb0 = nbt ? nbt[0] : 0;
   constexpr int U = STATS_MAXS / 32;
   double nv[U], mv[U], qv[U];
 #pragma unroll
@@ -152,17 +159,16 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
   M2 = sh[0][0][cl];
   double var = n > 0 ? M2 / n : 0.0;
   float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   float mean = (float)m;
   scale[c] = g * invstd;
   shift[c] = b - mean * g * invstd;
   if (smean) smean[c] = mean;
   if (sinvstd) sinvstd[c] = invstd;
-  if (nbt && c == 0) nbt[0] += 1;
-  if (rmean && momentum != 0.f) {
+  if (nbt && c == 0) nbt[0] = nb0 + 1;
+  if (upd) {
     double unb = n > 1 ? M2 / (n - 1) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    rmean[c] = (1.f - momentum) * rm0 + momentum * mean;
+    rvar[c] = (1.f - momentum) * rv0 + momentum * (float)unb;
   }
 }
 
@@ -355,26 +361,33 @@ __global__ void chan_partial_scalar(RedArgs r) {
 // stage 2: fp64 column sums of the [nblk][2][C] partials (colsum32, fixed order)
 __global__ void chan_final_sum(const float* part, int nblk, int C, float* out, int accumulate) {
   int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const float o0 = accumulate ? out[c < C ? c : C - 1] : 0.f;   // before the sums (bn_bwd_final)
   double s[1];
   colsum32<1>(part, nblk, 2 * (int64_t)C, C, c, c < C, s);
-  if (threadIdx.x < 32 && c < C) out[c] = accumulate ? out[c] + (float)s[0] : (float)s[0];
+  if (threadIdx.x < 32 && c < C) out[c] = accumulate ? o0 + (float)s[0] : (float)s[0];
 }
 
 __global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, const float* gamma,
                              const float* invstd, float* dgamma, float* dbeta, int accumulate,
                              float* coef, int train) {
   int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  // the per-channel operands (and the gradients accumulated into) are loaded
+  // BEFORE the column sums, which they do not depend on: after them, behind
+  // the coef stores they may alias, they were 3 more serial round trips
+  const int cl = c < C ? c : C - 1;
+  const float g = gamma ? gamma[cl] : 1.f;
+  const float is = invstd[cl];
+  const float dg0 = (dgamma && accumulate) ? dgamma[cl] : 0.f;
+  const float db0 = (dbeta && accumulate) ? dbeta[cl] : 0.f;
   double s[2];
   colsum32<2>(part, nblk, 2 * (int64_t)C, C, c, c < C, s);
   if (threadIdx.x >= 32 || c >= C) return;
-  float g = gamma ? gamma[c] : 1.f;
-  float is = invstd[c];
   float k1 = g * is;
   coef[c] = k1;
   coef[C + c] = train ? (float)(-(double)k1 * is * s[1] / (double)P) : 0.f;
   coef[2 * C + c] = train ? (float)(-(double)k1 * s[0] / (double)P) : 0.f;
-  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)s[1] : (float)s[1];
-  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s[0] : (float)s[0];
+  if (dgamma) dgamma[c] = accumulate ? dg0 + (float)s[1] : (float)s[1];
+  if (dbeta) dbeta[c] = accumulate ? db0 + (float)s[0] : (float)s[0];
 }
 
 template <typename T, bool NT>
