@@ -37,6 +37,10 @@ VU_DEV float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
 
+// opaque register tie of a Vec8 (keeps its computation above a guarded store)
+VU_DEV void vec8_tie(Vec8<bf16_t>& v) { asm volatile("" : "+v"(v.v)); }
+VU_DEV void vec8_tie(Vec8<float>& v) { asm volatile("" : "+v"(v.a), "+v"(v.b)); }
+
 VU_DEV float group_sum(float v, int lpp) {
   if (lpp >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
   if (lpp >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -343,22 +347,28 @@ __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux
           vb[u].load(ux + p * F + c);
         }
       }
+      // every row's output formed (and tied) before the guarded stores: with
+      // the work inside the branches each store waited vmcnt(0) -- i.e. for
+      // the previous row's store (4 serial write round trips per round)
+      Vec8<T> o[U];
+      bool okp[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (it + u >= niter) break;
         const int64_t p = p0 + w * ppw + slot + (it + u) * 4 * ppw;
-        if (p >= P) continue;
-        if (sub == 0) db += g[u];
-        Vec8<T> o;
+        okp[u] = it + u < niter && p < P;
+        if (okp[u] && sub == 0) db += g[u];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float s = va[u].get(k) * wsg[k] + wtg[k] + vb[u].get(k) * wsx[k] + wtx[k];
           bool on = s > 0.f;
-          dw[k] += on ? g[u] * s : 0.f;
-          o.set(k, on ? g[u] * wp[k] : 0.f);
+          if (okp[u]) dw[k] += on ? g[u] * s : 0.f;
+          o[u].set(k, on ? g[u] * wp[k] : 0.f);
         }
-        o.store(ds + p * F + c);
+        vec8_tie(o[u]);
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (okp[u]) o[u].store(ds + (p0 + w * ppw + slot + (it + u) * 4 * ppw) * F + c);
     }
   }
 #pragma unroll

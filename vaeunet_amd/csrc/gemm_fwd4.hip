@@ -580,9 +580,42 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
       sb[q] += *reinterpret_cast<const f32x4*>(src + 4);
     }
   }
+  // The epilogue's loads -- the old output rows (accumulate) and the BN-
+  // backward operands (bnb_part) -- issued together before the first store:
+  // behind the stores they may alias they were ~12 serial round trips.
+  bf16_t* dstq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int64_t m = (int64_t)rb * 128 + rs + 32 * q;
+    int64_t orow = m;
+    if (p.out_mode == 2) {  // stride-2 sub-lattice (parity-class input gradients)
+      const int64_t hw = (int64_t)p.a.H * p.a.W;
+      const int64_t n = m / hw, rem = m - n * hw;
+      const int h = (int)(rem / p.a.W), w = (int)(rem - (int64_t)h * p.a.W);
+      orow = ((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx;
+    }
+    dstq[q] = out + orow * p.out_stride + p.out_coff + c0;
+  }
+  Vec8<bf16_t> old[4], xq[4];
+  float bsc[8], bsf[8], bmu[8], bis[8];
+  if (p.accumulate) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) old[q].load(dstq[q]);
+  }
+  if (p.bnb_part) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      xq[q].load(reinterpret_cast<const bf16_t*>(p.bnb_x) + ((int64_t)rb * 128 + rs + 32 * q) * p.bnb_xstride + c0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = p.bnb_scale[c0 + e];
+      bsf[e] = p.bnb_shift[c0 + e];
+      bmu[e] = p.bnb_mean[c0 + e];
+      bis[e] = p.bnb_invstd[c0 + e];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
     const f32x4 a = sa[q], b = sb[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -592,24 +625,14 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
     if (p.relu)
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[q][e] = fmaxf(v[q][e], 0.f);
-    int64_t orow = m;
-    if (p.out_mode == 2) {  // stride-2 sub-lattice (parity-class input gradients)
-      const int64_t hw = (int64_t)p.a.H * p.a.W;
-      const int64_t n = m / hw, rem = m - n * hw;
-      const int h = (int)(rem / p.a.W), w = (int)(rem - (int64_t)h * p.a.W);
-      orow = ((int64_t)n * p.oH + 2 * h + p.opy) * p.oW + 2 * w + p.opx;
-    }
-    bf16_t* dst = out + orow * p.out_stride + p.out_coff + c0;
     Vec8<bf16_t> o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o.set(e, v[q][e]);
     if (p.accumulate) {
-      Vec8<bf16_t> old;
-      old.load(dst);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o.set(e, old.get(e) + v[q][e]);
+      for (int e = 0; e < 8; ++e) o.set(e, old[q].get(e) + v[q][e]);
     }
-    o.store(dst);
+    o.store(dstq[q]);
   }
   if (p.bnb_part) {
     // BatchNorm-backward partials of this 128-row tile (see VuGemmFwd.bnb_part)
@@ -618,16 +641,13 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
     for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int64_t m = (int64_t)rb * 128 + rs + 32 * q;
-      Vec8<bf16_t> xq;
-      xq.load(reinterpret_cast<const bf16_t*>(p.bnb_x) + m * p.bnb_xstride + c0);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float xv = xq.get(e);
+        const float xv = xq[q].get(e);
         float dz = v[q][e];
-        if (p.bnb_relu && !(xv * p.bnb_scale[c0 + e] + p.bnb_shift[c0 + e] > 0.f)) dz = 0.f;
+        if (p.bnb_relu && !(xv * bsc[e] + bsf[e] > 0.f)) dz = 0.f;
         s0[e] += dz;
-        s1[e] += dz * ((xv - p.bnb_mean[c0 + e]) * p.bnb_invstd[c0 + e]);
+        s1[e] += dz * ((xv - bmu[e]) * bis[e]);
       }
     }
 #pragma unroll

@@ -321,6 +321,9 @@ __global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* slab, in
     for (; k + 3 * SL < splits; k += 4 * SL)
 #pragma unroll
       for (int u = 0; u < 4; ++u) a[u] += s4[(int64_t)(k + u * SL) * tot4 + idx4];
+    // (the < 4 remaining splits of a lane: clamped loads issued together
+    // measured slower here -- the duplicate loads cost more than the round
+    // trips, profiles/r4al_ab_epilogue_latency.log)
     for (; k < splits; k += SL) a[0] += s4[(int64_t)k * tot4 + idx4];
   }
   sh[q][l] = (a[0] + a[1]) + (a[2] + a[3]);
@@ -329,15 +332,33 @@ __global__ void __launch_bounds__(256) slab_reduce4_kernel(const float* slab, in
   f32x4 s = sh[0][l];
 #pragma unroll
   for (int w = 1; w < SL; ++w) s += sh[w][l];
+  // the 4 destinations, then (accumulate) their old values loaded together
+  // before the first store (loaded behind the stores they were 4 round trips)
+  float* o[4];
+  float old[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int64_t idx = idx4 * 4 + e;
     const int i = (int)(idx / nj), j = (int)(idx - (int64_t)i * nj);
     const int tap = j / C, c = j - tap * C;
-    if (c >= cvalid) continue;
-    float* o = out + i * s_i + tap * s_tap + c * s_c;
-    *o = accumulate ? *o + s[e] : s[e];
+    o[e] = c < cvalid ? out + i * s_i + tap * s_tap + c * s_c : nullptr;
   }
+  if (accumulate) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) old[e] = o[e] ? *o[e] : 0.f;
+  }
+  // the values formed (one wait for the loads) before the guarded stores:
+  // sunk into the branches, each store waited vmcnt(0) -- for the previous
+  // store too
+  float val[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    val[e] = accumulate ? old[e] + s[e] : s[e];
+    asm volatile("" : "+v"(val[e]));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (o[e]) *o[e] = val[e];
 }
 
 template <int SL>
