@@ -669,6 +669,11 @@ __global__ __launch_bounds__(256) void bn_fwd_fused_kernel(BnFusedArgs a) {
   {
     const int cl = tid & 31, tl = tid >> 5;
     const int c = cg * 32 + cl;
+    // the per-channel operands first (bn_stats_stage2)
+    const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+    const bool upd = sp == 0 && a.rmean && a.momentum != 0.f;
+    const float rm0 = upd ? a.rmean[c] : 0.f, rv0 = upd ? a.rvar[c] : 0.f;
+    const int64_t nb0 = (sp == 0 && a.nbt) ? a.nbt[0] : 0;
     constexpr int U = BNF_MAXT / 8;
     float sv[U], mv[U];
 #pragma unroll
@@ -707,7 +712,6 @@ __global__ __launch_bounds__(256) void bn_fwd_fused_kernel(BnFusedArgs a) {
       const double n = (double)a.P;
       const double var = M2 / n;
       const float invstd = (float)(1.0 / sqrt(var + (double)a.eps));
-      const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
       const float mean = (float)m;
       const float scale = g * invstd, shift = b - mean * g * invstd;
       ssc[cl] = scale;
@@ -717,11 +721,11 @@ __global__ __launch_bounds__(256) void bn_fwd_fused_kernel(BnFusedArgs a) {
         a.coef[a.C + c] = shift;
         a.coef[2 * a.C + c] = mean;
         a.coef[3 * a.C + c] = invstd;
-        if (a.nbt && c == 0) a.nbt[0] += 1;
-        if (a.rmean && a.momentum != 0.f) {
+        if (a.nbt && c == 0) a.nbt[0] = nb0 + 1;
+        if (upd) {
           const double unb = n > 1 ? M2 / (n - 1) : var;
-          a.rmean[c] = (1.f - a.momentum) * a.rmean[c] + a.momentum * mean;
-          a.rvar[c] = (1.f - a.momentum) * a.rvar[c] + a.momentum * (float)unb;
+          a.rmean[c] = (1.f - a.momentum) * rm0 + a.momentum * mean;
+          a.rvar[c] = (1.f - a.momentum) * rv0 + a.momentum * (float)unb;
         }
       }
     }
@@ -813,6 +817,13 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_apply_kernel(BnBwdFusedArgs 
   {
     const int cl = tid & 31, tl = tid >> 5;
     const int c = cg * 32 + cl;
+    // the per-channel operands first (after the trees, behind the stores
+    // they may alias, they were 3 serial round trips)
+    const float g = a.gamma ? a.gamma[c] : 1.f;
+    const float is = a.invstd[c];
+    const bool wr = sp == 0 && a.accumulate;
+    const float dg0 = (wr && a.dgamma) ? a.dgamma[c] : 0.f;
+    const float db0 = (wr && a.dbeta) ? a.dbeta[c] : 0.f;
     double s0 = 0.0, s1 = 0.0;
     for (int r0 = tl; r0 < a.nblk; r0 += 64) {
       float v0[8], v1[8];
@@ -839,15 +850,13 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_apply_kernel(BnBwdFusedArgs 
         S0 += shd[0][k][cl];
         S1 += shd[1][k][cl];
       }
-      const float g = a.gamma ? a.gamma[c] : 1.f;
-      const float is = a.invstd[c];
       const float k1 = g * is;
       sk[0][cl] = k1;
       sk[1][cl] = a.train ? (float)(-(double)k1 * is * S1 / (double)a.P) : 0.f;
       sk[2][cl] = a.train ? (float)(-(double)k1 * S0 / (double)a.P) : 0.f;
       if (sp == 0) {
-        if (a.dgamma) a.dgamma[c] = a.accumulate ? a.dgamma[c] + (float)S1 : (float)S1;
-        if (a.dbeta) a.dbeta[c] = a.accumulate ? a.dbeta[c] + (float)S0 : (float)S0;
+        if (a.dgamma) a.dgamma[c] = a.accumulate ? dg0 + (float)S1 : (float)S1;
+        if (a.dbeta) a.dbeta[c] = a.accumulate ? db0 + (float)S0 : (float)S0;
       }
     }
     __syncthreads();
