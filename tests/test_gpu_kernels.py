@@ -388,6 +388,8 @@ STREAM_CASES = [
     (64, 128, False),   # 8 column fragments per wave tile
     (128, 256, False),  # 16 column fragments, 16-pixel wave tiles
     (64, 128, True),
+    (64, 32, True),     # 2 column fragments: the GS < 4 accumulate store pass
+    (128, 256, True),   # 16 column fragments, accumulate
 ]
 
 

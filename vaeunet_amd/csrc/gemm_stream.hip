@@ -24,6 +24,8 @@
 
 namespace {
 
+template <bool B> struct BoolTag { static constexpr bool value = B; };
+
 typedef __attribute__((address_space(3))) void lds_void;
 
 template <int R>
@@ -178,57 +180,87 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
       }
       return out + m * p.out_stride + p.out_coff + col0;
     };
-    auto add_old = [&](u32x4& v, const bf16_t* dst) {
-      const u32x4 o = *reinterpret_cast<const u32x4*>(dst);
+    auto add_old = [&](u32x4& v, const u32x4 o) {
 #pragma unroll
       for (int w = 0; w < 4; ++w)
         v[w] = pack2(__uint_as_float(o[w] << 16) + __uint_as_float(v[w] << 16),
                      __uint_as_float(o[w] & 0xffff0000u) + __uint_as_float(v[w] & 0xffff0000u));
     };
+    // Two instantiations of the store pass behind ONE uniform branch: with
+    // `if (accumulate) load` inside the loop, the vmcnt(0) the compiler puts
+    // after that branch ran for plain stores too -- every store waited for
+    // the previous one (and for the next tile's prefetch), which is where
+    // most of this kernel's wave cycles were spent waiting.  Accumulate: the
+    // old values of a pixel fragment's stores are loaded together first.
+    auto store_pass = [&](auto acc_tag) {
+      constexpr bool ACC = decltype(acc_tag)::value;
 #pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int64_t m = pb + 16 * f + r16;
-#pragma unroll
-      for (int grp = 0; grp < NJ / GS; ++grp) {
+      for (int f = 0; f < NF; ++f) {
+        const int64_t m = pb + 16 * f + r16;
         if constexpr (GS == 4) {
-          u32x4 c[2];
+          u32x4 c[NJ / GS][2];
+          bf16_t* dst[NJ / GS][2];
 #pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            const f32x4 a = acc[f][grp * 4 + 2 * h2], b = acc[f][grp * 4 + 2 * h2 + 1];
-            c[h2] = u32x4{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
+          for (int grp = 0; grp < NJ / GS; ++grp) {
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const f32x4 a = acc[f][grp * 4 + 2 * h2], b = acc[f][grp * 4 + 2 * h2 + 1];
+              c[grp][h2] = u32x4{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              const auto r1 = __builtin_amdgcn_permlane16_swap(c[grp][0][w], c[grp][1][w], false, false);
+              const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
+              c[grp][0][w] = r2[0];
+              c[grp][1][w] = r2[1];
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) dst[grp][h] = dst_of(m, grp * 64 + 32 * h + 8 * gq);
+          }
+          if constexpr (ACC) {
+            u32x4 o[NJ / GS][2];
+#pragma unroll
+            for (int grp = 0; grp < NJ / GS; ++grp)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) o[grp][h] = *reinterpret_cast<const u32x4*>(dst[grp][h]);
+#pragma unroll
+            for (int grp = 0; grp < NJ / GS; ++grp)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) add_old(c[grp][h], o[grp][h]);
           }
 #pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const auto r1 = __builtin_amdgcn_permlane16_swap(c[0][w], c[1][w], false, false);
-            const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
-            c[0][w] = r2[0];
-            c[1][w] = r2[1];
-          }
+          for (int grp = 0; grp < NJ / GS; ++grp)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            bf16_t* dst = dst_of(m, grp * 64 + 32 * h + 8 * gq);
-            if (p.accumulate) add_old(c[h], dst);
-            *reinterpret_cast<u32x4*>(dst) = c[h];
-          }
+            for (int h = 0; h < 2; ++h) *reinterpret_cast<u32x4*>(dst[grp][h]) = c[grp][h];
         } else {
-          bf16_t* dst = dst_of(m, grp * 16 * GS + 4 * GS * gq);
+          bf16_t* dst = dst_of(m, 4 * GS * gq);   // NJ == GS: one column group
+          u32x4 v[GS / 2];
 #pragma unroll
           for (int h2 = 0; h2 < GS / 2; ++h2) {
-            const f32x4 a = acc[f][grp * GS + 2 * h2], b = acc[f][grp * GS + 2 * h2 + 1];
-            u32x4 v{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
-            if (p.accumulate) {
-              // out += result: unpack the stored pairs and round the sums once
-              const u32x4 o = *reinterpret_cast<const u32x4*>(dst + 8 * h2);
-              v = u32x4{pack2(__uint_as_float(o[0] << 16) + a[0], __uint_as_float(o[0] & 0xffff0000u) + a[1]),
-                        pack2(__uint_as_float(o[1] << 16) + a[2], __uint_as_float(o[1] & 0xffff0000u) + a[3]),
-                        pack2(__uint_as_float(o[2] << 16) + b[0], __uint_as_float(o[2] & 0xffff0000u) + b[1]),
-                        pack2(__uint_as_float(o[3] << 16) + b[2], __uint_as_float(o[3] & 0xffff0000u) + b[3])};
-            }
-            *reinterpret_cast<u32x4*>(dst + 8 * h2) = v;
+            const f32x4 a = acc[f][2 * h2], b = acc[f][2 * h2 + 1];
+            v[h2] = u32x4{pack2(a[0], a[1]), pack2(a[2], a[3]), pack2(b[0], b[1]), pack2(b[2], b[3])};
           }
+          if constexpr (ACC) {
+            // out += result: unpack the stored pairs and round the sums once
+            u32x4 o[GS / 2];
+#pragma unroll
+            for (int h2 = 0; h2 < GS / 2; ++h2) o[h2] = *reinterpret_cast<const u32x4*>(dst + 8 * h2);
+#pragma unroll
+            for (int h2 = 0; h2 < GS / 2; ++h2) {
+              const f32x4 a = acc[f][2 * h2], b = acc[f][2 * h2 + 1];
+              v[h2] = u32x4{pack2(__uint_as_float(o[h2][0] << 16) + a[0], __uint_as_float(o[h2][0] & 0xffff0000u) + a[1]),
+                            pack2(__uint_as_float(o[h2][1] << 16) + a[2], __uint_as_float(o[h2][1] & 0xffff0000u) + a[3]),
+                            pack2(__uint_as_float(o[h2][2] << 16) + b[0], __uint_as_float(o[h2][2] & 0xffff0000u) + b[1]),
+                            pack2(__uint_as_float(o[h2][3] << 16) + b[2], __uint_as_float(o[h2][3] & 0xffff0000u) + b[3])};
+            }
+          }
+#pragma unroll
+          for (int h2 = 0; h2 < GS / 2; ++h2) *reinterpret_cast<u32x4*>(dst + 8 * h2) = v[h2];
         }
       }
-    }
+    };
+    if (p.accumulate) store_pass(BoolTag<true>{});
+    else store_pass(BoolTag<false>{});
   }
 }
 
