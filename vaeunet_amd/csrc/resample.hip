@@ -338,6 +338,27 @@ __global__ __launch_bounds__(256) void input_pack8_kernel(const float* x, int64_
   }
 }
 
+// The common case of the packing: a dense NHWC 3-channel fp32 image (the
+// channels_last input batch).  A lane takes 4 pixels = 48 contiguous bytes
+// (three 16-byte loads) and writes their 4 x 8 channels contiguously: no
+// pixel decode, no 12-byte-strided scalar loads.
+template <typename TO>
+__global__ __launch_bounds__(256) void input_pack3x4_kernel(const float* x, int64_t Q, TO* y) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += (int64_t)gridDim.x * blockDim.x) {
+    const f32x4* s = reinterpret_cast<const f32x4*>(x + q * 12);
+    const f32x4 a = s[0], b = s[1], c = s[2];
+    const float v[12] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3], c[0], c[1], c[2], c[3]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      Vec8<TO> o;
+      o.zero();
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) o.set(ch, v[3 * k + ch]);
+      o.store(y + (q * 4 + k) * 8);
+    }
+  }
+}
+
 }  // namespace
 
 #define DISPATCH_T(dtype, ...) \
@@ -707,6 +728,13 @@ extern "C" int vu_input_pack(const float* x, int64_t sn, int64_t sc, int64_t sh,
   int64_t tot = (int64_t)N * H * W * Cp;
   if (tot == 0) return 0;
   const int64_t P = (int64_t)N * H * W;
+  if (Cp == 8 && C == 3 && sc == 1 && sw == 3 && sh == 3 * (int64_t)W && sn == 3 * (int64_t)H * W && P % 4 == 0 &&
+      ((uintptr_t)x & 15) == 0) {
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((input_pack3x4_kernel<T>), dim3(ew_grid(P / 4)), dim3(256), 0, st, x, P / 4, (T*)y);
+    })
+    return (int)hipGetLastError();
+  }
   if (Cp == 8 && C >= 1 && C <= 8 && P < ((int64_t)1 << 31) && (int64_t)H * W < ((int64_t)1 << 31)) {
     DISPATCH_T(dtype, {
       hipLaunchKernelGGL((input_pack8_kernel<T>), dim3(ew_grid(P)), dim3(256), 0, st, x, sn, sc, sh, sw, (int)P, C,
