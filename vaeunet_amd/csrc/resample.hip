@@ -223,6 +223,65 @@ __global__ void upsample_bwd_kernel(const T* dy, int64_t dys, int N, int Hi, int
     float o[VW];
 #pragma unroll
     for (int k = 0; k < VW; ++k) o[k] = 0.f;
+    if constexpr (VW == 8) {
+      // the contributing output rows / columns (<= 4 each for the 2x
+      // upsampling) collected first, then all their loads issued together and
+      // summed in the same (row, column) order as the loop below, which
+      // issued one load per memory round trip
+      // (static slots filled by selects: a dynamically indexed array was
+      // placed in LDS by the compiler)
+      int yv[4] = {0, 0, 0, 0}, xv[4] = {0, 0, 0, 0};
+      float wyv[4] = {0.f, 0.f, 0.f, 0.f}, wxv[4] = {0.f, 0.f, 0.f, 0.f};
+      int ny = 0, nx = 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int yy = ylo + r;
+        const float wy = yy <= yhi ? ac_w(yy, i, sh, Hi) : 0.f;
+        const bool ok = wy != 0.f && yy + py >= 0 && yy + py < Hp;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (ok && ny == t) { yv[t] = yy; wyv[t] = wy; }
+        ny += ok ? 1 : 0;
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int xx = xlo + r;
+        const float wx = xx <= xhi ? ac_w(xx, j, sw, Wi) : 0.f;
+        const bool ok = wx != 0.f && xx + px >= 0 && xx + px < Wp;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (ok && nx == t) { xv[t] = xx; wxv[t] = wx; }
+        nx += ok ? 1 : 0;
+      }
+      if (ny <= 4 && nx <= 4 && yhi - ylo < 8 && xhi - xlo < 8) {
+        Vec8<T> v[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            // slots past the counts re-load slot 0's pixel (in range: clamped
+            // to row / column py, px when there is no contributor at all)
+            const int yy = a < ny ? yv[a] : (ny > 0 ? yv[0] : -py);
+            const int xx = b < nx ? xv[b] : (nx > 0 ? xv[0] : -px);
+            v[a][b].load(dy + (((int64_t)n * Hp + yy + py) * Wp + xx + px) * dys + c);
+          }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            if (a >= ny || b >= nx) continue;
+            const float wgt = wyv[a] * wxv[b];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] += wgt * v[a][b].get(k);
+          }
+        T* dst = dx + q * dxs + c;
+        Vec8<T> w8;
+        if (accumulate) { w8.load(dst); for (int k = 0; k < 8; ++k) o[k] += w8.get(k); }
+        for (int k = 0; k < 8; ++k) w8.set(k, o[k]);
+        w8.store(dst);
+        continue;
+      }
+    }
     for (int yy = ylo; yy <= yhi; ++yy) {
       float wy = ac_w(yy, i, sh, Hi);
       if (wy == 0.f) continue;
