@@ -352,7 +352,11 @@ def vae_secondary(args):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)
     if r.returncode != 0:
         return {"error": f"exit {r.returncode}"}
-    sec = json.loads(r.stdout.strip().splitlines()[-1])
+    lines = r.stdout.strip().splitlines()
+    try:
+        sec = json.loads(lines[-1])
+    except (IndexError, ValueError) as e:   # never lose the measured headline over the secondary
+        return {"error": f"unparsable child output: {e!r}"}
     for k in ("metric", "higher_is_better", "vs_baseline", "cpu_baseline", "parity", "data", "n_gpus"):
         sec.pop(k, None)
     return sec
@@ -392,7 +396,10 @@ def main():
             mod = importlib.import_module("vaeunet_amd." + modname)
         if not hasattr(mod, name):
             raise SystemExit(f"bench: no engine switch {name}")
-        setattr(mod, name, bool(int(val)))
+        old = getattr(mod, name)
+        # keep the knob's type: a bool switch stays a bool, an integer knob
+        # (e.g. kernels.WGRAD_SPLIT_CAP=4) keeps its value
+        setattr(mod, name, bool(int(val)) if isinstance(old, bool) else type(old)(int(val)))
     from vaeunet_amd.loss import CombinedLoss
     from vaeunet_amd import parallel
 

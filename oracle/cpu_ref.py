@@ -37,6 +37,28 @@ import torch.nn.functional as F
 # ----------------------------------------------------------------------------
 # primitives
 # ----------------------------------------------------------------------------
+# Conditioning probe (tests only): when set to a dict, every train-mode
+# BatchNorm records (xhat, output) under its prefix and keeps the output's
+# gradient, so a test can form the per-channel sums of |terms| of the affine
+# gradients (sum |dz| for the bias, sum |dz * xhat| for the weight) -- the
+# conditioning of those reductions (tests/test_gpu_config_parity.py).
+PROBE = None
+
+
+def probe_bn_conditioning():
+    """{prefix + 'weight' / 'bias': per-channel sum of |terms|} of the probed
+    BatchNorms after backward (fp64 run)."""
+    out = {}
+    for pre, v in PROBE.items():
+        if pre.startswith("gate:"):
+            continue
+        xh, y = v
+        dz = y.grad
+        out[pre + "bias"] = dz.abs().sum(dim=(0, 2, 3)).detach().double()
+        out[pre + "weight"] = (dz * xh.detach()).abs().sum(dim=(0, 2, 3)).double()
+    return out
+
+
 def batch_norm_train(x, p, pre, bufs, momentum=0.1, eps=1e-5):
     """Batch statistics over (N,H,W); biased var for normalisation, unbiased
     for the running estimate (in-place on ``bufs``)."""
@@ -50,7 +72,11 @@ def batch_norm_train(x, p, pre, bufs, momentum=0.1, eps=1e-5):
             rv.mul_(1 - momentum).add_(momentum * var.detach() * n / max(n - 1, 1))
             bufs[pre + "num_batches_tracked"] += 1
     xh = (x - mean[None, :, None, None]) / torch.sqrt(var[None, :, None, None] + eps)
-    return xh * p[pre + "weight"][None, :, None, None] + p[pre + "bias"][None, :, None, None]
+    y = xh * p[pre + "weight"][None, :, None, None] + p[pre + "bias"][None, :, None, None]
+    if PROBE is not None and y.requires_grad:
+        y.retain_grad()
+        PROBE[pre] = (xh, y)
+    return y
 
 
 def batch_norm_eval(x, p, pre, bufs, eps=1e-5):
@@ -89,8 +115,15 @@ def attention_gate(g, x, p, pre, bufs, train):
     g1 = bn(conv(g, p, pre + "W_g.0."), p, pre + "W_g.1.", bufs, train)
     x1 = bn(conv(x, p, pre + "W_x.0."), p, pre + "W_x.1.", bufs, train)
     s = torch.relu(g1 + x1)
-    psi = torch.sigmoid(bn(conv(s, p, pre + "psi.0."), p, pre + "psi.1.", bufs, train))
-    return x * psi
+    q = conv(s, p, pre + "psi.0.")
+    z = bn(q, p, pre + "psi.1.", bufs, train)
+    psi = torch.sigmoid(z)
+    out = x * psi
+    if PROBE is not None and out.requires_grad:   # test probe: the gate's intermediates
+        for t in (z, psi, out):
+            t.retain_grad()
+        PROBE["gate:" + pre] = (q, z, psi, out)
+    return out
 
 
 def up(x1, x2, p, pre, bufs, train, bilinear):

@@ -222,11 +222,24 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
 # parameter gradient of the HIP fp32 path vs the fp64 oracle, judged against
 # the fp32 oracle's OWN error at the same size (the reference's CPU fp32
 # autograd is what a user of the reference gets):
-#   ||g_hip - g64||  <=  GRAD_ERR_FACTOR * ||g32 - g64||  +  GRAD_ERR_FLOOR * max_k ||g64_k||
-# (the floor: an error below 1e-6 of the largest parameter gradient is fp32
-# summation noise -- a cancellation-dominated sum such as an attention psi
-# BatchNorm(1) bias gradient carries a relative error of several % in the
-# reference's own fp32 path).  Gradients that are mathematically zero (the bias of a conv feeding a
+#
+#   ||g_hip - g64||  <=  GRAD_ERR_FACTOR * ( ||g32 - g64||  +  sigma_k  +  u32 * ||g64|| )
+#
+# sigma_k, per BatchNorm affine gradient (round 5, replaces round 4's global
+# floor 1e-6 * max_k ||g64_k||): the gradient is a reduction over pixels,
+# dbeta = sum_p dz_p and dgamma = sum_p dz_p * xhat_p, and its error is the
+# sum of its terms' errors.  The oracle probes every BatchNorm
+# (oracle/cpu_ref.PROBE) and sigma_k = || t32 - t64 ||_2 over the terms t of
+# that reduction: the spread a sum of the terms has when each term carries the
+# fp32 oracle's own per-term error (independent term errors add in quadrature).
+# It matters where a reduction is ill-conditioned, sum |t| >> |sum t|: the
+# attention psi BatchNorm(1) bias at up2 has sum |dz| / |sum dz| = 4.5e3, so
+# the ~0.5 % per-pixel error the fp32 backward carries at that depth (oracle:
+# 4.7e-3, HIP path: 7.4e-3 -- measured by tools/psi_probe.py,
+# profiles/r5a_psi_probe.log) becomes 4-25 % on the sum, and that sum of the
+# HIP path's own dbnq in fp64 reproduces the HIP gradient's error exactly (the
+# reduction kernels add nothing).  u32 * ||g64||: storing the result in fp32.
+# Gradients that are mathematically zero (the bias of a conv feeding a
 # train-mode BatchNorm: BN(x + b) does not depend on b) are written as exact
 # zeros by the HIP path for the 1x1 / ConvT convs (engine.bias_grad), where
 # the reference's autograd leaves summation noise (the psi conv's bias, summed
@@ -234,11 +247,11 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
 # floor 1e-5 * max ||g||" instead, and the exact zeros are counted.
 # ---------------------------------------------------------------------------
 GRAD_ERR_FACTOR = 4.0
-GRAD_ERR_FLOOR = 1e-6
+U32 = 2.0 ** -24
 BW_B = 2
 
 
-def _grad_adjudicate(tag, names, g_hip, g32, g64):
+def _grad_adjudicate(tag, names, g_hip, g32, g64, sigma):
     gmax = max(float(g.norm()) for g in g64.values())
     worst, zero = [], []
     for k in names:
@@ -250,13 +263,14 @@ def _grad_adjudicate(tag, names, g_hip, g32, g64):
             continue
         d_h = float((g_hip[k] - g64[k]).norm())
         d_32 = float((g32[k] - g64[k]).norm())
+        s = sigma.get(k, 0.0)
         # > 1: outside the bound
-        worst.append((d_h / (GRAD_ERR_FACTOR * d_32 + GRAD_ERR_FLOOR * gmax), k, d_h / r, d_32 / r))
+        worst.append((d_h / (GRAD_ERR_FACTOR * (d_32 + s + U32 * r)), k, d_h / r, d_32 / r, s / r))
     worst.sort(reverse=True)
-    print(f"{tag}: {len(worst)} gradients adjudicated vs fp64, {len(zero)} mathematically zero "
-          f"({sum(zero)} written as exact zeros); worst "
-          f"(err / bound, name, HIP rel err, fp32-oracle rel err): "
-          f"{[(f'{a:.2e}', b, f'{c:.2e}', f'{d:.2e}') for a, b, c, d in worst[:4]]}")
+    print(f"{tag}: {len(worst)} gradients adjudicated vs fp64 ({len(sigma)} BatchNorm-affine with a term "
+          f"spread), {len(zero)} mathematically zero ({sum(zero)} written as exact zeros); worst "
+          f"(err / bound, name, HIP rel err, fp32-oracle rel err, term spread / |g|): "
+          f"{[(f'{a:.2e}', b, f'{c:.2e}', f'{d:.2e}', f'{e:.2e}') for a, b, c, d, e in worst[:4]]}")
     assert worst[0][0] <= 1.0, worst[:4]
     return worst
 
@@ -266,14 +280,41 @@ def _bw_batch(classes):
     return x[:BW_B].contiguous(memory_format=CL), t[:BW_B].contiguous()
 
 
-def _oracle_grads(fwd, state, dtype):
+def _oracle_grads(fwd, state, dtype, probe=False):
+    """The oracle's gradients (fp64 copies) and loss; probe: also the terms
+    of every train-mode BatchNorm's affine-gradient reductions
+    (prefix+'bias': dz, prefix+'weight': dz * xhat), in fp64."""
+    from oracle import cpu_ref as R
     p, bufs = _split(state, dtype)
     for v in p.values():
         v.requires_grad_(True)
-    loss = fwd(p, bufs)
-    loss.backward()
-    return {k: v.grad.detach().double() if v.grad is not None else torch.zeros_like(v, dtype=torch.float64)
-            for k, v in p.items()}, float(loss.detach())
+    R.PROBE = {} if probe else None
+    try:
+        loss = fwd(p, bufs)
+        loss.backward()
+        terms = {}
+        if probe:
+            for pre, v in R.PROBE.items():
+                if pre.startswith("gate:"):
+                    continue
+                xh, y = v
+                dz = y.grad.detach().double()
+                terms[pre + "bias"] = dz
+                terms[pre + "weight"] = dz * xh.detach().double()
+    finally:
+        R.PROBE = None
+    grads = {k: v.grad.detach().double() if v.grad is not None else torch.zeros_like(v, dtype=torch.float64)
+             for k, v in p.items()}
+    return grads, float(loss.detach()), terms
+
+
+def _oracle_pair(fwd, state):
+    """fp64 and fp32 oracle gradients + the per-BatchNorm term spreads sigma."""
+    g64, loss64, t64 = _oracle_grads(fwd(torch.float64), state, torch.float64, probe=True)
+    g32, _, t32 = _oracle_grads(fwd(torch.float32), state, torch.float32, probe=True)
+    sigma = {k: float((t32[k] - t64[k]).norm()) for k in t64 if k in t32}
+    del t32, t64
+    return g32, g64, loss64, sigma
 
 
 @pytest.mark.timeout(900)
@@ -287,17 +328,17 @@ def test_unet_config2_fp32_backward_512_vs_fp64():
     state = model.state_dict()
     names = [k for k, _ in model.named_parameters()]
     x, t = _bw_batch(2)
-    g32, loss32 = _oracle_grads(lambda p, b: R.combined_loss(R.unet_forward(x, p, b, True), t), state,
-                                torch.float32)
-    g64, loss64 = _oracle_grads(lambda p, b: R.combined_loss(R.unet_forward(x.double(), p, b, True), t.double()),
-                                state, torch.float64)
+
+    def fwd(dtype):
+        return lambda p, b: R.combined_loss(R.unet_forward(x.to(dtype), p, b, True), t.to(dtype))
+    g32, g64, loss64, sigma = _oracle_pair(fwd, state)
     model = model.to(DEV).to(memory_format=CL).train()
     loss = CombinedLoss()(model(x.to(DEV)), t.to(DEV))
     loss.backward()
     assert abs(float(loss.detach()) - loss64) < 1e-5
     params = dict(model.named_parameters())
     gh = {k: params[k].grad.detach().double().cpu() for k in names}
-    _grad_adjudicate("config2 fp32 backward B=2 512^2", names, gh, g32, g64)
+    _grad_adjudicate("config2 fp32 backward B=2 512^2", names, gh, g32, g64, sigma)
 
 
 @pytest.mark.timeout(900)
@@ -318,8 +359,7 @@ def test_unetresnet_config3_fp32_backward_512_vs_fp64():
             lg, mu, lv = R.unet_resnet_forward(x.to(dtype), p, b, eps=eps.to(dtype))
             return R.combined_loss(lg, t.to(dtype)) + 1e-3 * R.kl_with_free_bits(mu, lv, 1e-3)
         return f
-    g32, _ = _oracle_grads(fwd(torch.float32), state, torch.float32)
-    g64, loss64 = _oracle_grads(fwd(torch.float64), state, torch.float64)
+    g32, g64, loss64, sigma = _oracle_pair(fwd, state)
     model = model.to(DEV).to(memory_format=CL).train()
     model.eps_override = eps.to(DEV)
     lg, mu, lv = model(x.to(DEV))
@@ -329,4 +369,4 @@ def test_unetresnet_config3_fp32_backward_512_vs_fp64():
     params = dict(model.named_parameters())
     gh = {k: (params[k].grad.detach().double().cpu() if params[k].grad is not None
               else torch.zeros_like(params[k], dtype=torch.float64, device="cpu")) for k in names}
-    _grad_adjudicate("config3 fp32 backward B=2 512^2", names, gh, g32, g64)
+    _grad_adjudicate("config3 fp32 backward B=2 512^2", names, gh, g32, g64, sigma)

@@ -303,13 +303,37 @@ def test_double_conv_fp8_delayed_scaling(up):
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         yb = mod(torch.cat(xs, 1)).float()
     for step in range(3):
-        yd = fp8.double_conv_forward(mod, xs).float()
+        yd = fp8.double_conv_forward(mod, xs, delayed=True).float()
         assert ((yd - yj).abs().max() / yj.abs().max()).item() < 0.03, step
         assert ((yd - yb).abs().max() / yb.abs().max()).item() < 0.15, step
         ds_in, ds_mid, _ = mod._vu_fp8_scales
         assert ds_in.t == step + 1
         assert ds_in.ring[ds_in.slot].item() == max(float(t.float().abs().max()) for t in xs)
         assert ds_mid.ring[ds_mid.slot].item() > 0
+
+
+def test_double_conv_fp8_default_is_self_contained():
+    """the default forward scales just in time, so a second call on
+    a 4x-larger input is not clipped by the first call's amax; a delayed call
+    after reset_scales calibrates again (equal to just-in-time on its first
+    call); chained arguments without delayed=True are refused."""
+    from vaeunet_amd import DoubleConv, fp8
+    torch.manual_seed(8)
+    mod = DoubleConv(64, 64).to(DEV)
+    x = _act(torch.randn(2, 64, 32, 64).relu())
+    x4 = _act(4.0 * torch.randn(2, 64, 32, 64).relu())
+    fp8.double_conv_forward(mod, x)
+    y_default = fp8.double_conv_forward(mod, x4).float()
+    fresh = DoubleConv(64, 64).to(DEV)
+    fresh.load_state_dict(mod.state_dict())
+    y_fresh = fp8.double_conv_forward(fresh, x4).float()
+    assert torch.equal(y_default, y_fresh)
+    fp8.double_conv_forward(mod, x, delayed=True)     # history at x's range
+    fp8.reset_scales(mod)
+    y_cal = fp8.double_conv_forward(mod, x4, delayed=True).float()   # calibrates on x4
+    assert ((y_cal - y_fresh).abs().max() / y_fresh.abs().max()).item() < 0.03
+    with pytest.raises(ValueError):
+        fp8.double_conv_forward(mod, None, x_q=([x], torch.ones(1, device=DEV)))
 
 
 def test_double_conv_fp8_chained():
@@ -326,8 +350,8 @@ def test_double_conv_fp8_chained():
     fp8.calibrate(x, None, False, ds)
     xq, xdq = fp8.bn_apply_quant(x, None, False, ds)
     for step in range(3):
-        ref = fp8.double_conv_forward(mod, None, x_q=([xq], xdq))          # same input, bf16 output
-        q, dq = fp8.double_conv_forward(mod, None, x_q=([xq], xdq), out_fp8=True)
+        ref = fp8.double_conv_forward(mod, None, delayed=True, x_q=([xq], xdq))   # same input, bf16 output
+        q, dq = fp8.double_conv_forward(mod, None, delayed=True, x_q=([xq], xdq), out_fp8=True)
         got = q.float() * dq
         err = (got - ref.float()).abs()
         assert (err <= 2.0 ** -3 * ref.float().abs() + 1e-3 * ref.float().abs().max()).all(), step

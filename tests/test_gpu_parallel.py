@@ -295,3 +295,75 @@ def test_dp_unused_parameter_left_untouched():
         assert ok and moved > 0, (mode, ok, moved)
         for name, grad_none, same, nstate in ok:
             assert same and nstate == 0, (mode, name, grad_none, same, nstate)
+
+
+def _grads_worker(rank, world, port, backend, out_q):
+    """Every parameter the single-process backward gives a gradient gets the
+    SAME gradient through the DP reducer at world 1 (RCCL AVG over one rank is
+    exact), and no other parameter gets one: UNet and UNetResNet in every
+    latent-injection mode (the reducer must never drop a gradient
+    a backward path forgot to report)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        from vaeunet_amd import UNet, UNetResNet, parallel
+        from vaeunet_amd.init import seeded_init_
+        from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
+        g = torch.Generator().manual_seed(9)
+        x = torch.rand(2, 3, 64, 64, generator=g).cuda().contiguous(memory_format=torch.channels_last)
+        t1 = (torch.rand(2, 1, 64, 64, generator=g) > 0.5).float().cuda()
+        t2 = torch.cat([1 - t1, t1], 1)
+        cases = [("unet", None)] + [("vae", m) for m in ("all", "none", "first", "last", "bottleneck",
+                                                                   "inject_no_bottleneck")]
+        res = {}
+        for kind, inj in cases:
+            grads = []
+            for use_red in (False, True):
+                if kind == "unet":
+                    model = seeded_init_(UNet(3, 2), 0)
+                else:
+                    model = seeded_init_(UNetResNet(3, 1, pretrained=False, latent_injection=inj), 0)
+                model = model.cuda().to(memory_format=torch.channels_last).train()
+                if kind == "vae":
+                    model.eps_override = torch.randn(2, 32, generator=torch.Generator().manual_seed(3)).cuda()
+                red = parallel.attach(model, bucket_bytes=2 * 1024 * 1024) if use_red else None
+                if red is not None:
+                    red.prepare()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    if kind == "unet":
+                        loss = CombinedLoss()(model(x), t2)
+                    else:
+                        lg, mu, lv = model(x)
+                        loss = CombinedLoss()(lg, t1) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+                loss.backward()
+                if red is not None:
+                    red.finish()
+                torch.cuda.synchronize()
+                grads.append({n: (p.grad.detach().float().cpu().clone() if p.grad is not None else None)
+                              for n, p in model.named_parameters()})
+            plain, dp = grads
+            bad = [n for n in plain if (plain[n] is None) != (dp[n] is None)
+                   or (plain[n] is not None and not torch.equal(plain[n], dp[n]))]
+            res[f"{kind}:{inj}"] = (bad, sum(v is None for v in plain.values()), len(plain))
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_reducer_gradients_equal_single_process():
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join(
+        [os.path.dirname(here), here] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_grads_worker, args=(0, 1, _free_port(), "nccl", q))
+    p.start()
+    _, res = q.get(timeout=280)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for case, (bad, n_none, n) in res.items():
+        assert not bad, (case, bad[:8])
+        if case.startswith("unet"):
+            assert n_none == 0

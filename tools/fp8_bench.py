@@ -57,19 +57,19 @@ def double_main(args):
         def bf16():
             E.double_conv_fwd(M, mod.double_conv, srcs)
         msb = timeit(bf16, args.reps)
-        ms8 = timeit(lambda: fp8.double_conv_forward(mod, srcs), args.reps)
+        ms8 = timeit(lambda: fp8.double_conv_forward(mod, srcs, delayed=True), args.reps)
         msj = timeit(lambda: fp8.double_conv_forward(mod, srcs, delayed=False), args.reps)
         # chained: input already e4m3 (quantised by the producing block), output e4m3
-        xq = fp8.double_conv_forward(mod, srcs)  # (warm the scales)
+        xq = fp8.double_conv_forward(mod, srcs, delayed=True)  # (warm the scales)
         dsq = fp8.DelayedScale(dev)
         fp8.calibrate(srcs[0], None, False, dsq)
         qin = [fp8.bn_apply_quant(t, None, False, dsq)[0] for t in srcs]
         qdq = fp8.bn_apply_quant(srcs[0], None, False, dsq)[1]
         del xq
-        msc = timeit(lambda: fp8.double_conv_forward(mod, None, x_q=(qin, qdq), out_fp8=True), args.reps)
+        msc = timeit(lambda: fp8.double_conv_forward(mod, None, delayed=True, x_q=(qin, qdq), out_fp8=True), args.reps)
         with torch.no_grad():
             yb = E.double_conv_fwd(M, mod.double_conv, srcs)[0].float()
-            y8 = fp8.double_conv_forward(mod, srcs).float()
+            y8 = fp8.double_conv_forward(mod, srcs, delayed=True).float()
         row = {"block": name, "cin": ci, "cout": co, "hw": H, "bf16_us": round(msb * 1e3, 1),
                "fp8_us": round(ms8 * 1e3, 1), "fp8_jit_us": round(msj * 1e3, 1),
                "fp8_chain_us": round(msc * 1e3, 1),

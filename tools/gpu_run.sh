@@ -1,0 +1,89 @@
+#!/bin/bash
+# One parameterised GPU-box run: a chain of steps, each under its own time
+# limit, stopping at the first failure.  Replaces the per-call gpu_r4*.sh
+# scripts of round 4.
+#
+# usage: bash tools/gpu_run.sh <tag> <step> [<step> ...]      -> gpurun_out/<tag>/
+# steps:
+#   tests[:<pytest -k or file list, comma separated>]  GPU tests (default: whole -m gpu suite)
+#   bench[:<model>]        the default bench line (model unet: CPU leg + config-3 secondary)
+#   ab[:<model>[:<reps>]]  whole-tree A/B vs the tree copied to ab/tree (alternating, same box)
+#   flag:<module.NAME>[:<model>]  A/B of an engine flag (0 vs 1) on the current tree
+#   prof[:<model>]         rocprofv3 --kernel-trace --stats of a short bench -> <model>_kernel_stats.csv
+#   evidence               tools/gpu_evidence.sh (both benches profiled + PMC traffic + tables)
+#   conv[:<args>]          tools/conv_bench.py with the given args (spaces as '+')
+#   enc[:<args>]           tools/enc_bench.py with the given args (spaces as '+')
+#   py:<script>[:<args>]   any python tool under tools/ (args: spaces as '+')
+set -o pipefail
+export TMPDIR=/tmp
+tag=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$tag
+mkdir -p $O
+cd $R
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}
+  arg=""; [[ "$step" == *:* ]] && arg=${step#*:}
+  case $kind in
+    tests)
+      sel="tests"
+      if [ -n "$arg" ]; then
+        if [[ "$arg" == tests/* ]]; then sel=${arg//,/ }; else sel="tests -k ${arg//,/ or }"; fi
+      fi
+      timeout -k 10 1000 python -u -m pytest $sel -m gpu -x -q --timeout 300 --timeout-method thread \
+        > $O/tests_$n.log 2>&1 || { echo "TESTS_FAIL ($step)"; tail -40 $O/tests_$n.log; exit 1; }
+      tail -1 $O/tests_$n.log ;;
+    bench)
+      m=${arg:-unet}
+      extra=""; [ "$m" != unet ] && extra="--model $m"
+      timeout -k 10 600 python -u bench.py $extra > $O/bench_$m.json 2> $O/bench_$m.err \
+        || { echo "BENCH_FAIL $m"; tail -20 $O/bench_$m.err; exit 1; }
+      tail -1 $O/bench_$m.json | cut -c1-240 ;;
+    ab)
+      m=${arg%%:*}; m=${m:-unet}
+      reps=2; [[ "$arg" == *:* ]] && reps=${arg#*:}
+      for i in $(seq 1 $reps); do
+        (cd ab/tree && timeout -k 10 300 python -u bench.py --model $m --no-cpu-baseline --no-roofline --steps 40) \
+          > $O/ab_${m}_old_$i.log 2>&1 || { echo "AB_FAIL old $m"; tail -5 $O/ab_${m}_old_$i.log; exit 1; }
+        timeout -k 10 300 python -u bench.py --model $m --no-cpu-baseline --no-roofline --steps 40 \
+          > $O/ab_${m}_new_$i.log 2>&1 || { echo "AB_FAIL new $m"; tail -5 $O/ab_${m}_new_$i.log; exit 1; }
+        python tools/ab_line.py "$m rep$i" $O/ab_${m}_old_$i.log $O/ab_${m}_new_$i.log | tee -a $O/ab_summary.txt
+      done ;;
+    flag)
+      f=${arg%%:*}; m=unet; [[ "$arg" == *:* ]] && m=${arg#*:}
+      for i in 1 2; do
+        for v in 0 1; do
+          timeout -k 10 300 python -u bench.py --model $m --no-cpu-baseline --no-roofline --steps 40 \
+            --engine-flag $f=$v > $O/flag_${f}_${m}_${v}_$i.log 2>&1 || { echo "FLAG_FAIL $f=$v"; tail -5 $O/flag_${f}_${m}_${v}_$i.log; exit 1; }
+        done
+        python tools/ab_line.py "$f $m rep$i (0 vs 1)" $O/flag_${f}_${m}_0_$i.log $O/flag_${f}_${m}_1_$i.log | tee -a $O/ab_summary.txt
+      done ;;
+    prof)
+      m=${arg:-unet}
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$m -o p -- \
+        python -u $R/bench.py --model $m --steps 10 --warmup 3 --no-cpu-baseline --no-roofline > $O/prof_$m.log 2>&1) \
+        || { echo "PROF_FAIL $m"; tail -5 $O/prof_$m.log; exit 1; }
+      find $O/prof_$m -name "*kernel_stats.csv" -exec cp {} $O/${m}_kernel_stats.csv \;
+      rm -rf $O/prof_$m
+      echo "prof $m done" ;;
+    evidence)
+      bash tools/gpu_evidence.sh $tag || exit 1 ;;
+    conv)
+      timeout -k 10 400 python -u tools/conv_bench.py ${arg//+/ } > $O/conv_$n.log 2>&1 \
+        || { echo "CONV_FAIL"; tail -10 $O/conv_$n.log; exit 1; }
+      tail -3 $O/conv_$n.log ;;
+    enc)
+      timeout -k 10 300 python -u tools/enc_bench.py ${arg//+/ } > $O/enc_$n.log 2>&1 \
+        || { echo "ENC_FAIL"; tail -10 $O/enc_$n.log; exit 1; }
+      tail -3 $O/enc_$n.log ;;
+    py)
+      s=${arg%%:*}; a=""; [[ "$arg" == *:* ]] && a=${arg#*:}
+      timeout -k 10 500 python -u tools/$s ${a//+/ } > $O/py_${n}_${s%.py}.log 2>&1 \
+        || { echo "PY_FAIL $s"; tail -15 $O/py_${n}_${s%.py}.log; exit 1; }
+      tail -3 $O/py_${n}_${s%.py}.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "gpu_run $tag done"

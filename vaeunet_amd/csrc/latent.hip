@@ -307,6 +307,11 @@ constexpr int LB_NCH = 8;   // samples per split-sum round
 constexpr int LB_ODW = 8;   // weight-gradient rows held per thread (LB_CW * 64 / LB_T)
 constexpr int LH_CW = 8;    // encoder channels per latent_bwd_heads block
 constexpr int LH_ODW = 4;   // head weight-gradient elements per thread (2 * 64 * LH_CW / LB_T)
+// latent_bwd_bn's split-sum phase: thread (q8, c) adds splits 4 q8 .. 4 q8 + 3
+// of sample k = q8 -- i.e. the 8 thread groups cover exactly LAT_SPLITS splits
+// and the block is exactly LB_NCH sample rows of LB_CW channels
+static_assert(LAT_SPLITS == 4 * (LB_T / LB_CW), "latent_bwd_bn: split sums assume 4 splits per thread group");
+static_assert(LB_T == LB_NCH * LB_CW, "latent_bwd_bn: one sample row per thread group");
 
 // Global-address-space pointers: through plain (generic) pointers the
 // compiler emits flat loads / stores, which also count in lgkmcnt, so every

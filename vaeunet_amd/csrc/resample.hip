@@ -614,6 +614,9 @@ __global__ __launch_bounds__(256) void permute4_batch_kernel(const VuPermJob* jo
   const int a = q == 0 ? 1 : 0, c = q == 2 ? 1 : 2;  // the two batch dims, in order
   const uint32_t tq = (d[q] + TT - 1) / TT, t3 = (d[3] + TT - 1) / TT;
   const uint32_t b = blk / (tq * t3), rem = blk - b * (tq * t3);
+  // a caller that sized the job's block range for another tile size: blocks
+  // past the job's real tile count do nothing (block-uniform, before the barrier)
+  if (b >= (uint32_t)d[a] * (uint32_t)d[c]) return;
   const int iq0 = (int)(rem / t3) * TT, i30 = (int)(rem - (rem / t3) * t3) * TT;
   const int ia = (int)(b / d[c]), ic = (int)(b - (b / d[c]) * d[c]);
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;

@@ -173,27 +173,41 @@ def conv3x3_q(srcs, weight, bias=None, stats=False):
 
 
 def _site_scales(mod, device):
+    """The module's three DelayedScale sites (input, mid, output).  They are
+    not module state (not in state_dict, not moved by .to()): a module used
+    on another device starts a fresh history (calibration step) there."""
     ent = mod.__dict__.get("_vu_fp8_scales")
-    if ent is None:
+    if ent is None or ent[0].ring.device != torch.device(device):
         ent = (DelayedScale(device), DelayedScale(device), DelayedScale(device))
         mod.__dict__["_vu_fp8_scales"] = ent
     return ent
 
 
+def reset_scales(mod):
+    """Forget the delayed-scaling history of ``mod`` (e.g. between train and
+    eval, or before inputs with a different range): the next delayed call
+    calibrates again."""
+    mod.__dict__.pop("_vu_fp8_scales", None)
+
+
 @torch.no_grad()
-def double_conv_forward(mod, x, delayed=True, x_q=None, out_fp8=False):
+def double_conv_forward(mod, x, delayed=False, x_q=None, out_fp8=False):
     """DoubleConv.forward (unet_parts.py:32-49) with both 3x3 convs in fp8:
     conv -> BatchNorm (batch statistics from the fp8 conv epilogue in train
     mode, running statistics in eval mode) -> ReLU, twice; bf16 NHWC out.
     x: a bf16 NHWC tensor, or the list of channel-concat sources of an Up
     block's DoubleConv (they share one scale, as in conv3x3_q).
 
-    delayed=True (default): both activation quantisations use the amax the
-    previous call recorded (DelayedScale, one per site, kept on the module):
-    the input is quantised in one pass (no amax pass) and BN1 + ReLU is
+    delayed=False (default): just-in-time scaling (amax pass + quantise pass
+    of the input and of the bf16 BN1 output): every call is self-contained.
+    delayed=True (opt-in, for step loops over same-range data): both
+    activation quantisations use the amax the previous call recorded
+    (DelayedScale, one per site, kept on the module; ``reset_scales`` drops
+    it): the input is quantised in one pass (no amax pass) and BN1 + ReLU is
     applied and quantised in the same pass (vu_bn_apply_fp8), so conv2's
-    input is never stored in bf16.  delayed=False: just-in-time scaling
-    (amax pass + quantise pass of the bf16 BN1 output).
+    input is never stored in bf16.  Values above the previous call's amax
+    saturate at +-448.  The host-side slot counter advances per call: a
+    captured graph would freeze it, so delayed calls are not graph-safe.
 
     Chained fp8 blocks (delayed only): ``x_q = (e4m3 sources, dequant scale)``
     is an input already quantised by the producing block, and
@@ -202,6 +216,8 @@ def double_conv_forward(mod, x, delayed=True, x_q=None, out_fp8=False):
     the activations between fp8 blocks are then never stored in bf16."""
     conv1, bn1, _, conv2, bn2, _ = mod.double_conv
     srcs = list(x) if isinstance(x, (list, tuple)) else ([x] if x is not None else [])
+    if (x_q is not None or out_fp8) and not delayed:
+        raise ValueError("fp8.double_conv_forward: x_q / out_fp8 (chained fp8 blocks) need delayed=True")
     if not delayed:
         a = srcs
         for conv, bn in ((conv1, bn1), (conv2, bn2)):

@@ -52,6 +52,7 @@ class GradBucketReducer:
         self._pending = None
         self._handles = []
         self._sync = True
+        self._unused = {}          # id(param) -> reported-never AND zero slot (finish())
         with torch.no_grad():
             for p in self.params:
                 dist.broadcast(p.data, src=0, group=group)
@@ -148,11 +149,15 @@ class GradBucketReducer:
         them (a no-op after a ``no_sync`` micro-batch).
 
         A parameter the engine never reported during a synchronised backward
-        received no gradient (UNetResNet's z_initial when use_bottleneck is
-        False): its ``.grad`` is reset to None afterwards -- torch semantics,
-        so the optimizer skips it (no AdamW state, no weight decay) as it
-        would without the reducer.  Only when the engine reported at all (a
-        model without the grad_ready hook keeps every bound gradient)."""
+        AND whose reduced gradient slot is exactly zero on every rank received
+        no gradient (UNetResNet's z_initial when use_bottleneck is False): its
+        ``.grad`` is reset to None afterwards -- torch semantics, so the
+        optimizer skips it (no AdamW state, no weight decay) as it would
+        without the reducer.  A non-zero slot is kept: a backward path that
+        forgot to report a parameter only delays its bucket, it never drops a
+        real gradient.  The zero test is a host read, made once
+        per parameter on an eager step and cached; while a graph is being
+        captured an undecided parameter keeps its gradient."""
         if not self._sync:
             return
         unseen = []
@@ -169,8 +174,14 @@ class GradBucketReducer:
                 flat.div_(self.world)
         self._handles = []
         self._pending = None
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         for p in unseen:
-            p.grad = None
+            unused = self._unused.get(id(p))
+            if unused is None and not capturing and p.grad is not None:
+                unused = bool(torch.count_nonzero(p.grad).item() == 0)
+                self._unused[id(p)] = unused
+            if unused:
+                p.grad = None
 
 
 def attach(model, **kw):
