@@ -131,10 +131,46 @@ def _drift(a, ref):
     return d.max().item() / ref.abs().max().item(), (d.pow(2).mean().sqrt() / ref.pow(2).mean().sqrt()).item()
 
 
+def _ref_bf16_run(R, state, x, t, eps, names, probe=False):
+    """The reference's own CPU-bf16 autocast step: (per-parameter gradient
+    norms, logits, mu, logvar, loss, per-BatchNorm dz if probe)."""
+    ref16 = R.UNetResNetRef(state)
+    R.PROBE = {} if probe else None
+    try:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            l16, mu16, lv16 = ref16.forward(x, eps, True)
+            loss16 = R.combined_loss(l16.float(), t) + 1e-3 * R.kl_with_free_bits(mu16.float(), lv16.float(), 1e-3)
+        loss16.backward()
+        dz = {k: v[1].grad.detach().float() for k, v in R.PROBE.items() if not k.startswith("gate:")} \
+            if probe else None
+    finally:
+        R.PROBE = None
+    g16 = np.array([float(ref16.p[k].grad.double().norm()) if ref16.p[k].grad is not None else 0.0
+                    for k in names])
+    return g16, l16.detach().float().contiguous(), mu16.detach().float(), lv16.detach().float(), loss16, dz, ref16
+
+
+# The reference's own bf16 drift of ONE parameter's gradient norm is not a
+# stable yardstick: for the cancellation-dominated BatchNorm-affine sums
+# (dgamma = sum dz * xhat over up to 524k pixels) it swings by up to 17x
+# between inputs that are the same at bf16 resolution (encoder.bn1.weight:
+# 6.1 % / 13.8 % / 1.6 % for the bench input and two copies perturbed by a
+# relative 2^-12 / 2^-10 -- below the bf16 half-ulp, so only elements at a
+# rounding boundary change -- and layer1.2.bn1.weight 3.1 / 2.2 / 27.4 %),
+# because the bf16 backward is ~80 % away from the fp32 one elementwise at
+# the encoder (the dz of every BatchNorm, in the reference's path as in ours:
+# tools/bn_drift_probe.py, profiles/r5b_bn_drift_probe.log).  Round 5: the
+# yardstick per parameter is the max over that three-input ensemble of the
+# reference's runs, and the elementwise dz drift is compared at every
+# BatchNorm (HIP must not drift more than the reference's own bf16 path).
+REF_PERTURB = (2.0 ** -12, 2.0 ** -10)
+DZ_VS_REF = 1.05
+
+
 @pytest.mark.timeout(900)
 def test_unetresnet_config3_bf16_b8_vs_oracle():
     from oracle import cpu_ref as R
-    from vaeunet_amd import UNetResNet
+    from vaeunet_amd import UNetResNet, engine as E
     from vaeunet_amd.init import seeded_init_
     from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
     _threads()
@@ -144,29 +180,47 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     x, t = _batch(1)
     eps = _eps()
     ref = R.UNetResNetRef(state)
-    lref, muref, lvref = ref.forward(x, eps, True)
-    loss_ref = R.combined_loss(lref, t) + 1e-3 * R.kl_with_free_bits(muref, lvref, 1e-3)
-    loss_ref.backward()
+    R.PROBE = {}
+    try:
+        lref, muref, lvref = ref.forward(x, eps, True)
+        loss_ref = R.combined_loss(lref, t) + 1e-3 * R.kl_with_free_bits(muref, lvref, 1e-3)
+        loss_ref.backward()
+        dz32 = {k: v[1].grad.detach().float() for k, v in R.PROBE.items() if not k.startswith("gate:")}
+    finally:
+        R.PROBE = None
     gref = np.array([float(ref.p[k].grad.double().norm()) if ref.p[k].grad is not None else 0.0 for k in names])
     lref, muref, lvref = lref.detach().contiguous(), muref.detach(), lvref.detach()
-    ref16 = R.UNetResNetRef(state)
-    with torch.autocast("cpu", dtype=torch.bfloat16):
-        l16, mu16, lv16 = ref16.forward(x, eps, True)
-        loss16 = R.combined_loss(l16.float(), t) + 1e-3 * R.kl_with_free_bits(mu16.float(), lv16.float(), 1e-3)
-    loss16.backward()
-    g16 = np.array([float(ref16.p[k].grad.double().norm()) if ref16.p[k].grad is not None else 0.0
-                    for k in names])
-    l16, mu16, lv16 = l16.detach().float().contiguous(), mu16.detach().float(), lv16.detach().float()
+    g16, l16, mu16, lv16, loss16, dz16, ref16 = _ref_bf16_run(R, state, x, t, eps, names, probe=True)
     ref_max, ref_rms = _drift(l16, lref)
     ref_flips = int(((l16 > 0) != (lref > 0)).sum())
     ref_mu = max(_drift(mu16, muref)[0], _drift(lv16, lvref)[0])
+    r = torch.rand(x.shape, generator=torch.Generator().manual_seed(5)) * 2 - 1
+    g16_ens = [g16] + [_ref_bf16_run(R, state, (x * (1 + sc * r)).contiguous(memory_format=CL), t, eps, names)[0]
+                       for sc in REF_PERTURB]
 
     model = model.to(DEV).to(memory_format=CL).train()
     model.eps_override = eps
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        lg, mu, lv = model(x.to(DEV))
-        loss = CombinedLoss()(lg, t.to(DEV)) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
-    loss.backward()
+    bn_name = {id(mod): n + "." for n, mod in model.named_modules() if isinstance(mod, torch.nn.BatchNorm2d)}
+    dz_hip = {}
+    orig = E.bn_bwd
+
+    def bn_bwd(dy, xx, coef, bn, relu, M, *a, **kw):   # records dz = dL/d(BN output) per BatchNorm
+        pre = bn_name.get(id(bn))
+        if pre is not None and not isinstance(dy, E.PoolGrad):
+            d = dy.detach().float()
+            if relu:
+                C_ = xx.shape[1]
+                d = d * ((xx.float() * coef[0].view(1, C_, 1, 1) + coef[1].view(1, C_, 1, 1)) > 0).float()
+            dz_hip[pre] = d.cpu()
+        return orig(dy, xx, coef, bn, relu, M, *a, **kw)
+    E.bn_bwd = bn_bwd
+    try:
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            lg, mu, lv = model(x.to(DEV))
+            loss = CombinedLoss()(lg, t.to(DEV)) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+        loss.backward()
+    finally:
+        E.bn_bwd = orig
     lg = lg.detach().float().cpu().contiguous()
     max_rel, rms_rel = _drift(lg, lref)
     flips = int(((lg > 0) != (lref > 0)).sum())
@@ -175,45 +229,58 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     gn = np.array([float(params[k].grad.double().norm()) if params[k].grad is not None else 0.0 for k in names])
     big = gref > 1e-3 * gref.max()
     grel = np.abs(gn - gref) / np.maximum(gref, 1e-30)
+    grel_ens = np.max([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in g16_ens], axis=0)
     grel16 = np.abs(g16 - gref) / np.maximum(gref, 1e-30)   # the reference's own bf16 gradient drift
-    # per parameter: excess over the reference's own bf16 drift
-    excess = grel - BF16_VS_REF_DRIFT * grel16
-    worst = sorted(((excess[i], names[i], grel[i], grel16[i]) for i in np.where(big)[0]), reverse=True)[:5]
+    # per parameter: excess over the reference's own bf16 drift (ensemble max)
+    excess = grel - BF16_VS_REF_DRIFT * grel_ens
+    worst = sorted(((excess[i], names[i], grel[i], grel_ens[i]) for i in np.where(big)[0]), reverse=True)[:5]
     tot = abs(np.sqrt((gn ** 2).sum()) / np.sqrt((gref ** 2).sum()) - 1)
     npx = lg.numel()
+    # elementwise dz drift at every BatchNorm: HIP vs the reference's bf16
+    dzr = []
+    for k, d32 in dz32.items():
+        if k in dz_hip and k in dz16:
+            den = float(d32.double().norm())
+            if den > 0:
+                dzr.append((float((dz_hip[k].double() - d32.double()).norm()) / den,
+                            float((dz16[k].double() - d32.double()).norm()) / den, k))
+    dz_worst = max(dzr, key=lambda v: v[0] / (DZ_VS_REF * v[1] + 0.01))
     print(f"config3 bf16 B=8 vs fp32 oracle: HIP logits max_rel {max_rel:.3e} rms_rel {rms_rel:.3e} flips "
           f"{flips}/{npx}, mu/logvar max_rel {mu_rel:.3e}; reference CPU-bf16 max_rel {ref_max:.3e} rms_rel "
           f"{ref_rms:.3e} flips {ref_flips} mu/logvar {ref_mu:.3e}; loss {loss.item():.6f} vs "
-          f"{loss_ref.item():.6f}; grad-norm worst (excess, name, HIP, CPU-bf16) "
+          f"{loss_ref.item():.6f}; grad-norm worst (excess, name, HIP, CPU-bf16 ensemble max) "
           f"{[(round(float(a), 4), b, round(float(c), 4), round(float(d), 4)) for a, b, c, d in worst[:3]]}; "
-          f"total {tot:.2e}")
+          f"total {tot:.2e}; dz drift at {len(dzr)} BatchNorms, HIP / CPU-bf16 max "
+          f"{max(a / b for a, b, _ in dzr):.3f} (worst {dz_worst[2]}: {dz_worst[0]:.3f} vs {dz_worst[1]:.3f})")
     assert max_rel <= BF16_VS_REF_DRIFT * ref_max + 5e-3
     assert rms_rel <= BF16_VS_REF_DRIFT * ref_rms + 5e-3
     assert mu_rel <= BF16_VS_REF_DRIFT * ref_mu + 5e-3
     assert flips <= BF16_FLIPS * ref_flips + 1e-3 * npx
     assert abs(loss.item() - loss_ref.item()) < BF16_LOSS
-    # per-parameter gradient norms.  Weights (conv / linear, >= 2-D): within
-    # 1.5x the reference's own bf16 drift + 5 %.  BatchNorm affine gradients
-    # (1-D: dgamma = sum dz * xhat, dbeta = sum dz over up to 524k pixels) are
-    # cancellation-prone sums whose bf16 error scales with sum |dz * xhat| /
-    # |dgamma|: the CPU-bf16 path itself moves the ResNet34 stem's by 6 %, ours
-    # (bf16 gradient storage between every kernel) by up to 19 %; they are
-    # held as a group (relative L2 error of the concatenated BN-affine
-    # gradients within 1.5x the reference's + 5 %) and individually to 25 %.
+    assert len(dzr) >= 50   # every conv BatchNorm of the encoder and the decoder blocks (53)
+    for a, b, k in dzr:
+        assert a <= DZ_VS_REF * b + 0.01, (k, a, b)
+    # per-parameter gradient norms within 1.5x the reference's own bf16 drift
+    # (max over the ensemble) + 5 %: weights (>= 2-D) and, individually, the
+    # BatchNorm-affine gradients; the latter also as a group (relative L2
+    # error of the concatenated BN-affine gradients within 1.5x the
+    # reference's + 5 %).
     dims = {k: p.dim() for k, p in model.named_parameters()}
     wbig = [i for i in np.where(big)[0] if dims[names[i]] >= 2]
     bbig = [i for i in np.where(big)[0] if dims[names[i]] == 1]
     worst_w = max(excess[i] for i in wbig)
     assert worst_w < BF16_GNORM, [w for w in worst if dims[w[1]] >= 2]
+    worst_b = max(excess[i] for i in bbig)
+    assert worst_b < BF16_GNORM, [w for w in worst if dims[w[1]] == 1]
     vecs = {k: (params[k].grad.double().cpu().reshape(-1), ref.p[k].grad.double().reshape(-1),
                 ref16.p[k].grad.double().reshape(-1)) for k in (names[i] for i in bbig)}
-    num = sum(float((a - r).pow(2).sum()) for a, r, _ in vecs.values()) ** 0.5
-    num16 = sum(float((c - r).pow(2).sum()) for _, r, c in vecs.values()) ** 0.5
-    den = sum(float(r.pow(2).sum()) for _, r, _ in vecs.values()) ** 0.5
+    num = sum(float((a - r_).pow(2).sum()) for a, r_, _ in vecs.values()) ** 0.5
+    num16 = sum(float((c - r_).pow(2).sum()) for _, r_, c in vecs.values()) ** 0.5
+    den = sum(float(r_.pow(2).sum()) for _, r_, _ in vecs.values()) ** 0.5
     print(f"config3 bf16: BN-affine gradients, relative L2 error HIP {num / den:.3e} vs CPU-bf16 "
-          f"{num16 / den:.3e}; worst weight excess {worst_w:.3e}")
+          f"{num16 / den:.3e}; worst weight excess {worst_w:.3e}, worst BN-affine excess {worst_b:.3e}; "
+          f"bench-input-only CPU-bf16 drift of the worst: {grel16[names.index(worst[0][1])]:.3f}")
     assert num / den <= BF16_VS_REF_DRIFT * num16 / den + BF16_GNORM
-    assert max(grel[i] for i in bbig) < 0.25
     assert tot < BF16_TOTAL
 
 
