@@ -96,6 +96,19 @@ typedef struct VuGemmFwd {
    * vaeunet_amd.engine.fold_bn_eval; with accumulate it applies to the new
    * term; not with bnb_part).  0 = none. */
   int32_t relu;
+  /* Optional per-sample, per-border-class bias (round 5): the latent-broadcast
+   * shortcut of a DecoderBlock's conv1 (unet/unet_resnet.py:37-41, 92-99).
+   * The z_proj source of that conv is a per-sample constant map c_n, so its
+   * share of the 3x3 conv is sum over the taps INSIDE the image of W_z c_n:
+   * one of 9 vectors per sample by the pixel's border class.  Before the
+   * storage rounding, the ReLU and the statistics:
+   *   out[m][j] += zbias[(n * 9 + cls) * ncol + j],   m = (n, h, w),
+   *   cls = 3 * rc(h, H) + rc(w, W),  rc(v, L) = v == 0 ? 0 : v == L - 1 ? 2 : 1
+   * (vu_zbias_fwd builds the table).  out_mode 0, H >= 2, W >= 2, no
+   * bnb_part; served by the ping-pong kernel (incl. its split-K finish) and
+   * the generic kernel -- the dispatcher keeps such problems on those.
+   * NULL: none. */
+  const float* zbias;
 } VuGemmFwd;
 
 /* Weight-gradient GEMM: out[s][i][j] = sum_{m in split s} P[m][i] * Q[m][j]
@@ -667,6 +680,11 @@ typedef struct VuLatentJob {
   float* dbias;
   float* dgamma;
   float* dbeta;
+  /* round 5: the consumer's activated vectors [N][co] (rounded to the
+   * storage dtype, i.e. the values its map would hold) are written here when
+   * non-NULL; out = NULL (the latent shortcut of a DecoderBlock: no map) then
+   * skips the map stores (cpad = co, out_stride 0). */
+  float* act;
 } VuLatentJob;
 
 /* the heads' backward inputs / outputs for vu_latent_bwd */
@@ -705,6 +723,45 @@ int vu_latent_bwd_supported(int N, int L, int64_t sum_co, int C);
  * encoder channels) */
 int vu_latent_bwd(const VuLatentJob* jobs, int njobs, const VuLatentHeads* heads, int N, int L,
                   float* workspace, void* stream);
+
+/* ---- latent-broadcast shortcut of a DecoderBlock's conv1 (round 5) ------
+ * unet/unet_resnet.py:37-41, 92-99: conv1 contracts over the concat
+ * [x, skip, z_proj(z) broadcast]; the last source is a per-sample constant
+ * map c_n (L channels at input channels [cz0, cz0 + L) of conv1.weight).  Its
+ * contribution becomes VuGemmFwd.zbias (forward) and its backward reduces to
+ * per-sample region sums of conv1's pre-BatchNorm output gradient dy:
+ *   R[n][c][tap] = sum over the output pixels whose tap reads inside the image
+ *                = T - [ky=0] Row0 - [ky=2] RowL - [kx=0] Col0 - [kx=2] ColL + corners
+ *   dW[c][cz0 + l][tap] (+)= sum_n c_n[l] R[n][c][tap]
+ *   dc[n][l]             = sum_c sum_tap W[c][cz0 + l][tap] R[n][c][tap]
+ * dc (the pixel sum of d(map), what vu_latent_bwd_sums produced from the map
+ * gradient) goes to the consumer's VuLatentJob.part split by 32-channel
+ * chunk of c (vu_latent_bwd sums the splits).  Jobs travel by value
+ * (at most 8); block0 is filled by the library. */
+typedef struct VuZbJob {
+  const float* w;              /* conv1.weight (fp32), element strides below */
+  int64_t ws_co, ws_ci, ws_ky, ws_kx;
+  int32_t cz0, L, co, H, W;    /* z channels [cz0, cz0 + L); co = conv1 outputs; output image H x W */
+  const float* act;            /* [N][L] the z_proj vectors (VuLatentJob.act) */
+  const float* row_scale;      /* [co] or NULL: eval-mode BN folded into conv1 (table rows scaled) */
+  float* table;                /* forward: [N][9][co] */
+  const void* dy;              /* backward: conv1's pre-BN output gradient, NHWC, co channels */
+  int64_t dy_stride;
+  float* rs;                   /* region-sum partials, vu_zbias_rs_floats(N, co) */
+  float* part;                 /* the consumer's VuLatentJob.part ([N][32][L]) */
+  float* dw;                   /* conv1.weight.grad (strides of w): z columns written, or added when grad_acc */
+  int32_t grad_acc;
+  int32_t pad_;
+  int64_t block0;
+} VuZbJob;
+/* 1 when the shortcut serves N samples, L latent channels and co conv1 outputs */
+int vu_zbias_supported(int N, int L, int co);
+int64_t vu_zbias_rs_floats(int N, int co);
+/* the [N][9][co] tables of every job (one launch) */
+int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream);
+/* region sums of every job's dy, then dW's z columns and the dc partials
+ * (two launches); dtype: dy's storage (VU_BF16 / VU_F32) */
+int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, void* stream);
 /* 0 when a consumer of this geometry is served (co = 8 * 2^k <= 2048, cpad % 8,
  * stride % 8), else hipErrorInvalidValue */
 int vu_latent_check_job(int co, int cpad, int64_t out_stride, int dtype);

@@ -9,7 +9,7 @@ stem, ...), and then evaluates the contraction the descriptor DEFINES
 (include/vaeunet.h: ``VuGather`` / ``VuGemmFwd`` / ``VuGemmWgrad``) in fp64 on
 the device from the very same operands:
 
-  fwd    out[m][j] = relu?(sum_k A[m][k] B[j][k] + bias)  (+ old out)
+  fwd    out[m][j] = relu?(sum_k A[m][k] B[j][k] + zbias[n][cls(h, w)][j] + bias)  (+ old out)
          A = im2col of the (1-3) NHWC channel sources, zero padding;
          B = the derived weight image the kernel read;
   wgrad  grad[i, tap, c] = sum_m P[m][i] Q[m][tap*C + c]  (+ old grad).
@@ -103,7 +103,7 @@ class GemmAudit:
         self.chunk_pixels = chunk_pixels
 
     # ---------------------------------------------------------------- forward
-    def gemm_fwd(self, a, dtype, g, wmat, out, bias, st, launch):
+    def gemm_fwd(self, a, dtype, g, wmat, out, bias, st, launch, zbias=None):
         kern = self.kernel_of(a, dtype)
         pre = out.clone()
         launch()
@@ -121,6 +121,13 @@ class GemmAudit:
         written = torch.zeros(out.shape, dtype=torch.bool, device=out.device)
         col = _Im2col(g)
         HW = g.H * g.W
+        zcls = None
+        if zbias is not None:   # VuGemmFwd.zbias: row m = (n, h, w) adds zbias[n][cls(h, w)]
+            rc = lambda v, L: torch.where(v == 0, 0, torch.where(v == L - 1, 2, 1))  # noqa: E731
+            hh = torch.arange(g.H, device=out.device)[:, None].expand(g.H, g.W)
+            ww = torch.arange(g.W, device=out.device)[None, :].expand(g.H, g.W)
+            zcls = (3 * rc(hh, g.H) + rc(ww, g.W)).reshape(-1)
+            zb64 = zbias.double()
         step = max(1, self.chunk_pixels // HW)
         emax = 0.0
         pieces = []
@@ -132,6 +139,10 @@ class GemmAudit:
                 Bt = B[:, tap * g.C:(tap + 1) * g.C]
                 res.addmm_(A, Bt.t())
                 sab.addmm_(A.abs(), Babs[:, tap * g.C:(tap + 1) * g.C].t())
+            if zcls is not None:
+                zt = zb64[n0:n1][:, zcls, :].reshape(-1, ncol)
+                res += zt
+                sab += zt.abs()
             if bvec is not None:
                 res += bvec
                 sab += bvec.abs()

@@ -1,0 +1,150 @@
+"""The latent-broadcast shortcut of a DecoderBlock's conv1 (round 5,
+csrc/zbias.hip + the VuGemmFwd.zbias epilogue; unet/unet_resnet.py:37-41,
+92-99): against the convolution of the concat with the per-sample constant
+z map it replaces -- the forward GEMM on every kernel that serves it (the
+ping-pong kernel, its split-K finish, the generic kernel, bf16 and fp32), and
+the backward's weight-gradient z columns and pixel-summed map gradient."""
+import ctypes as C
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last
+TUNE_V4_MIN_BLOCKS, TUNE_V4_SPLITK, TUNE_GEN = 0, 6, 12
+TUNE_DEFAULTS = ((TUNE_V4_MIN_BLOCKS, 256), (TUNE_V4_SPLITK, 1), (TUNE_GEN, 4))
+
+
+def _tune(*kv):
+    from vaeunet_amd import _lib
+    for k, v in kv:
+        _lib.call("vu_gemm_set_tuning", k, v)
+
+
+def _job(w, cz0, L, H, W, act, table=None):
+    from vaeunet_amd import _lib
+    j = _lib.VuZbJob()
+    j.w = w.data_ptr()
+    j.ws_co, j.ws_ci, j.ws_ky, j.ws_kx = w.stride()
+    j.cz0, j.L, j.co, j.H, j.W = cz0, L, w.shape[0], H, W
+    j.act = act.data_ptr()
+    j.table = table.data_ptr() if table is not None else None
+    return j
+
+
+def _table(w, cz0, L, H, W, act):
+    from vaeunet_amd import kernels as K
+    N, co = act.shape[0], w.shape[0]
+    table = torch.empty((N, 9, co), dtype=torch.float32, device=DEV)
+    arr = (type(_job(w, cz0, L, H, W, act)) * 1)()
+    arr[0] = _job(w, cz0, L, H, W, act, table)
+    K.call("vu_zbias_fwd", arr, 1, N, K.stream())
+    return table
+
+
+# (N, [cin per non-z source], L, H, W, cout, mode, tuning, kernel id)
+FWD_CASES = [
+    (2, [64, 64], 32, 32, 32, 64, "bf16", ((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 0)), 4),    # pp<64>
+    (2, [64, 64], 32, 16, 64, 128, "bf16", ((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 0)), 4),   # pp<128>
+    (1, [128, 64], 32, 8, 32, 256, "bf16", ((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 0)), 4),   # pp<256>
+    (2, [128, 64], 32, 16, 32, 256, "bf16", ((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 2)), 4),  # split-K finish
+    (2, [64, 64], 32, 12, 20, 64, "bf16", ((TUNE_GEN, 1),), 1),                                  # generic bf16
+    (2, [32, 24], 32, 9, 13, 48, "f32", (), 1),                                                  # generic fp32
+]
+
+
+@pytest.mark.parametrize("case", FWD_CASES)
+def test_zbias_forward_matches_concat_conv(case):
+    """conv over [sources] + zbias == conv over [sources, broadcast z map]
+    (the map holds the storage-rounded vectors), per element within the
+    GEMM bound, with the BatchNorm statistics of the stored output."""
+    from vaeunet_amd import kernels as K, engine as E
+    N, cins, L, H, W, co, mode, tune, kern = case
+    dt = torch.bfloat16 if mode == "bf16" else torch.float32
+    d = 1 if mode == "bf16" else 0
+    g = torch.Generator().manual_seed(21)
+    xs = [torch.randn(N, c, H, W, generator=g).to(dt).float() for c in cins]
+    lead = sum(cins)
+    w = (torch.randn(co, lead + L, 3, 3, generator=g) / (3 * (lead + L) ** 0.5)).to(DEV)
+    act = torch.rand(N, L, generator=g).to(dt).float().to(DEV)   # ReLU'd vectors, storage-rounded
+    table = _table(w, lead, L, H, W, act)
+    srcs = [x.to(DEV, dt).contiguous(memory_format=CL) for x in xs]
+    out = K.empty_act(N, co, H, W, dt, DEV)
+    _tune(*tune)
+    try:
+        wm = E.w3x3_fwd(w, d, cin_use=lead)
+        from vaeunet_amd import _lib
+        a = _lib.VuGemmFwd()
+        a.a = K.gather3x3(srcs)
+        a.b, a.ldb, a.ncol = wm.data_ptr(), wm.shape[-1], co
+        a.out, a.out_stride, a.out_mode = out.data_ptr(), K.pstride(out), 0
+        a.zbias = table.data_ptr()
+        assert K.query("vu_gemm_fwd_kernel", C.byref(a), d) == kern
+        st = K.gemm_fwd(K.gather3x3(srcs), wm, co, out, d, stats=True, zbias=table)
+    finally:
+        _tune(*TUNE_DEFAULTS)
+    zmap = act.cpu()[:, :, None, None].expand(N, L, H, W)
+    wq = w.cpu().to(dt).float() if mode == "bf16" else w.cpu()
+    xcat = torch.cat(xs + [zmap], 1)
+    # the shortcut keeps the fp32 weights for the z part (the map path rounds them to bf16)
+    wz = torch.cat([wq[:, :lead], w.cpu()[:, lead:]], 1)
+    ref = F.conv2d(xcat.double(), wz.double(), padding=1)
+    sab = F.conv2d(xcat.abs().double(), wz.abs().double(), padding=1)
+    got = out.double().cpu()
+    u = 2.0 ** -8 if mode == "bf16" else 2.0 ** -24
+    bound = u * torch.maximum(ref.abs(), got.abs()) + 1e-5 * sab + 1e-7 * float(ref.abs().max())
+    err = (got - ref).abs()
+    assert bool((err <= bound).all()), float((err / bound).max())
+    stored = out.double().cpu()
+    n = torch.tensor([min(st.tile_rows, st.rows - t * st.tile_rows) for t in range(st.tiles)], dtype=torch.float64)
+    s = st.psum.double().cpu()
+    mean = s.sum(0) / n.sum()
+    m2 = st.pm2.double().cpu() + n[:, None] * (s / n[:, None] - mean) ** 2
+    torch.testing.assert_close(mean, stored.mean((0, 2, 3)), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m2.sum(0) / n.sum(), stored.var((0, 2, 3), unbiased=False), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode", ["bf16", "f32"])
+@pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_zbias_backward_matches_map_gradient(mode, shape, acc):
+    """From conv1's pre-BN gradient dy: the weight gradient's z columns
+    (written / accumulated; the other columns untouched) and the pixel sums
+    of the z map's gradient (the split partials the latent backward sums)
+    equal conv2d_weight / conv2d_input of the broadcast map, in fp64."""
+    from vaeunet_amd import kernels as K
+    N, L, H, W, co = shape
+    lead = 64
+    dt = torch.bfloat16 if mode == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(23)
+    w = (torch.randn(co, lead + L, 3, 3, generator=g) / 10).to(DEV)
+    act = torch.rand(N, L, generator=g).to(DEV)
+    dy = torch.randn(N, co, H, W, generator=g).to(dt)
+    dyd = dy.to(DEV).contiguous(memory_format=CL)
+    dw = torch.randn(co, lead + L, 3, 3, generator=g).to(DEV)
+    dw0 = dw.clone()
+    part = torch.full((N * 32 * L,), float("nan"), dtype=torch.float32, device=DEV)
+    rs = torch.empty(K.query("vu_zbias_rs_floats", N, co), dtype=torch.float32, device=DEV)
+    arr = (type(_job(w, lead, L, H, W, act)) * 1)()
+    j = _job(w, lead, L, H, W, act)
+    j.dy, j.dy_stride = dyd.data_ptr(), K.pstride(dyd)
+    j.rs, j.part, j.dw, j.grad_acc = rs.data_ptr(), part.data_ptr(), dw.data_ptr(), 1 if acc else 0
+    arr[0] = j
+    K.call("vu_zbias_bwd", arr, 1, N, 1 if mode == "bf16" else 0, K.stream())
+    torch.cuda.synchronize()
+    zmap = act.cpu().double()[:, :, None, None].expand(N, L, H, W)
+    dy64 = dy.double()
+    gw = torch.nn.grad.conv2d_weight(zmap, (co, L, 3, 3), dy64, padding=1)
+    gwa = torch.nn.grad.conv2d_weight(zmap.abs(), (co, L, 3, 3), dy64.abs(), padding=1)
+    exp_w = gw + (dw0.cpu().double()[:, lead:] if acc else 0)
+    got_w = dw.cpu().double()[:, lead:]
+    assert bool(((got_w - exp_w).abs() <= 1e-5 * gwa + 2.0 ** -24 * exp_w.abs() + 1e-12).all())
+    assert torch.equal(dw[:, :lead], dw0[:, :lead])
+    dmap = torch.nn.grad.conv2d_input((N, L, H, W), w.cpu().double()[:, lead:], dy64, padding=1)
+    dmapa = torch.nn.grad.conv2d_input((N, L, H, W), w.cpu().double()[:, lead:].abs(), dy64.abs(), padding=1)
+    dc = dmap.sum((2, 3))
+    got_dc = part.view(N, 32, L).double().cpu().sum(1)
+    assert bool(((got_dc - dc).abs() <= 1e-5 * dmapa.sum((2, 3)) + 1e-12).all())
+    assert not bool(torch.isnan(part).any())   # every split written (unused ones zero)

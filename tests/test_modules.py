@@ -95,10 +95,11 @@ def test_abi_struct_sizes_match_the_binding():
     field added on one side only would shift every later field)."""
     from vaeunet_amd import _lib
     lib = ctypes.CDLL(_lib.LIB_PATH)
-    out = (ctypes.c_int64 * 8)()
+    out = (ctypes.c_int64 * 9)()
     lib.vu_abi_struct_sizes(out)
     mine = [ctypes.sizeof(c) for c in (_lib.VuGather, _lib.VuGemmFwd, _lib.VuGemmWgrad, _lib.VuConvFp8,
-                                       _lib.VuPermJob, _lib.VuMtEntry, _lib.VuLatentJob, _lib.VuLatentHeads)]
+                                       _lib.VuPermJob, _lib.VuMtEntry, _lib.VuLatentJob, _lib.VuLatentHeads,
+                                       _lib.VuZbJob)]
     assert list(out) == mine, (list(out), mine)
 
 

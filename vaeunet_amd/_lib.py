@@ -42,7 +42,7 @@ class VuGemmFwd(C.Structure):
                 ("ksplit", C.c_int32), ("workspace", _p),
                 ("bnb_x", _p), ("bnb_xstride", _l), ("bnb_scale", _p), ("bnb_shift", _p),
                 ("bnb_mean", _p), ("bnb_invstd", _p), ("bnb_part", _p), ("bnb_relu", C.c_int32),
-                ("relu", C.c_int32)]
+                ("relu", C.c_int32), ("zbias", _p)]
 
 
 class VuGemmWgrad(C.Structure):
@@ -74,7 +74,15 @@ class VuLatentJob(C.Structure):
                 ("train", C.c_int32), ("co", C.c_int32), ("cpad", C.c_int32), ("HW", C.c_int32),
                 ("out", _p), ("out_stride", _l), ("y", _p), ("coef", _p), ("block0", _l),
                 ("cgroups", C.c_int32), ("grad_acc", C.c_int32), ("dmap", _p), ("dmap_stride", _l),
-                ("part", _p), ("sblock0", _l), ("dw", _p), ("dbias", _p), ("dgamma", _p), ("dbeta", _p)]
+                ("part", _p), ("sblock0", _l), ("dw", _p), ("dbias", _p), ("dgamma", _p), ("dbeta", _p),
+                ("act", _p)]
+
+
+class VuZbJob(C.Structure):
+    _fields_ = [("w", _p), ("ws_co", _l), ("ws_ci", _l), ("ws_ky", _l), ("ws_kx", _l), ("cz0", C.c_int32),
+                ("L", C.c_int32), ("co", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("act", _p),
+                ("row_scale", _p), ("table", _p), ("dy", _p), ("dy_stride", _l), ("rs", _p), ("part", _p),
+                ("dw", _p), ("grad_acc", C.c_int32), ("pad_", C.c_int32), ("block0", _l)]
 
 
 class VuLatentHeads(C.Structure):
@@ -180,6 +188,10 @@ _SIGS = {
     "vu_latent_bwd_workspace_bytes": (_l, [_i, _i, _l]),
     "vu_latent_bwd": (_i, [_p, _i, C.POINTER(VuLatentHeads), _i, _i, _p, _p]),
     "vu_latent_check_job": (_i, [_i, _i, _l, _i]),
+    "vu_zbias_supported": (_i, [_i, _i, _i]),
+    "vu_zbias_rs_floats": (_l, [_i, _i]),
+    "vu_zbias_fwd": (_i, [_p, _i, _i, _p]),
+    "vu_zbias_bwd": (_i, [_p, _i, _i, _i, _p]),
     "vu_mean_groups": (_i, [_p, _i, _l, _p, _p]),
     "vu_sigmoid": (_i, [_p, _l, _p, _p]),
     "vu_patch_blend": (_i, [_p, _l, _i, _i, _i, _p, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p]),

@@ -62,6 +62,9 @@ struct FastDiv {
   VU_DEV uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
 };
 
+// border class of a row / column index (VuGemmFwd.zbias): 0 first, 2 last, 1 inside
+VU_DEV int zb_class(int v, int L) { return v == 0 ? 0 : (v == L - 1 ? 2 : 1); }
+
 // Round a float to the storage precision (identity for fp32).
 template <typename T> VU_DEV float rnd(float v);
 template <> VU_DEV float rnd<float>(float v) { return v; }

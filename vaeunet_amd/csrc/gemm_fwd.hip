@@ -50,6 +50,15 @@ template <> struct Mma<float> {
 
 struct RowPix { int n, h, w; bool ok; };
 
+// VuGemmFwd.zbias of output row m (pixel (n, h, w)), column j
+VU_DEV float zbias_at(const VuGemmFwd& p, int64_t m, int j) {
+  const int hw = p.a.H * p.a.W;
+  const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
+  const int h = rem / p.a.W, w = rem - (rem / p.a.W) * p.a.W;
+  const int cls = 3 * zb_class(h, p.a.H) + zb_class(w, p.a.W);
+  return p.zbias[((int64_t)n * 9 + cls) * p.ncol + j];
+}
+
 template <typename T>
 VU_DEV u32x4 gather_chunk(const VuGather& g, const RowPix& rp, int tap, int ch) {
   // ch: channel of the first element of this 16-byte chunk (all in one source)
@@ -192,7 +201,9 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int row = wm * (BM / 2) + i * 16 + 4 * (lane >> 4) + r;
-        E[row * ES + col] = rnd<T>(epi_act(acc[i][j][r] + bv, p.relu));
+        float a = acc[i][j][r];
+        if (p.zbias && gj < p.ncol && m0 + row < M) a += zbias_at(p, m0 + row, gj);
+        E[row * ES + col] = rnd<T>(epi_act(a + bv, p.relu));
       }
     }
   __syncthreads();
@@ -359,7 +370,16 @@ static bool use_v2(int dtype) { return g_tune_gen >= 2 && dtype == VU_BF16; }
 static bool use_v3(int dtype) { return g_tune_gen >= 3 && use_v2(dtype); }
 static bool use_v4(int dtype) { return g_tune_gen >= 4 && use_v3(dtype); }
 
+// VuGemmFwd.zbias problems run on the ping-pong kernel (incl. its split-K
+// finish) when it serves them, else on the generic kernel: the only two
+// epilogues that add the per-sample border-class bias
+static bool zb_v4(const VuGemmFwd* a, int dtype) { return use_v4(dtype) && gemm_fwd_v4_bm(*a, dtype); }
+static bool zb_ok(const VuGemmFwd* a) {
+  return a->out_mode == 0 && a->a.H >= 2 && a->a.W >= 2 && !a->bnb_part;
+}
+
 extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
+  if (args->zbias) return zb_v4(args, dtype) ? 128 : pick_bm(*args);
   if (use_v2(dtype)) {
     int bm = conv_image_bm(*args, dtype);
     if (bm) return bm;
@@ -390,6 +410,7 @@ extern "C" int64_t vu_gemm_fwd_row_tile(const VuGemmFwd* args, int dtype) {
 }
 
 extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype) {
+  if (args->zbias) return zb_v4(args, dtype) ? gemm_fwd_v4_workspace(*args, dtype) : 0;
   if (use_v2(dtype) && (conv_image_bm(*args, dtype) || conv_stem_bm(*args, dtype) || gemm_stream_bm(*args, dtype)))
     return 0;
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return 0;
@@ -402,6 +423,7 @@ extern "C" int64_t vu_gemm_fwd_workspace_bytes(const VuGemmFwd* args, int dtype)
 // The BatchNorm-backward partial tile of the kernel the dispatcher below picks
 // (it must mirror the dispatch order), 0 when that kernel cannot emit them.
 extern "C" int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype) {
+  if (args->zbias) return 0;
   if (use_v2(dtype) && (conv_image_bm(*args, dtype) || conv_stem_bm(*args, dtype) || gemm_stream_bm(*args, dtype)))
     return 0;
   if (use_v4(dtype) && gemm_fwd_v6_bm(*args, dtype)) return gemm_fwd_v6_bnb_tile(*args, dtype);
@@ -415,6 +437,7 @@ extern "C" int64_t vu_gemm_fwd_bnb_tile(const VuGemmFwd* args, int dtype) {
 // 8 1x1 stream, 9 image conv, 10 7x7 stem, 12 v2 small-grid mode, 13 v2
 // tail (small grids nothing else admits).
 extern "C" int vu_gemm_fwd_kernel(const VuGemmFwd* args, int dtype) {
+  if (args->zbias) return zb_v4(args, dtype) ? 4 : 1;
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return 9;
   if (use_v2(dtype) && conv_stem_bm(*args, dtype)) return 10;
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return 8;
@@ -439,6 +462,11 @@ extern "C" int vu_gemm_fwd(const VuGemmFwd* args, int dtype, void* stream) {
     if (g.cend[t] % epc != 0 || g.stride[t] % epc != 0) return (int)hipErrorInvalidValue;
   if ((args->ldb % epc) != 0) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (args->zbias) {
+    if (!zb_ok(args)) return (int)hipErrorInvalidValue;
+    if (zb_v4(args, dtype)) return gemm_fwd_v4_launch(*args, st);
+    return dtype == VU_BF16 ? dispatch_fwd<bf16_t>(*args, st) : dispatch_fwd<float>(*args, st);
+  }
   if (use_v2(dtype) && conv_image_bm(*args, dtype)) return conv_image_launch(*args, st);
   if (use_v2(dtype) && conv_stem_bm(*args, dtype)) return conv_stem_launch(*args, st);
   if (use_v2(dtype) && gemm_stream_bm(*args, dtype)) return gemm_stream_launch(*args, st);
@@ -462,4 +490,5 @@ extern "C" void vu_abi_struct_sizes(int64_t* out) {
   out[5] = sizeof(VuMtEntry);
   out[6] = sizeof(VuLatentJob);
   out[7] = sizeof(VuLatentHeads);
+  out[8] = sizeof(VuZbJob);
 }

@@ -84,7 +84,9 @@ VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_ad
 // 32-MFMA segment per step (2 barriers) instead of two 16-MFMA halves (4
 // barriers): twice the matrix work per barrier interval, 16 more fragment
 // registers (VU_TUNE_PP_FULL, A/B).
-template <int BN, bool SPLIT, bool BNB, bool RELU = false, bool FULL = false>
+// ZB: the latent-shortcut epilogue (VuGemmFwd.zbias) as its own
+// instantiation -- a runtime branch pushed the others to 256 VGPRs + scratch.
+template <int BN, bool SPLIT, bool BNB, bool RELU = false, bool FULL = false, bool ZB = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -347,6 +349,28 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     }
     return;
   }
+  if constexpr (ZB) {
+    // the latent-broadcast shortcut (VuGemmFwd.zbias): fragment i's pixel is
+    // tile row wm*4 + i/2, column (i&1)*16 + (lane&15); its border class picks
+    // one of the sample's 9 bias rows (4 channels per 16-byte load).  One
+    // fragment at a time, its loads fenced: batched, they spilled.
+    // (lane-derived values made opaque here, so that nothing of this address
+    // math is hoisted above the MFMA loop and held live through it)
+    int lz = lane;
+    asm volatile("" : "+v"(lz));
+    const float* const zb0 = ep->zbias + (int64_t)img * 9 * ep->ncol + n0 + wn * 64 + 4 * (lz >> 4);
+    const int cx0 = zb_class(x0 + (lz & 15), W), cx1 = zb_class(x0 + 16 + (lz & 15), W);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int zo = (3 * zb_class(y0 + wm * 4 + (i >> 1), H) + ((i & 1) ? cx1 : cx0)) * ep->ncol;
+      f32x4 zv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zv[j] = *reinterpret_cast<const f32x4*>(zb0 + zo + j * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += zv[j];
+      asm volatile("" ::: "memory");
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -598,6 +622,21 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
   }
   Vec8<bf16_t> old[4], xq[4];
   float bsc[8], bsf[8], bmu[8], bis[8];
+  f32x4 za[4], zb[4];  // VuGemmFwd.zbias of the 4 rows (latent shortcut)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) za[q] = zb[q] = f32x4{0, 0, 0, 0};
+  if (p.zbias) {
+    const int hw = p.a.H * p.a.W;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t m = (int64_t)rb * 128 + rs + 32 * q;
+      const int n = (int)(m / hw), rem = (int)(m - (int64_t)n * hw);
+      const int h = rem / p.a.W, w = rem - (rem / p.a.W) * p.a.W;
+      const float* z = p.zbias + ((int64_t)n * 9 + 3 * zb_class(h, p.a.H) + zb_class(w, p.a.W)) * p.ncol + c0;
+      za[q] = *reinterpret_cast<const f32x4*>(z);
+      zb[q] = *reinterpret_cast<const f32x4*>(z + 4);
+    }
+  }
   if (p.accumulate) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) old[q].load(dstq[q]);
@@ -616,7 +655,7 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(VuGemmFwd p) {
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const f32x4 a = sa[q], b = sb[q];
+    const f32x4 a = p.zbias ? sa[q] + za[q] : sa[q], b = p.zbias ? sb[q] + zb[q] : sb[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       v[q][e] = rnd<bf16_t>(a[e] + bv[e]);
@@ -801,7 +840,10 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
   if (ks <= 1) {
     VuGemmFwd q = p;
     q.ksplit = 1;
-    if (p.bnb_part)
+    if (p.zbias)
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64, true>), dim3((unsigned)tiles),
+                         dim3(512), 0, st, q);
+    else if (p.bnb_part)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     else if (p.relu)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);

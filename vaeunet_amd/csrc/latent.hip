@@ -208,12 +208,15 @@ __global__ __launch_bounds__(256) void latent_fwd_kernel(const LatentJobs jobs, 
       for (int n = 0; n < N; ++n) {
         const float a = fmaxf(act[n * LAT_CG + tid] * scale + shift, 0.f);
         act[n * LAT_CG + tid] = rnd<T>(a);
+        // the activated vectors (the latent shortcut's c_n: zbias.hip)
+        if (pc == 0 && J.act) J.act[(int64_t)n * J.co + c] = rnd<T>(a);
       }
     } else {
       for (int n = 0; n < N; ++n) act[n * LAT_CG + tid] = 0.f;  // channel padding of the concat source
     }
   }
   if (J.train && pc == 0 && cg == 0 && tid == 0 && J.num_batches_tracked) *J.num_batches_tracked += 1;
+  if (!J.out) return;  // the latent shortcut: vectors only, no map (block-uniform, before the barrier)
   __syncthreads();
   // map stores: pixels [pc*PCH, (pc+1)*PCH) of the flattened (n, p) range,
   // this block's channels [c0, min(c0 + 64, cpad)) as 8-channel vectors
@@ -588,10 +591,11 @@ static int pack(const VuLatentJob* jobs, int njobs, int N, LatentJobs& J, int64_
     VuLatentJob& q = J.j[j];
     if (vu_latent_check_job(q.co, q.cpad, q.out_stride, 0) != 0 || q.HW < 1) return (int)hipErrorInvalidValue;
     if ((int64_t)N * q.HW * 8 >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;  // 32-bit decodes
+    if (!q.out && (!q.act || q.cpad != q.co)) return (int)hipErrorInvalidValue;  // shortcut: vectors only
     q.cgroups = (q.cpad + LAT_CG - 1) / LAT_CG;
     q.block0 = fblocks;
     q.sblock0 = sblocks;
-    fblocks += vu_latent_fwd_blocks(N, q.HW, q.cpad);
+    fblocks += q.out ? vu_latent_fwd_blocks(N, q.HW, q.cpad) : q.cgroups;
     sblocks += (int64_t)N * LAT_SPLITS;
   }
   return 0;

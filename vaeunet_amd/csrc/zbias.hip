@@ -1,0 +1,300 @@
+// The latent-broadcast shortcut of a DecoderBlock's conv1 (round 5;
+// unet/unet_resnet.py:37-41, 92-99).
+//
+// conv1 contracts over the channel concat [x, skip, z_proj(z)]; the z_proj
+// source is interpolate(z[..., None, None]) through a 1x1 conv + BatchNorm +
+// ReLU -- a per-sample CONSTANT map c_n (latent.hip computes c_n on the
+// sample vectors).  A 3x3 convolution of a constant map is, at output pixel
+// (h, w), W_z c_n summed over the taps that read inside the image: one of 9
+// vectors per sample, by the pixel's border class (corner, edge, interior).
+// So the z channels leave conv1's K loop (and the 64-channel-padded map is
+// never written nor read):
+//
+//   vu_zbias_fwd  table[n][cls][c] = sum over the taps valid for cls of
+//                 S[n][c][tap],  S = sum_l W[c][cz0 + l][tap] c_n[l]
+//                 -> VuGemmFwd.zbias of conv1's GEMM (added in its epilogue);
+//   vu_zbias_bwd  the backward: with dy = conv1's pre-BN output gradient and
+//                 R[n][c][tap] = the sum of dy over the output pixels whose tap
+//                 reads inside the image (the total minus the excluded border
+//                 row / column sums plus the corner they both excluded),
+//                   dW[c][cz0 + l][tap] (+)= sum_n c_n[l] R[n][c][tap]
+//                   dc[n][l]              = sum_c sum_tap W[c][cz0+l][tap] R[n][c][tap]
+//                 -- dc is the pixel sum of d(map) the latent backward needs
+//                 (vu_latent_bwd_sums produced it from the map gradient).
+//                 Two launches: region partials per (sample, row band), then
+//                 one block per 32 output channels finishing R, writing its
+//                 dW rows and its dc partial into split `chunk` of the
+//                 consumer's part array (vu_latent_bwd sums the splits).
+// Every sum runs in a fixed order (reproducible run to run).
+#include "common.h"
+#include "../../include/vaeunet.h"
+
+namespace {
+
+constexpr int ZB_MAXJ = 8;
+constexpr int ZB_SPLITS = 32;  // == latent.hip LAT_SPLITS: the part array is [N][32][L]
+constexpr int ZB_BANDS = 16;   // row bands per sample of the region pass
+constexpr int ZB_CW = 32;      // output channels per finish block
+constexpr int ZB_NS = 5;       // region partials: total, col 0, col W-1, row 0, row H-1
+constexpr int ZB_MAXN = 64;
+
+struct ZbJobs {
+  VuZbJob j[ZB_MAXJ];
+};
+
+VU_DEV int find_job(const ZbJobs& jobs, int njobs) {
+  int j = 0;
+  while (j + 1 < njobs && (int64_t)blockIdx.x >= jobs.j[j + 1].block0) ++j;
+  return j;
+}
+
+// tap k (0..2) of a row / column is inside the image for border class cr
+VU_DEV bool tap_in(int cr, int k) { return !((cr == 0 && k == 0) || (cr == 2 && k == 2)); }
+
+// ---- forward: the bias tables -------------------------------------------
+__global__ __launch_bounds__(256) void zbias_fwd_kernel(const ZbJobs jobs, int njobs, int N) {
+  const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
+  const int e = (int)((int64_t)blockIdx.x - J.block0) * 256 + threadIdx.x;
+  if (e >= N * J.co) return;
+  const int n = e / J.co, c = e - n * J.co;
+  float S[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) S[t] = 0.f;
+  const float* a = J.act + (int64_t)n * J.L;
+  const float* wr = J.w + (int64_t)c * J.ws_co + (int64_t)J.cz0 * J.ws_ci;
+  for (int l = 0; l < J.L; ++l) {
+    const float av = a[l];
+    const float* w = wr + (int64_t)l * J.ws_ci;
+    float wv[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wv[t] = w[(t / 3) * J.ws_ky + (t % 3) * J.ws_kx];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) S[t] += wv[t] * av;
+  }
+  const float sc = J.row_scale ? J.row_scale[c] : 1.f;
+#pragma unroll
+  for (int cr = 0; cr < 3; ++cr)
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) {
+      float t = 0.f;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+          if (tap_in(cr, ky) && tap_in(cc, kx)) t += S[ky * 3 + kx];
+      J.table[((int64_t)n * 9 + cr * 3 + cc) * J.co + c] = t * sc;
+    }
+}
+
+// ---- backward 1: region partials per (sample, row band) -----------------
+// rs[((n * ZB_BANDS + band) * ZB_NS + k) * co + c]
+template <typename T>
+__global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int njobs, int N) {
+  __shared__ float sh[ZB_NS * 2048];
+  const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
+  const int lb = (int)((int64_t)blockIdx.x - J.block0);
+  const int n = lb / ZB_BANDS, band = lb - (lb / ZB_BANDS) * ZB_BANDS;
+  const int H = J.H, W = J.W, C = J.co;
+  const int V = C >> 3, slots = 256 / V;
+  const int tid = threadIdx.x, cv = tid % V, slot = tid / V;
+  const int r0 = band * H / ZB_BANDS, r1 = (band + 1) * H / ZB_BANDS;
+  float s[ZB_NS][8];
+#pragma unroll
+  for (int k = 0; k < ZB_NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[k][e] = 0.f;
+  if (slot < slots) {
+    const T* base = reinterpret_cast<const T*>(J.dy) + (int64_t)n * H * W * J.dy_stride + cv * 8;
+    const FastDiv dw((uint32_t)W);
+    const int p1 = r1 * W;
+    for (int p = r0 * W + slot; p < p1; p += 4 * slots) {
+      Vec8<T> v[4];
+      int pp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // 4 loads in flight, clamped (summed only when inside)
+        pp[u] = p + u * slots;
+        v[u].load(base + (int64_t)(pp[u] < p1 ? pp[u] : p1 - 1) * J.dy_stride);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pp[u] >= p1) break;
+        const int y = (int)dw.div((uint32_t)pp[u]), x = pp[u] - y * W;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[u].get(e);
+          s[0][e] += d;
+          if (x == 0) s[1][e] += d;
+          if (x == W - 1) s[2][e] += d;
+          if (y == 0) s[3][e] += d;
+          if (y == H - 1) s[4][e] += d;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < ZB_NS; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sh[(k * slots + slot) * C + cv * 8 + e] = s[k][e];
+  }
+  __syncthreads();
+  for (int q = tid; q < ZB_NS * C; q += 256) {
+    const int k = q / C, c = q - (q / C) * C;
+    float t = 0.f;
+    for (int r = 0; r < slots; ++r) t += sh[(k * slots + r) * C + c];
+    J.rs[(((int64_t)n * ZB_BANDS + band) * ZB_NS + k) * C + c] = t;
+  }
+}
+
+// ---- backward 2: per 32 output channels, R -> dW rows, dc partial -------
+template <typename T>
+__global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int njobs, int N) {
+  extern __shared__ float zsm[];
+  const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
+  const int chunk = (int)((int64_t)blockIdx.x - J.block0);
+  const int c0 = chunk * ZB_CW, cw = J.co - c0 < ZB_CW ? J.co - c0 : ZB_CW;
+  const int L = J.L, H = J.H, W = J.W, C = J.co;
+  const int nchunks = (C + ZB_CW - 1) / ZB_CW;
+  float* R = zsm;                        // [N][ZB_CW][9]
+  float* Wl = R + N * ZB_CW * 9;         // [ZB_CW][L][9]
+  float* A = Wl + ZB_CW * L * 9;         // [N][L]
+  const int tid = threadIdx.x;
+  for (int e = tid; e < N * L; e += 256) A[e] = J.act[e];
+  for (int e = tid; e < ZB_CW * L * 9; e += 256) {
+    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
+    Wl[e] = c < cw ? J.w[(int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky +
+                         (t % 3) * J.ws_kx]
+                   : 0.f;
+  }
+  // R[n][c][tap] from the band partials (fixed order) and the four corners
+  const T* dy = reinterpret_cast<const T*>(J.dy);
+  for (int e = tid; e < N * ZB_CW; e += 256) {
+    const int n = e / ZB_CW, c = e - n * ZB_CW;
+    float tot = 0.f, col0 = 0.f, colL = 0.f, row0 = 0.f, rowL = 0.f, k00 = 0.f, k0L = 0.f, kL0 = 0.f, kLL = 0.f;
+    if (c < cw) {
+      const float* rp = J.rs + (int64_t)n * ZB_BANDS * ZB_NS * C + c0 + c;
+      for (int b = 0; b < ZB_BANDS; ++b) {
+        tot += rp[(b * ZB_NS + 0) * C];
+        col0 += rp[(b * ZB_NS + 1) * C];
+        colL += rp[(b * ZB_NS + 2) * C];
+        row0 += rp[(b * ZB_NS + 3) * C];
+        rowL += rp[(b * ZB_NS + 4) * C];
+      }
+      const T* d = dy + (int64_t)n * H * W * J.dy_stride + c0 + c;
+      k00 = ld1<T>(d);
+      k0L = ld1<T>(d + (int64_t)(W - 1) * J.dy_stride);
+      kL0 = ld1<T>(d + (int64_t)(H - 1) * W * J.dy_stride);
+      kLL = ld1<T>(d + ((int64_t)(H - 1) * W + W - 1) * J.dy_stride);
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        float r = tot;
+        if (ky == 0) r -= row0;
+        if (ky == 2) r -= rowL;
+        if (kx == 0) r -= col0;
+        if (kx == 2) r -= colL;
+        if (ky == 0 && kx == 0) r += k00;
+        if (ky == 0 && kx == 2) r += k0L;
+        if (ky == 2 && kx == 0) r += kL0;
+        if (ky == 2 && kx == 2) r += kLL;
+        R[(n * ZB_CW + c) * 9 + ky * 3 + kx] = r;
+      }
+  }
+  __syncthreads();
+  // dW[c0 + c][cz0 + l][tap] (+)= sum_n act[n][l] R[n][c][tap]  (dw NULL: conv1 frozen)
+  for (int e = tid; J.dw && e < cw * L; e += 256) {
+    const int c = e / L, l = e - (e / L) * L;
+    float s[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) s[t] = 0.f;
+    for (int n = 0; n < N; ++n) {
+      const float a = A[n * L + l];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) s[t] += a * R[(n * ZB_CW + c) * 9 + t];
+    }
+    float* d = J.dw + (int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      float* p = d + (t / 3) * J.ws_ky + (t % 3) * J.ws_kx;
+      *p = J.grad_acc ? *p + s[t] : s[t];
+    }
+  }
+  // dc partial of this chunk -> split `chunk` of part[n][split][l]; chunk 0
+  // also zeroes the splits no chunk uses
+  for (int e = tid; e < N * L; e += 256) {
+    const int n = e / L, l = e - (e / L) * L;
+    float s = 0.f;
+    for (int c = 0; c < cw; ++c)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) s += Wl[(c * L + l) * 9 + t] * R[(n * ZB_CW + c) * 9 + t];
+    J.part[((int64_t)n * ZB_SPLITS + chunk) * L + l] = s;
+    if (chunk == 0)
+      for (int sp = nchunks; sp < ZB_SPLITS; ++sp) J.part[((int64_t)n * ZB_SPLITS + sp) * L + l] = 0.f;
+  }
+}
+
+#define DISPATCH_T(dtype, ...) \
+  if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
+
+size_t bwd_lds_bytes(int N, int L) { return (size_t)(N * ZB_CW * 9 + ZB_CW * L * 9 + N * L) * sizeof(float); }
+
+int pack(const VuZbJob* jobs, int njobs, ZbJobs& J) {
+  if (njobs < 1 || njobs > ZB_MAXJ) return (int)hipErrorInvalidValue;
+  for (int j = 0; j < njobs; ++j) J.j[j] = jobs[j];
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int vu_zbias_supported(int N, int L, int co) {
+  if (N < 1 || N > ZB_MAXN || L < 1 || L > 64 || co < 8 || co % 8 || co / 8 > 256) return 0;
+  if ((co + ZB_CW - 1) / ZB_CW > ZB_SPLITS) return 0;
+  return bwd_lds_bytes(N, L) <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int64_t vu_zbias_rs_floats(int N, int co) { return (int64_t)N * ZB_BANDS * ZB_NS * co; }
+
+extern "C" int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream) {
+  ZbJobs J;
+  if (int rc = pack(jobs, njobs, J)) return rc;
+  int64_t blocks = 0;
+  for (int j = 0; j < njobs; ++j) {
+    VuZbJob& q = J.j[j];
+    if (!vu_zbias_supported(N, q.L, q.co) || !q.w || !q.act || !q.table) return (int)hipErrorInvalidValue;
+    q.block0 = blocks;
+    blocks += ((int64_t)N * q.co + 255) / 256;
+  }
+  hipLaunchKernelGGL(zbias_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J, njobs, N);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, void* stream) {
+  ZbJobs J;
+  if (int rc = pack(jobs, njobs, J)) return rc;
+  int64_t rblocks = 0;
+  int maxL = 1;
+  for (int j = 0; j < njobs; ++j) {
+    VuZbJob& q = J.j[j];
+    if (!vu_zbias_supported(N, q.L, q.co) || !q.w || !q.act || !q.dy || !q.rs || !q.part ||
+        q.H < 2 || q.W < 2 || q.dy_stride % 8)
+      return (int)hipErrorInvalidValue;
+    if ((int64_t)q.H * q.W >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+    q.block0 = rblocks;
+    rblocks += (int64_t)N * ZB_BANDS;
+    maxL = q.L > maxL ? q.L : maxL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((zbias_rs_kernel<T>), dim3((unsigned)rblocks), dim3(256), 0, st, J, njobs, N);
+  })
+  int64_t fblocks = 0;
+  for (int j = 0; j < njobs; ++j) {
+    J.j[j].block0 = fblocks;
+    fblocks += (J.j[j].co + ZB_CW - 1) / ZB_CW;
+  }
+  const size_t lds = bwd_lds_bytes(N, maxL);
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((zbias_bwd_kernel<T>), dim3((unsigned)fblocks), dim3(256), lds, st, J, njobs, N);
+  })
+  return (int)hipGetLastError();
+}

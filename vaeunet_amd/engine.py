@@ -233,23 +233,34 @@ def refresh_weights(params):
                 cache[key] = (ver, build())
 
 
-def w3x3_fwd(w, d, cin_pad=None):
-    """[Cout, Cin, R, S] -> B[Cout][(r*S+s)*Cp + c] (Cp >= Cin zero padded)."""
+def w3x3_fwd(w, d, cin_pad=None, cin_use=None):
+    """[Cout, Cin, R, S] -> B[Cout][(r*S+s)*Cp + c] (Cp >= Cin zero padded).
+    cin_use < Cin: only the first cin_use input channels (Cp = cin_use) -- a
+    DecoderBlock conv1 whose z_proj source rides the latent shortcut."""
     co, ci, R, S = w.shape
-    cp = cin_pad or ci
+    nv = cin_use or ci
+    cp = cin_use or cin_pad or ci
 
     def build():
         s = w.stride()
-        return K.permute4(w.detach(), 0, (s[0], s[2], s[3], s[1]), (co, R, S, cp), ci, d).view(co, -1)
-    return _cached(w, ("w3f", d, cp), build)
+        return K.permute4(w.detach(), 0, (s[0], s[2], s[3], s[1]), (co, R, S, cp), nv, d).view(co, -1)
+    return _cached(w, ("w3f", d, cp, nv), build)
 
 
-def w3x3_dgrad(w, d, rows_pad=None):
+def w3x3_dgrad(w, d, rows_pad=None, rows_use=None):
     """Input-gradient weights: B[ci][(r'*S+s')*Cout + co] = W[co][ci][R-1-r'][S-1-s'].
     rows_pad > Cin: zero rows for the padded input channels of a 64-aligned
     concat (a persistent zero-initialised image whose first Cin rows are
-    rebuilt each step)."""
+    rebuilt each step).  rows_use < Cin: the first rows_use input channels
+    only (the latent shortcut, as w3x3_fwd's cin_use)."""
     co, ci, R, S = w.shape
+    if rows_use is not None and rows_use < ci:
+        def build_sub():
+            s = w.stride()
+            base = (R - 1) * s[2] + (S - 1) * s[3]
+            return K.permute4(w.detach(), base, (s[1], -s[2], -s[3], s[0]), (rows_use, R, S, co), co,
+                              d).view(rows_use, -1)
+        return _cached(w, ("w3d", d, "use", rows_use), build_sub)
     rp = rows_pad or ci
 
     def build():
@@ -336,8 +347,10 @@ def convT_layout(g):
     return (s[0], s[3], s[1])
 
 
-def wgrad3x3(dy, srcs, w, M, cvalid=None):
-    g, acc = grad_sink(w)
+def wgrad3x3(dy, srcs, w, M, cvalid=None, sink=None):
+    """sink: a (grad, accumulate) taken by the caller -- when another kernel
+    writes other input channels of the same gradient (the latent shortcut)."""
+    g, acc = sink if sink is not None else grad_sink(w)
     if g is None:
         return
     co = dy.shape[1]
@@ -502,7 +515,7 @@ def can_fold(M, bn):
         and bn.running_mean is not None
 
 
-def fold_bn_eval(M, conv, bn, cin_pad=None):
+def fold_bn_eval(M, conv, bn, cin_pad=None, cin_use=None):
     """(weight image, bias) of ``conv`` followed by the eval-mode ``bn``:
     rows of the fp32 image scaled by gamma / sqrt(running_var + eps), bias
     (conv bias) * scale + beta - running_mean * scale; storage dtype image.
@@ -510,7 +523,7 @@ def fold_bn_eval(M, conv, bn, cin_pad=None):
     train-mode kernels, so no version counter would tell a cache)."""
     co = conv.out_channels
     coef = bn_coef(bn, None, co)                    # eval rows: scale, shift
-    img = w3x3_fwd(conv.weight, F32, cin_pad)       # [co][R*S*Cp] fp32, cached
+    img = w3x3_fwd(conv.weight, F32, cin_pad, cin_use)  # [co][R*S*Cp] fp32, cached
     w = img * coef[0][:, None]
     if M.d != F32:
         w = w.to(torch.bfloat16)
@@ -518,19 +531,21 @@ def fold_bn_eval(M, conv, bn, cin_pad=None):
     return w, b.contiguous()
 
 
-def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
+def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False, zbias=None, cin_use=None):
     """defer: leave BN + ReLU unapplied (returns a = None) when the consumer
-    is a MaxPool2d that applies it in the same pass (down_fwd)."""
+    is a MaxPool2d that applies it in the same pass (down_fwd).  zbias /
+    cin_use: the latent shortcut of a DecoderBlock conv1 (the conv contracts
+    over the first cin_use input channels; VuGemmFwd.zbias adds the rest)."""
     N, _, H, W = srcs[0].shape
     co = conv.out_channels
     if can_fold(M, bn) and not defer:
-        wf, bf = fold_bn_eval(M, conv, bn, cin_pad)
+        wf, bf = fold_bn_eval(M, conv, bn, cin_pad, cin_use)
         a = M.act(N, co, H, W)
-        K.gemm_fwd(K.gather3x3(srcs), wf, co, a, M.d, bias=bf, relu=True)
+        K.gemm_fwd(K.gather3x3(srcs), wf, co, a, M.d, bias=bf, relu=True, zbias=zbias)
         return a, None
     y = M.act(N, co, H, W)
-    st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad), co, y, M.d,
-                    stats=bn.training)
+    st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad, cin_use), co, y, M.d,
+                    stats=bn.training, zbias=zbias)
     if defer and K.pool_fusable(y):
         return None, (y, bn_coef(bn, st, co))
     a = M.act(N, co, H, W)
@@ -539,10 +554,15 @@ def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False):
 
 
 def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=None, dsrc_acc=False,
-                     cin_pad=None, da_part=None, feeds=None):
+                     cin_pad=None, da_part=None, feeds=None, shortcut=None):
     """cin_pad: compute the input gradient for cin_pad channels (zero weight
     rows past conv.in_channels) so that its column count stays a tile
     multiple; the caller reads the real channels only.
+    shortcut: the latent shortcut of a DecoderBlock conv1 (vae_engine.ZShortcut):
+    srcs are its first shortcut.lead input channels; their weight gradient is
+    written through shortcut.sink; dy (the pre-BN gradient) is kept for the
+    shortcut's backward, which writes the z columns and then reports the
+    weight to the DP reducer.
     da_part: BatchNorm-backward partials of ``da`` from the GEMM that made it.
     feeds=(saved, bn) of the BN(+ReLU) the input gradient feeds (the previous
     conv's): its first backward reduction stage then rides this input-gradient
@@ -550,25 +570,27 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     cannot."""
     y, coef = saved
     dy = bn_bwd(da, y, coef, bn, True, M, part=da_part)
+    if shortcut is not None:
+        shortcut.dy = dy
 
     def wg():
-        wgrad3x3(dy, srcs, conv.weight, M, cvalid)
-        M.notify([conv.weight, bn.weight, bn.bias])
+        wgrad3x3(dy, srcs, conv.weight, M, cvalid, sink=shortcut.sink if shortcut is not None else None)
+        M.notify([bn.weight, bn.bias] + ([conv.weight] if shortcut is None else []))
     M.side(wg, dy, *srcs)
     if not need_dsrc:
         return None
     N, _, H, W = y.shape
     # a channel-padded input (the 3-channel image) gets a gradient for its
     # real channels only: the dgrad weights have conv.in_channels rows
-    cin = cin_pad or conv.in_channels
+    cin = shortcut.lead if shortcut is not None else (cin_pad or conv.in_channels)
     if dsrc is None:
         dsrc = M.act(N, cin, H, W)
     bnb = None
     if feeds is not None and FUSE_BN_BWD_REDUCE:
         (fy, fcoef), fbn = feeds
         bnb = (fy, fcoef, True)
-    part = K.gemm_fwd(K.gather3x3([dy]), w3x3_dgrad(conv.weight, M.d, cin), cin, dsrc, M.d, accumulate=dsrc_acc,
-                      kind="dgrad", bnb=bnb)
+    wd = w3x3_dgrad(conv.weight, M.d, rows_use=cin) if shortcut is not None else w3x3_dgrad(conv.weight, M.d, cin)
+    part = K.gemm_fwd(K.gather3x3([dy]), wd, cin, dsrc, M.d, accumulate=dsrc_acc, kind="dgrad", bnb=bnb)
     if feeds is not None:
         return dsrc, part
     return dsrc

@@ -97,6 +97,7 @@ def _decode(model, M, feats, z, skip_always=False):
         # z_initial and every z_proj on the [N, L] vectors, maps written once
         cons, zps = V.latent_consumers(M, model, feats, N, skip_always)
         V.latent_fwd(M, z.float().contiguous(), cons)
+        V.zbias_tables(M, [c.zsc for c in cons if c.zsc is not None])
         h = cons[0].out if model.use_bottleneck else feats[-1]
     elif model.use_bottleneck:
         h, _ = V.cbr1x1_fwd(M, model.z_initial, V.latent_map(M, z, N, H4, W4))

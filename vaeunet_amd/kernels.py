@@ -167,7 +167,7 @@ class BnbPart:
 
 
 def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accumulate=False,
-             convT=None, kind="fwd", strided=None, bnb=None, flops=None, relu=False):
+             convT=None, kind="fwd", strided=None, bnb=None, flops=None, relu=False, zbias=None):
     """out[m][j] = sum_k A[m][k] wmat[j][k] (+bias).  convT=(oH,oW,opy,opx,cout) selects
     the pixel-shuffle epilogue, strided=(oH,oW,opy,opx) the stride-2 sub-lattice one.
     bnb=(x, coef, relu): also emit the BatchNorm-backward partials of the output
@@ -175,8 +175,9 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     invstd) when the selected kernel can (returns a BnbPart then, else None).
     flops: the algorithmic work the roofline accounting credits this launch
     with (default 2*M*N*K of the GEMM as launched).  relu: epilogue ReLU on
-    acc + bias (an eval-mode BatchNorm folded into wmat / bias).  Returns
-    Stats if requested."""
+    acc + bias (an eval-mode BatchNorm folded into wmat / bias).  zbias: the
+    [N][9][ncol] fp32 per-sample border-class bias table of the latent
+    shortcut (VuGemmFwd.zbias, vu_zbias_fwd).  Returns Stats if requested."""
     a = VuGemmFwd()
     a.a = g
     a.b = wmat.data_ptr()
@@ -195,6 +196,7 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     else:
         a.out_mode = 0
     a.bias = bias.data_ptr() if bias is not None else None
+    a.zbias = zbias.data_ptr() if zbias is not None else None
     a.accumulate = 1 if accumulate else 0
     a.relu = 1 if relu else 0
     st = None
@@ -240,7 +242,7 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
     M = g.N * g.H * g.W
     launch = lambda: call("vu_gemm_fwd", C.byref(a), dtype, stream())  # noqa: E731
     if AUDIT is not None:
-        AUDIT.gemm_fwd(a, dtype, g, wmat, out, bias, st, launch)
+        AUDIT.gemm_fwd(a, dtype, g, wmat, out, bias, st, launch, zbias=zbias)
     else:
         def kname():
             k = FWD_KERNELS.get(query("vu_gemm_fwd_kernel", C.byref(a), dtype), "?")

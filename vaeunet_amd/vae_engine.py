@@ -308,7 +308,9 @@ def sample_sum(M, x, scale=1.0, out=None, accumulate=False):
 def decoder_fwd(M, blk, x, skip, z, zp_vec=None):
     """zp_vec: the block's z_proj map already written by the latent vector
     path (latent_fwd; cpad channels incl. the zero padding) -- its backward
-    is then deferred to latent_bwd (decoder_bwd returns the map's gradient)."""
+    is then deferred to latent_bwd (decoder_bwd returns the map's gradient);
+    or a ZShortcut (round 5): no map at all, conv1 contracts over [x, skip]
+    and adds the z part as its per-sample border-class bias table."""
     N = x.shape[0]
     if skip is not None:
         H, W = skip.shape[2], skip.shape[3]
@@ -326,7 +328,10 @@ def decoder_fwd(M, blk, x, skip, z, zp_vec=None):
         srcs.append(sk)
     szp = None
     cpad = None
-    if blk.use_latent and zp_vec is not None:
+    zsc = zp_vec if isinstance(zp_vec, ZShortcut) else None
+    if zsc is not None:
+        szp = zsc
+    elif blk.use_latent and zp_vec is not None:
         L = blk.z_proj[0].out_channels
         lead = sum(t.shape[1] for t in srcs)
         if zp_vec.shape[1] != L:
@@ -355,7 +360,10 @@ def decoder_fwd(M, blk, x, skip, z, zp_vec=None):
         else:
             zp, szp = cbr1x1_fwd(M, blk.z_proj, zb)
         srcs.append(zp)
-    a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1], cin_pad=cpad)
+    if zsc is not None:
+        a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1], zbias=zsc.table, cin_use=zsc.lead)
+    else:
+        a1, s1 = E.conv_bn_relu_fwd(M, srcs, blk.conv1[0], blk.conv1[1], cin_pad=cpad)
     a2, s2 = E.conv_bn_relu_fwd(M, [a1], blk.conv2[0], blk.conv2[1])
     return a2, (x, skip, xu, srcs, satt, szp, a1, s1, s2, cpad)
 
@@ -367,8 +375,14 @@ def decoder_bwd(M, blk, saved, dout, z=None):
     da1, part = E.conv_bn_relu_bwd(M, [a1], blk.conv2[0], blk.conv2[1], s2, dout, True,
                                    feeds=(s1, blk.conv1[1]))
     conv1 = blk.conv1[0]
+    zsc = szp if isinstance(szp, ZShortcut) else None
+    if zsc is not None:
+        # one gradient sink for both writers of conv1.weight.grad (the GEMM:
+        # the [x, skip] columns; latent_bwd's vu_zbias_bwd: the z columns)
+        zsc.sink = E.grad_sink(conv1.weight)
     dsrc = E.conv_bn_relu_bwd(M, srcs, conv1, blk.conv1[1], s1, da1, True,
-                              cvalid=conv1.in_channels if cpad else None, cin_pad=cpad, da_part=part)
+                              cvalid=conv1.in_channels if cpad else None, cin_pad=cpad, da_part=part,
+                              shortcut=zsc)
     cx = xu.shape[1]
     off = cx
     dskip = dz = None
@@ -380,7 +394,9 @@ def decoder_bwd(M, blk, saved, dout, z=None):
         else:
             dskip = dsk
         off += cs
-    if blk.use_latent and szp == "vec":
+    if zsc is not None:
+        dz = ("shortcut", zsc)   # the z part's backward runs in latent_bwd (vu_zbias_bwd)
+    elif blk.use_latent and szp == "vec":
         # the z_proj backward runs on the sample vectors (latent_bwd)
         dz = ("vec", dsrc[:, off:off + blk.z_proj[0].out_channels])
     elif blk.use_latent:
@@ -455,15 +471,23 @@ class LatentConsumer:
     output map (``out``, cpad >= co channels, zeros past co) and the saved
     vectors y [N, co] (pre-BN) and coef [4, co] (scale, shift, mean, invstd)."""
 
-    def __init__(self, seq, out):
+    def __init__(self, seq, out, shape=None):
+        """out None (the latent shortcut): no map; shape = (N, H, W, device)
+        and the activated vectors land in ``act`` [N, co]."""
         self.conv, self.bn = seq[0], seq[1]
         self.out = out
-        N, _, H, W = out.shape
+        if out is not None:
+            N, _, H, W = out.shape
+            dev = out.device
+        else:
+            N, H, W, dev = shape
         co = self.conv.out_channels
         self.HW = H * W
-        self.y = torch.empty((N, co), dtype=torch.float32, device=out.device)
-        self.coef = torch.empty((4, co), dtype=torch.float32, device=out.device)
+        self.y = torch.empty((N, co), dtype=torch.float32, device=dev)
+        self.coef = torch.empty((4, co), dtype=torch.float32, device=dev)
+        self.act = torch.empty((N, co), dtype=torch.float32, device=dev) if out is None else None
         self.dmap = None
+        self.zsc = None   # the ZShortcut this consumer feeds
 
     def job(self):
         conv, bn = self.conv, self.bn
@@ -476,8 +500,13 @@ class LatentConsumer:
         j.num_batches_tracked = bn.num_batches_tracked.data_ptr() if track and bn.training else None
         j.momentum, j.eps = float(bn.momentum), float(bn.eps)
         j.train = 1 if bn.training else 0
-        j.co, j.cpad, j.HW = conv.out_channels, self.out.shape[1], self.HW
-        j.out, j.out_stride = self.out.data_ptr(), K.pstride(self.out)
+        if self.out is not None:
+            j.co, j.cpad, j.HW = conv.out_channels, self.out.shape[1], self.HW
+            j.out, j.out_stride = self.out.data_ptr(), K.pstride(self.out)
+        else:
+            j.co, j.cpad, j.HW = conv.out_channels, conv.out_channels, self.HW
+            j.out, j.out_stride = None, 0
+        j.act = K.ptr(self.act)
         j.y, j.coef = self.y.data_ptr(), self.coef.data_ptr()
         return j
 
@@ -495,7 +524,8 @@ def latent_consumers(M, model, feats, N, skip_always=False):
     DecoderBlock, each with its output map allocated at the size that block
     sees (the skip's, or twice its input's) -- the z_proj maps channel-padded
     to 64 when the concat before them is 64-aligned (decoder_fwd's layout).
-    Returns (consumers, per-block z_proj map or None)."""
+    Returns (consumers, per-block z_proj map, ZShortcut (the round-5 latent
+    shortcut: no map) or None)."""
     f4 = feats[-1]
     H4, W4 = f4.shape[2], f4.shape[3]
     cons, zps = [], [None] * len(model.decoder_blocks)
@@ -509,6 +539,12 @@ def latent_consumers(M, model, feats, N, skip_always=False):
         if blk.use_latent:
             Lb = blk.z_proj[0].out_channels
             lead = blk.conv1[0].in_channels - Lb
+            if shortcut_ok(M, blk, N, size):
+                c = LatentConsumer(blk.z_proj, None, (N, size[0], size[1], f4.device))
+                c.zsc = ZShortcut(blk, c, lead, size[0], size[1])
+                cons.append(c)
+                zps[i] = c.zsc
+                continue
             Lp = -(-Lb // 64) * 64
             cpad = Lp if (lead % 64 == 0 and Lp != Lb) else Lb
             cons.append(LatentConsumer(blk.z_proj, M.act(N, cpad, size[0], size[1])))
@@ -516,12 +552,99 @@ def latent_consumers(M, model, feats, N, skip_always=False):
     return cons, zps
 
 
+# The latent shortcut (round 5, csrc/zbias.hip): a DecoderBlock conv1 whose
+# z_proj source is the per-sample constant map of the vector path contracts
+# over [x, skip] only; the z part is a per-sample, per-border-class bias of
+# its GEMM epilogue, its backward per-sample region sums of conv1's dy.
+LATENT_SHORTCUT = True   # A/B switch: False = the round-4 map (64-channel padded z_proj source)
+
+
+def shortcut_ok(M, blk, N, size):
+    conv1 = blk.conv1[0]
+    Lb = blk.z_proj[0].out_channels
+    lead = conv1.in_channels - Lb
+    epc = 8 if M.d != F32 else 4
+    return (LATENT_SHORTCUT and size[0] >= 2 and size[1] >= 2 and lead > 0 and lead % epc == 0
+            and conv1.kernel_size == (3, 3) and conv1.stride == (1, 1) and conv1.padding == (1, 1)
+            and conv1.groups == 1 and conv1.bias is None
+            and bool(K.query("vu_zbias_supported", N, Lb, conv1.out_channels)))
+
+
+class ZShortcut:
+    """One DecoderBlock's latent shortcut: conv1's input channels [lead,
+    lead + L) are the consumer's constant map c_n (consumer.act)."""
+
+    def __init__(self, blk, cons, lead, H, W):
+        self.blk, self.cons, self.lead, self.H, self.W = blk, cons, lead, H, W
+        N = cons.act.shape[0]
+        self.table = torch.empty((N, 9, blk.conv1[0].out_channels), dtype=torch.float32,
+                                 device=cons.act.device)
+        self.row_scale = None    # eval-mode BN folded into conv1 (inference)
+        self.dy = None           # backward: conv1's pre-BN gradient (engine.conv_bn_relu_bwd)
+        self.sink = None         # backward: (conv1.weight.grad, accumulate)
+
+    def job(self):
+        conv1 = self.blk.conv1[0]
+        w = conv1.weight
+        j = _lib.VuZbJob()
+        j.w = w.data_ptr()
+        j.ws_co, j.ws_ci, j.ws_ky, j.ws_kx = w.stride()
+        j.cz0, j.L, j.co, j.H, j.W = self.lead, self.cons.conv.out_channels, conv1.out_channels, self.H, self.W
+        j.act = self.cons.act.data_ptr()
+        j.row_scale = K.ptr(self.row_scale)
+        j.table = self.table.data_ptr()
+        return j
+
+
+def _zb_jobs(zscs):
+    arr = (_lib.VuZbJob * len(zscs))()
+    for i, z in enumerate(zscs):
+        arr[i] = z.job()
+    return arr
+
+
+def zbias_tables(M, zscs):
+    """Every shortcut block's [N][9][co] table from the consumers' vectors (one launch)."""
+    if not zscs:
+        return
+    for z in zscs:
+        bn1 = z.blk.conv1[1]
+        z.row_scale = E.bn_coef(bn1, None, z.blk.conv1[0].out_channels)[0] if E.can_fold(M, bn1) else None
+    K.call("vu_zbias_fwd", _zb_jobs(zscs), len(zscs), zscs[0].table.shape[0], K.stream())
+
+
+def zbias_backward(M, zscs, parts):
+    """The shortcut blocks' z-part backward (two launches): conv1.weight.grad's
+    z columns and the consumers' dc partials (into ``parts``), then conv1's
+    weight reported to the DP reducer (behind its GEMM weight gradient)."""
+    N = zscs[0].table.shape[0]
+    arr = _zb_jobs(zscs)
+    keep = []
+    for i, z in enumerate(zscs):
+        conv1 = z.blk.conv1[0]
+        g, acc = z.sink
+        rs = torch.empty(K.query("vu_zbias_rs_floats", N, conv1.out_channels), dtype=torch.float32,
+                         device=z.table.device)
+        keep.append(rs)
+        arr[i].dy, arr[i].dy_stride = z.dy.data_ptr(), K.pstride(z.dy)
+        arr[i].rs, arr[i].part = rs.data_ptr(), parts[i].data_ptr()
+        arr[i].dw, arr[i].grad_acc = K.ptr(g), 1 if acc else 0
+    K.call("vu_zbias_bwd", arr, len(zscs), N, K.dcode(zscs[0].dy.dtype), K.stream())
+    ws = [z.blk.conv1[0].weight for z in zscs if z.sink[0] is not None]
+    M.side(lambda: M.notify(ws), *[z.dy for z in zscs])
+    for z in zscs:
+        z.dy = None
+        z.sink = None
+    return keep
+
+
 def latent_fwd(M, z, cons):
     """Every consumer's map from z [N, L] in one launch."""
     if not cons:
         return
     for c in cons:
-        K.call("vu_latent_check_job", c.conv.out_channels, c.out.shape[1], K.pstride(c.out), M.d)
+        if c.out is not None:
+            K.call("vu_latent_check_job", c.conv.out_channels, c.out.shape[1], K.pstride(c.out), M.d)
     K.call("vu_latent_fwd", _jobs(cons), len(cons), K.ptr(z), z.shape[0], z.shape[1], M.d, K.stream())
 
 
@@ -532,11 +655,15 @@ def latent_bwd(M, model, cons, z, eps, logvar, pooled, dmu, dlogvar):
     dev = z.device
     arr = _jobs(cons)
     keep = []
+    parts = []
     for i, c in enumerate(cons):
         part = torch.empty(K.query("vu_latent_part_floats", N, c.conv.out_channels), dtype=torch.float32,
                            device=dev)
         keep.append(part)
-        arr[i].dmap, arr[i].dmap_stride, arr[i].part = c.dmap.data_ptr(), K.pstride(c.dmap), part.data_ptr()
+        parts.append(part)
+        if c.zsc is None:
+            arr[i].dmap, arr[i].dmap_stride = c.dmap.data_ptr(), K.pstride(c.dmap)
+        arr[i].part = part.data_ptr()
         gw, accw = E.grad_sink(c.conv.weight)
         gb, accb = E.grad_sink(c.conv.bias) if c.conv.bias is not None else (None, accw)
         gg, gbe, accn = E.bn_grad_sinks(c.bn)
@@ -546,8 +673,15 @@ def latent_bwd(M, model, cons, z, eps, logvar, pooled, dmu, dlogvar):
         arr[i].grad_acc = 1 if accs == {True} else 0
         arr[i].dw, arr[i].dbias = K.ptr(gw), K.ptr(gb)
         arr[i].dgamma, arr[i].dbeta = K.ptr(gg), K.ptr(gbe)
-    if cons:
-        K.call("vu_latent_bwd_sums", arr, len(cons), N, K.dcode(cons[0].dmap.dtype), K.stream())
+    zi = [i for i, c in enumerate(cons) if c.zsc is not None]
+    if zi:
+        keep += zbias_backward(M, [cons[i].zsc for i in zi], [parts[i] for i in zi])
+    mi = [i for i, c in enumerate(cons) if c.zsc is None]
+    if mi:
+        sub = (_lib.VuLatentJob * len(mi))()
+        for k, i in enumerate(mi):
+            sub[k] = arr[i]
+        K.call("vu_latent_bwd_sums", sub, len(mi), N, K.dcode(cons[mi[0]].dmap.dtype), K.stream())
     hm, hl = model.mu_head[0], model.logvar_head[0]
     h = _lib.VuLatentHeads()
     dpooled = torch.empty_like(pooled)
@@ -608,6 +742,7 @@ def vae_tail_fwd(M, model, feats, Hin, Win, eps):
         pooled, mu, logvar, z = heads_fwd(M, model, f4, eps)
         cons, zps = latent_consumers(M, model, feats, N)
         latent_fwd(M, z, cons)
+        zbias_tables(M, [c.zsc for c in cons if c.zsc is not None])
     else:
         pooled = sample_sum(M, f4, 1.0 / (H4 * W4))
         mu = torch.empty((N, L), dtype=torch.float32, device=dev)
@@ -664,7 +799,7 @@ def vae_tail_bwd(M, model, state, dout, dmu, dlogvar):
             dh, dskip, dzi = decoder_bwd(M, model.decoder_blocks[i], sdec[i], dh)
             if dskip is not None:
                 dfeats[len(feats) - 2 - i] = dskip
-            if dzi is not None:
+            if dzi is not None and dzi[0] == "vec":
                 byblk[i].dmap = dzi[1]
         df4 = None
         if model.use_bottleneck:
