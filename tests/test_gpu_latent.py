@@ -52,19 +52,40 @@ def _rel(a, b):
 
 
 def _oracle64(model, x, t, eps, inj):
-    """fp64 gradients of the same train-mode micro-step on the CPU oracle."""
+    """fp64 gradients of the same train-mode micro-step on the CPU oracle, and
+    sigma: per BatchNorm-affine gradient, the spread ||t32 - t64|| of its
+    reduction terms (dz, dz * xhat) between the fp32 and fp64 oracle -- the
+    error a sum of those terms has from the fp32 per-term error alone
+    (tests/test_gpu_config_parity.py; the attention psi BatchNorm(1) sums are
+    ill-conditioned, sum |dz| / |sum dz| up to ~1e3-1e4)."""
     from oracle import cpu_ref as R
     st = model.state_dict()
-    p = {k: v.detach().cpu().double().requires_grad_(True) for k, v in st.items()
-         if "running" not in k and "num_batches" not in k}
-    b = {k: (v.detach().cpu().double() if v.is_floating_point() else v.detach().cpu().clone())
-         for k, v in st.items() if "running" in k or "num_batches" in k}
     sampling = inj not in ("none", "inject_no_bottleneck")
-    lg, mu, lv = R.unet_resnet_forward(x.cpu().double(), p, b, eps=eps.cpu().double() if sampling else None,
-                                       latent_injection=inj)
-    loss = R.combined_loss(lg, t.cpu().double()) + 1e-3 * R.kl_with_free_bits(mu, lv, 1e-3)
-    loss.backward()
-    return {k: v.grad for k, v in p.items() if v.grad is not None}
+
+    def run(dt):
+        p = {k: v.detach().cpu().to(dt).requires_grad_(True) for k, v in st.items()
+             if "running" not in k and "num_batches" not in k}
+        b = {k: (v.detach().cpu().to(dt) if v.is_floating_point() else v.detach().cpu().clone())
+             for k, v in st.items() if "running" in k or "num_batches" in k}
+        R.PROBE = {}
+        try:
+            lg, mu, lv = R.unet_resnet_forward(x.cpu().to(dt), p, b, eps=eps.cpu().to(dt) if sampling else None,
+                                               latent_injection=inj)
+            loss = R.combined_loss(lg, t.cpu().to(dt)) + 1e-3 * R.kl_with_free_bits(mu, lv, 1e-3)
+            loss.backward()
+            terms = {}
+            for pre, v in R.PROBE.items():
+                if not pre.startswith("gate:"):
+                    xh, y = v
+                    terms[pre + "bias"] = y.grad.detach().double()
+                    terms[pre + "weight"] = (y.grad * xh).detach().double()
+        finally:
+            R.PROBE = None
+        return {k: v.grad for k, v in p.items() if v.grad is not None}, terms
+    g64, t64 = run(torch.float64)
+    _, t32 = run(torch.float32)
+    sigma = {k: float((t32[k] - t64[k]).norm()) for k in t64 if k in t32}
+    return g64, sigma
 
 
 @pytest.mark.parametrize("inj", ["all", "first", "bottleneck", "none", "inject_no_bottleneck"])
@@ -81,7 +102,7 @@ def test_latent_vector_path_matches_map_path(inj, bf16):
     eps = torch.randn(B, 32, device=DEV)
     a = _model(inj)
     b = copy.deepcopy(a)
-    g64 = _oracle64(a, x, t, eps, inj)
+    g64, sigma = _oracle64(a, x, t, eps, inj)
     ra = _run(a, x, t, eps, True, bf16, steps=1)
     rb = _run(b, x, t, eps, False, bf16, steps=1)
     tol = 3e-2 if bf16 else 1e-4
@@ -97,7 +118,7 @@ def test_latent_vector_path_matches_map_path(inj, bf16):
         ga, gb = pa[k].grad, pb[k].grad
         da = float((ga.double().cpu() - ref).norm())
         db = float((gb.double().cpu() - ref).norm())
-        bound[k] = fac * db + floor * gmax
+        bound[k] = fac * (db + sigma.get(k, 0.0)) + floor * gmax
         worst.append((da / bound[k], k, da, db))
     worst.sort(reverse=True)
     print(f"{inj} bf16={bf16}: worst (err / bound, name, |vec - fp64|, |map - fp64|) {worst[:3]}")
