@@ -159,11 +159,15 @@ def _ref_bf16_run(R, state, x, t, eps, names, probe=False):
 # rounding boundary change -- and layer1.2.bn1.weight 3.1 / 2.2 / 27.4 %),
 # because the bf16 backward is ~80 % away from the fp32 one elementwise at
 # the encoder (the dz of every BatchNorm, in the reference's path as in ours:
-# tools/bn_drift_probe.py, profiles/r5b_bn_drift_probe.log).  Round 5: the
-# yardstick per parameter is the max over that three-input ensemble of the
-# reference's runs, and the elementwise dz drift is compared at every
-# BatchNorm (HIP must not drift more than the reference's own bf16 path).
-REF_PERTURB = (2.0 ** -12, 2.0 ** -10)
+# tools/bn_drift_probe.py, profiles/r5b_bn_drift_probe.log).  Round 5: both
+# paths run on the same four-input ensemble (the bench input and three
+# copies perturbed by a relative 2^-12 / 2^-11 / 2^-10); a BatchNorm-affine
+# gradient's drift is its MEAN over the ensemble, the HIP path's within 1.5x
+# the reference's + 5 %; weights (>= 2-D, well conditioned) compare the bench
+# input's drift with the reference ensemble's max; and the elementwise dz drift
+# is compared at every BatchNorm (HIP must not drift more than the
+# reference's own bf16 path).
+REF_PERTURB = (2.0 ** -12, 2.0 ** -11, 2.0 ** -10)
 DZ_VS_REF = 1.05
 
 
@@ -195,8 +199,8 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     ref_flips = int(((l16 > 0) != (lref > 0)).sum())
     ref_mu = max(_drift(mu16, muref)[0], _drift(lv16, lvref)[0])
     r = torch.rand(x.shape, generator=torch.Generator().manual_seed(5)) * 2 - 1
-    g16_ens = [g16] + [_ref_bf16_run(R, state, (x * (1 + sc * r)).contiguous(memory_format=CL), t, eps, names)[0]
-                       for sc in REF_PERTURB]
+    xps = [(x * (1 + sc * r)).contiguous(memory_format=CL) for sc in REF_PERTURB]
+    g16_ens = [g16] + [_ref_bf16_run(R, state, xp, t, eps, names)[0] for xp in xps]
 
     model = model.to(DEV).to(memory_format=CL).train()
     model.eps_override = eps
@@ -227,9 +231,25 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     mu_rel = max(_drift(mu.detach().float().cpu(), muref)[0], _drift(lv.detach().float().cpu(), lvref)[0])
     params = dict(model.named_parameters())
     gn = np.array([float(params[k].grad.double().norm()) if params[k].grad is not None else 0.0 for k in names])
+    ghip_ens = [gn]
+    for xp in xps:   # the same perturbed inputs through the HIP path (fresh model, same weights)
+        mp = UNetResNet(3, 1, pretrained=False)
+        mp.load_state_dict(state)
+        mp = mp.to(DEV).to(memory_format=CL).train()
+        mp.eps_override = eps
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            lp, mup, lvp = mp(xp.to(DEV))
+            lossp = CombinedLoss()(lp, t.to(DEV)) + 1e-3 * kl_with_free_bits(mup, lvp, free_bits=1e-3)
+        lossp.backward()
+        pp = dict(mp.named_parameters())
+        ghip_ens.append(np.array([float(pp[k].grad.double().norm()) if pp[k].grad is not None else 0.0
+                                  for k in names]))
+        del mp, pp
     big = gref > 1e-3 * gref.max()
     grel = np.abs(gn - gref) / np.maximum(gref, 1e-30)
     grel_ens = np.max([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in g16_ens], axis=0)
+    mean_ref = np.mean([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in g16_ens], axis=0)
+    mean_hip = np.mean([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in ghip_ens], axis=0)
     grel16 = np.abs(g16 - gref) / np.maximum(gref, 1e-30)   # the reference's own bf16 gradient drift
     # per parameter: excess over the reference's own bf16 drift (ensemble max)
     excess = grel - BF16_VS_REF_DRIFT * grel_ens
@@ -270,15 +290,18 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     bbig = [i for i in np.where(big)[0] if dims[names[i]] == 1]
     worst_w = max(excess[i] for i in wbig)
     assert worst_w < BF16_GNORM, [w for w in worst if dims[w[1]] >= 2]
-    worst_b = max(excess[i] for i in bbig)
-    assert worst_b < BF16_GNORM, [w for w in worst if dims[w[1]] == 1]
+    excess_b = mean_hip - BF16_VS_REF_DRIFT * mean_ref
+    worst_bl = sorted(((excess_b[i], names[i], mean_hip[i], mean_ref[i]) for i in bbig), reverse=True)[:3]
+    worst_b = worst_bl[0][0]
+    assert worst_b < BF16_GNORM, worst_bl
     vecs = {k: (params[k].grad.double().cpu().reshape(-1), ref.p[k].grad.double().reshape(-1),
                 ref16.p[k].grad.double().reshape(-1)) for k in (names[i] for i in bbig)}
     num = sum(float((a - r_).pow(2).sum()) for a, r_, _ in vecs.values()) ** 0.5
     num16 = sum(float((c - r_).pow(2).sum()) for _, r_, c in vecs.values()) ** 0.5
     den = sum(float(r_.pow(2).sum()) for _, r_, _ in vecs.values()) ** 0.5
     print(f"config3 bf16: BN-affine gradients, relative L2 error HIP {num / den:.3e} vs CPU-bf16 "
-          f"{num16 / den:.3e}; worst weight excess {worst_w:.3e}, worst BN-affine excess {worst_b:.3e}; "
+          f"{num16 / den:.3e}; worst weight excess {worst_w:.3e}; BN-affine ensemble-mean drift worst "
+          f"(excess, name, HIP, CPU-bf16) {[(round(float(a_), 4), b_, round(float(c_), 4), round(float(d_), 4)) for a_, b_, c_, d_ in worst_bl]}; "
           f"bench-input-only CPU-bf16 drift of the worst: {grel16[names.index(worst[0][1])]:.3f}")
     assert num / den <= BF16_VS_REF_DRIFT * num16 / den + BF16_GNORM
     assert tot < BF16_TOTAL

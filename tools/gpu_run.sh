@@ -32,7 +32,7 @@ for step in "$@"; do
       if [ -n "$arg" ]; then
         if [[ "$arg" == tests/* ]]; then sel=${arg//,/ }; else sel="tests -k ${arg//,/ or }"; fi
       fi
-      timeout -k 10 1000 python -u -m pytest $sel -m gpu -x -q --timeout 300 --timeout-method thread \
+      timeout -k 10 1000 python -u -m pytest $sel -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread \
         > $O/tests_$n.log 2>&1 || { echo "TESTS_FAIL ($step)"; tail -40 $O/tests_$n.log; exit 1; }
       tail -1 $O/tests_$n.log ;;
     bench)
