@@ -167,7 +167,7 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     with the persistent v5 kernel (gemm_fwd5.hip), 0 routes them to v2,
  *     k >= 2 caps its grid at k blocks (tests: several tiles per block);
  *   VU_TUNE_V6: 1 (default) serves 64 -> 64 3x3 convs (and their input
- *     gradients) with >= 2 tiles of 16x32 pixels per CU with the
+ *     gradients) with >= 1 tile of 16x32 pixels per CU with the
  *     resident-weight persistent kernel (gemm_fwd6.hip), 0 routes them to
  *     v3/v4, k >= 2 serves any grid with the grid capped at k (tests). */
 #define VU_TUNE_V4_MIN_BLOCKS 0

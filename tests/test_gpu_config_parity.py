@@ -174,10 +174,14 @@ DZ_VS_REF = 1.05
 @pytest.mark.timeout(900)
 def test_unetresnet_config3_bf16_b8_vs_oracle():
     from oracle import cpu_ref as R
-    from vaeunet_amd import UNetResNet, engine as E
+    from vaeunet_amd import UNetResNet, engine as E, _lib
     from vaeunet_amd.init import seeded_init_
     from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
     _threads()
+    # diagnostics: VU_TEST_TUNE="KEY=VAL,..." (vu_gemm_set_tuning before the run)
+    for kv in filter(None, os.environ.get("VU_TEST_TUNE", "").split(",")):
+        key, val = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(key), int(val))
     model = seeded_init_(UNetResNet(3, 1, pretrained=False), 0)
     state = model.state_dict()
     names = [k for k, _ in model.named_parameters()]

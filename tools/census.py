@@ -3,7 +3,7 @@ engine is bracketed by HIP events (on the launch stream) and attributed to
 its engine call site and, for the GEMMs, to its shape and algorithmic HBM
 bytes.  A tuning aid, not part of the product.
 
-usage: python tools/census.py [--model unet|vae] [--steps 2] [--top 60]
+usage: python tools/census.py [--model unet|vae] [--steps 2] [--top 60] [--engine-flag M.NAME=V] [--tune K=V]
 """
 import argparse
 import collections
@@ -75,8 +75,20 @@ def main():
     ap.add_argument("--model", default="unet")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=70)
+    ap.add_argument("--engine-flag", action="append", default=[], metavar="MODULE.NAME=VAL",
+                    help="set a vaeunet_amd module switch first (as bench.py), e.g. vae_engine.LATENT_SHORTCUT=0")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VAL")
     args = ap.parse_args()
     import importlib
+    for kv in args.engine_flag:
+        name, val = kv.split("=")
+        modname, name = name.rsplit(".", 1) if "." in name else ("engine", name)
+        mod = importlib.import_module("vaeunet_amd." + modname)
+        old = getattr(mod, name)
+        setattr(mod, name, bool(int(val)) if isinstance(old, bool) else type(old)(int(val)))
+    for kv in args.tune:
+        key, val = kv.split("=")
+        _lib.call("vu_gemm_set_tuning", int(key), int(val))
     _lib.call = tcall
     for m in ("kernels", "loss", "optim", "metrics", "fp8"):
         mod = importlib.import_module("vaeunet_amd." + m)

@@ -11,6 +11,7 @@
 #   flag:<module.NAME>[:<model>]  A/B of an engine flag (0 vs 1) on the current tree
 #   prof[:<model>]         rocprofv3 --kernel-trace --stats of a short bench -> <model>_kernel_stats.csv
 #   evidence               tools/gpu_evidence.sh (both benches profiled + PMC traffic + tables)
+#   sq[:<model>]           tools/gpu_sq_timing.sh (SQ wave-cycle / MFMA-busy counters per kernel)
 #   conv[:<args>]          tools/conv_bench.py with the given args (spaces as '+')
 #   enc[:<args>]           tools/enc_bench.py with the given args (spaces as '+')
 #   py:<script>[:<args>]   any python tool under tools/ (args: spaces as '+')
@@ -70,6 +71,9 @@ for step in "$@"; do
       echo "prof $m done" ;;
     evidence)
       bash tools/gpu_evidence.sh $tag || exit 1 ;;
+    sq)
+      bash tools/gpu_sq_timing.sh $tag ${arg:-unet} > $O/sq_${arg:-unet}.out 2>&1 || { echo "SQ_FAIL"; tail -5 $O/sq_${arg:-unet}.out; exit 1; }
+      echo "sq ${arg:-unet} done" ;;
     conv)
       timeout -k 10 400 python -u tools/conv_bench.py ${arg//+/ } > $O/conv_$n.log 2>&1 \
         || { echo "CONV_FAIL"; tail -10 $O/conv_$n.log; exit 1; }

@@ -372,7 +372,7 @@ int cu_count6() {
   return n;
 }
 
-int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 2 tiles per CU), k >= 2 on with the grid capped at k
+int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 1 tile per CU), k >= 2 on with the grid capped at k
 
 }  // namespace
 
