@@ -234,6 +234,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 /*   VU_TUNE_W2_BIG: 1 = 256 x 256 output tiles for the 1x1 / ConvT weight
  *     gradients with both dimensions >= 256 (0 = 128 x 256) */
 #define VU_TUNE_W2_BIG 28
+/*   VU_TUNE_V6_XM: experiment modes of the resident-weight 64 -> 64 kernel
+ *     (0 default; 1 = s_setprio around each tap's MFMAs). */
+#define VU_TUNE_V6_XM 29
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was
@@ -756,7 +759,7 @@ typedef struct VuZbJob {
 } VuZbJob;
 /* 1 when the shortcut serves N samples, L latent channels and co conv1 outputs */
 int vu_zbias_supported(int N, int L, int co);
-int64_t vu_zbias_rs_floats(int N, int co);
+int64_t vu_zbias_rs_floats(int N, int co, int H, int W);
 /* the [N][9][co] tables of every job (one launch) */
 int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream);
 /* region sums of every job's dy, then dW's z columns and the dc partials

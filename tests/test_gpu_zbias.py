@@ -107,7 +107,7 @@ def test_zbias_forward_matches_concat_conv(case):
 
 
 @pytest.mark.parametrize("mode", ["bf16", "f32"])
-@pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96)])
+@pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96), (2, 16, 48, 72, 64)])
 @pytest.mark.parametrize("acc", [False, True])
 def test_zbias_backward_matches_map_gradient(mode, shape, acc):
     """From conv1's pre-BN gradient dy: the weight gradient's z columns
@@ -126,7 +126,7 @@ def test_zbias_backward_matches_map_gradient(mode, shape, acc):
     dw = torch.randn(co, lead + L, 3, 3, generator=g).to(DEV)
     dw0 = dw.clone()
     part = torch.full((N * 32 * L,), float("nan"), dtype=torch.float32, device=DEV)
-    rs = torch.empty(K.query("vu_zbias_rs_floats", N, co), dtype=torch.float32, device=DEV)
+    rs = torch.empty(K.query("vu_zbias_rs_floats", N, co, H, W), dtype=torch.float32, device=DEV)
     arr = (type(_job(w, lead, L, H, W, act)) * 1)()
     j = _job(w, lead, L, H, W, act)
     j.dy, j.dy_stride = dyd.data_ptr(), K.pstride(dyd)

@@ -189,7 +189,7 @@ _SIGS = {
     "vu_latent_bwd": (_i, [_p, _i, C.POINTER(VuLatentHeads), _i, _i, _p, _p]),
     "vu_latent_check_job": (_i, [_i, _i, _l, _i]),
     "vu_zbias_supported": (_i, [_i, _i, _i]),
-    "vu_zbias_rs_floats": (_l, [_i, _i]),
+    "vu_zbias_rs_floats": (_l, [_i, _i, _i, _i]),
     "vu_zbias_fwd": (_i, [_p, _i, _i, _p]),
     "vu_zbias_bwd": (_i, [_p, _i, _i, _i, _p]),
     "vu_mean_groups": (_i, [_p, _i, _l, _p, _p]),

@@ -129,7 +129,9 @@ VU_DEV void bfly16_bcast(float m, int lane, float (&out)[16]) {
 
 // RELU: the epilogue ReLU (VuGemmFwd.relu) as a separate instantiation: the
 // runtime block spilled the statistics variant (+16 % in the training step)
-template <bool STATS, bool RELU = false>
+// XM (experiment modes, VU_TUNE_V6_XM): 1 = s_setprio(1) around each tap's
+// 16 MFMAs (the two waves of a SIMD otherwise free-run in the same phase)
+template <bool STATS, bool RELU = false, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
   char* const wl = smem;
@@ -244,12 +246,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
         const int P = (2 * wid + (i >> 1) + ty) * HWD + (i & 1) * 16 + tx + l16;
         af[i] = *reinterpret_cast<const u32x4*>(hb + P * 64 + (((kg + ((P >> 1) & 2)) & 3) << 4));
       }
+      if constexpr (XM == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
                                                               __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
+      if constexpr (XM == 1) __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -372,6 +376,7 @@ int cu_count6() {
   return n;
 }
 
+int g_v6_xm = 0;  // VU_TUNE_V6_XM (experiment modes of conv3x3_c64_kernel)
 int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 1 tile per CU), k >= 2 on with the grid capped at k
 
 }  // namespace
@@ -429,14 +434,21 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
   }
   if (p.stat_sum)
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<true, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
   else
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
 int gemm_fwd_v6_tune(int key, int value) {
+  if (key == VU_TUNE_V6_XM) {
+    if (value < 0 || value > 1) return (int)hipErrorInvalidValue;
+    g_v6_xm = value;
+    return 0;
+  }
   if (key == VU_TUNE_V6) {
     g_v6 = value < 0 ? 0 : value;
     return 0;

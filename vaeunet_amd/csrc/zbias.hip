@@ -21,7 +21,7 @@
 //                   dc[n][l]              = sum_c sum_tap W[c][cz0+l][tap] R[n][c][tap]
 //                 -- dc is the pixel sum of d(map) the latent backward needs
 //                 (vu_latent_bwd_sums produced it from the map gradient).
-//                 Two launches: region partials per (sample, row band), then
+//                 Two launches: region partials per (sample, pixel chunk), then
 //                 one block per 32 output channels finishing R, writing its
 //                 dW rows and its dc partial into split `chunk` of the
 //                 consumer's part array (vu_latent_bwd sums the splits).
@@ -33,7 +33,8 @@ namespace {
 
 constexpr int ZB_MAXJ = 8;
 constexpr int ZB_SPLITS = 32;  // == latent.hip LAT_SPLITS: the part array is [N][32][L]
-constexpr int ZB_BANDS = 16;   // row bands per sample of the region pass
+constexpr int ZB_PCH = 1024;   // pixels per region-pass block (a contiguous range of rows)
+constexpr int ZB_MAXCH = 1024; // pixel chunks per sample (HW <= 1024 * 1024)
 constexpr int ZB_CW = 32;      // output channels per finish block
 constexpr int ZB_NS = 5;       // region partials: total, col 0, col W-1, row 0, row H-1
 constexpr int ZB_MAXN = 64;
@@ -86,47 +87,52 @@ __global__ __launch_bounds__(256) void zbias_fwd_kernel(const ZbJobs jobs, int n
     }
 }
 
-// ---- backward 1: region partials per (sample, row band) -----------------
-// rs[((n * ZB_BANDS + band) * ZB_NS + k) * co + c]
+// ---- backward 1: region partials per (sample, pixel chunk) ---------------
+// rs[((n * nch + chunk) * ZB_NS + k) * co + c], nch = ceil(HW / ZB_PCH); a
+// chunk is ZB_PCH consecutive pixels of one sample, 8 loads in flight per
+// thread (a row-band version with 4 loads in flight was latency-bound)
 template <typename T>
 __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int njobs, int N) {
   __shared__ float sh[ZB_NS * 2048];
   const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
-  const int lb = (int)((int64_t)blockIdx.x - J.block0);
-  const int n = lb / ZB_BANDS, band = lb - (lb / ZB_BANDS) * ZB_BANDS;
   const int H = J.H, W = J.W, C = J.co;
+  const int HW = H * W, nch = (HW + ZB_PCH - 1) / ZB_PCH;
+  const int lb = (int)((int64_t)blockIdx.x - J.block0);
+  const int n = lb / nch, chunk = lb - (lb / nch) * nch;
   const int V = C >> 3, slots = 256 / V;
   const int tid = threadIdx.x, cv = tid % V, slot = tid / V;
-  const int r0 = band * H / ZB_BANDS, r1 = (band + 1) * H / ZB_BANDS;
+  const int p0 = chunk * ZB_PCH, p1 = min(HW, p0 + ZB_PCH);
+  constexpr int U = 8;
   float s[ZB_NS][8];
 #pragma unroll
   for (int k = 0; k < ZB_NS; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[k][e] = 0.f;
   if (slot < slots) {
-    const T* base = reinterpret_cast<const T*>(J.dy) + (int64_t)n * H * W * J.dy_stride + cv * 8;
+    const T* base = reinterpret_cast<const T*>(J.dy) + (int64_t)n * HW * J.dy_stride + cv * 8;
     const FastDiv dw((uint32_t)W);
-    const int p1 = r1 * W;
-    for (int p = r0 * W + slot; p < p1; p += 4 * slots) {
-      Vec8<T> v[4];
-      int pp[4];
+    for (int p = p0 + slot; p < p1; p += U * slots) {
+      Vec8<T> v[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // 4 loads in flight, clamped (summed only when inside)
-        pp[u] = p + u * slots;
-        v[u].load(base + (int64_t)(pp[u] < p1 ? pp[u] : p1 - 1) * J.dy_stride);
+      for (int u = 0; u < U; ++u) {  // clamped loads, summed only when inside
+        const int q = p + u * slots;
+        v[u].load(base + (int64_t)(q < p1 ? q : p1 - 1) * J.dy_stride);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pp[u] >= p1) break;
-        const int y = (int)dw.div((uint32_t)pp[u]), x = pp[u] - y * W;
+      for (int u = 0; u < U; ++u) {
+        const int q = p + u * slots;
+        if (q >= p1) break;
+        const int y = (int)dw.div((uint32_t)q), x = q - y * W;
+        const float m1 = x == 0 ? 1.f : 0.f, m2 = x == W - 1 ? 1.f : 0.f;
+        const float m3 = y == 0 ? 1.f : 0.f, m4 = y == H - 1 ? 1.f : 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float d = v[u].get(e);
           s[0][e] += d;
-          if (x == 0) s[1][e] += d;
-          if (x == W - 1) s[2][e] += d;
-          if (y == 0) s[3][e] += d;
-          if (y == H - 1) s[4][e] += d;
+          s[1][e] = fmaf(m1, d, s[1][e]);
+          s[2][e] = fmaf(m2, d, s[2][e]);
+          s[3][e] = fmaf(m3, d, s[3][e]);
+          s[4][e] = fmaf(m4, d, s[4][e]);
         }
       }
     }
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int nj
     const int k = q / C, c = q - (q / C) * C;
     float t = 0.f;
     for (int r = 0; r < slots; ++r) t += sh[(k * slots + r) * C + c];
-    J.rs[(((int64_t)n * ZB_BANDS + band) * ZB_NS + k) * C + c] = t;
+    J.rs[(((int64_t)n * nch + chunk) * ZB_NS + k) * C + c] = t;
   }
 }
 
@@ -164,26 +170,43 @@ __global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int n
                          (t % 3) * J.ws_kx]
                    : 0.f;
   }
-  // R[n][c][tap] from the band partials (fixed order) and the four corners
+  // R[n][c][tap] from the chunk partials (fixed order) and the four corners:
+  // first one thread per (n, c, statistic) sums its chunk column with every
+  // load issued up front (a per-(n, c) loop over chunks and statistics was a
+  // chain of dependent round trips), the corners one thread per (n, c, corner)
   const T* dy = reinterpret_cast<const T*>(J.dy);
+  const int nch = (H * W + ZB_PCH - 1) / ZB_PCH;
+  float* S = A + N * L;                  // [N][ZB_CW][ZB_NS + 4]
+  for (int e = tid; e < N * ZB_CW * ZB_NS; e += 256) {
+    const int n = e / (ZB_CW * ZB_NS), rem = e - n * (ZB_CW * ZB_NS), c = rem / ZB_NS, k = rem - c * ZB_NS;
+    float t = 0.f;
+    if (c < cw) {
+      const float* rp = J.rs + ((int64_t)n * nch * ZB_NS + k) * C + c0 + c;
+      for (int b0 = 0; b0 < nch; b0 += 16) {   // 16 loads in flight, summed in chunk order
+        float v[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) v[b] = b0 + b < nch ? rp[(int64_t)(b0 + b) * ZB_NS * C] : 0.f;
+#pragma unroll
+        for (int b = 0; b < 16; ++b) t += v[b];
+      }
+    }
+    S[(n * ZB_CW + c) * (ZB_NS + 4) + k] = t;
+  }
+  for (int e = tid; e < N * ZB_CW * 4; e += 256) {
+    const int n = e / (ZB_CW * 4), rem = e - n * (ZB_CW * 4), c = rem / 4, k = rem - c * 4;
+    float v = 0.f;
+    if (c < cw) {
+      const int y = (k >> 1) ? H - 1 : 0, x = (k & 1) ? W - 1 : 0;
+      v = ld1<T>(dy + ((int64_t)n * H * W + (int64_t)y * W + x) * J.dy_stride + c0 + c);
+    }
+    S[(n * ZB_CW + c) * (ZB_NS + 4) + ZB_NS + k] = v;
+  }
+  __syncthreads();
   for (int e = tid; e < N * ZB_CW; e += 256) {
     const int n = e / ZB_CW, c = e - n * ZB_CW;
-    float tot = 0.f, col0 = 0.f, colL = 0.f, row0 = 0.f, rowL = 0.f, k00 = 0.f, k0L = 0.f, kL0 = 0.f, kLL = 0.f;
-    if (c < cw) {
-      const float* rp = J.rs + (int64_t)n * ZB_BANDS * ZB_NS * C + c0 + c;
-      for (int b = 0; b < ZB_BANDS; ++b) {
-        tot += rp[(b * ZB_NS + 0) * C];
-        col0 += rp[(b * ZB_NS + 1) * C];
-        colL += rp[(b * ZB_NS + 2) * C];
-        row0 += rp[(b * ZB_NS + 3) * C];
-        rowL += rp[(b * ZB_NS + 4) * C];
-      }
-      const T* d = dy + (int64_t)n * H * W * J.dy_stride + c0 + c;
-      k00 = ld1<T>(d);
-      k0L = ld1<T>(d + (int64_t)(W - 1) * J.dy_stride);
-      kL0 = ld1<T>(d + (int64_t)(H - 1) * W * J.dy_stride);
-      kLL = ld1<T>(d + ((int64_t)(H - 1) * W + W - 1) * J.dy_stride);
-    }
+    const float* q = S + (n * ZB_CW + c) * (ZB_NS + 4);
+    const float tot = q[0], col0 = q[1], colL = q[2], row0 = q[3], rowL = q[4];
+    const float k00 = q[5], k0L = q[6], kL0 = q[7], kLL = q[8];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -236,7 +259,9 @@ __global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int n
 #define DISPATCH_T(dtype, ...) \
   if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
 
-size_t bwd_lds_bytes(int N, int L) { return (size_t)(N * ZB_CW * 9 + ZB_CW * L * 9 + N * L) * sizeof(float); }
+size_t bwd_lds_bytes(int N, int L) {
+  return (size_t)(N * ZB_CW * 9 + ZB_CW * L * 9 + N * L + N * ZB_CW * (ZB_NS + 4)) * sizeof(float);
+}
 
 int pack(const VuZbJob* jobs, int njobs, ZbJobs& J) {
   if (njobs < 1 || njobs > ZB_MAXJ) return (int)hipErrorInvalidValue;
@@ -252,7 +277,9 @@ extern "C" int vu_zbias_supported(int N, int L, int co) {
   return bwd_lds_bytes(N, L) <= 160 * 1024 ? 1 : 0;
 }
 
-extern "C" int64_t vu_zbias_rs_floats(int N, int co) { return (int64_t)N * ZB_BANDS * ZB_NS * co; }
+extern "C" int64_t vu_zbias_rs_floats(int N, int co, int H, int W) {
+  return (int64_t)N * (((int64_t)H * W + ZB_PCH - 1) / ZB_PCH) * ZB_NS * co;
+}
 
 extern "C" int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream) {
   ZbJobs J;
@@ -278,9 +305,9 @@ extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, vo
     if (!vu_zbias_supported(N, q.L, q.co) || !q.w || !q.act || !q.dy || !q.rs || !q.part ||
         q.H < 2 || q.W < 2 || q.dy_stride % 8)
       return (int)hipErrorInvalidValue;
-    if ((int64_t)q.H * q.W >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+    if ((int64_t)q.H * q.W > (int64_t)ZB_MAXCH * ZB_PCH) return (int)hipErrorInvalidValue;
     q.block0 = rblocks;
-    rblocks += (int64_t)N * ZB_BANDS;
+    rblocks += (int64_t)N * ((q.H * q.W + ZB_PCH - 1) / ZB_PCH);
     maxL = q.L > maxL ? q.L : maxL;
   }
   hipStream_t st = (hipStream_t)stream;

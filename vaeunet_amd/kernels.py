@@ -256,6 +256,30 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
 SPLIT_PIX = 4096
 SPLIT_MAX = 1024
 WGRAD_SPLIT_CAP = 0   # A/B runs (tools/enc_bench.py --wsplit): cap on the split-K ways, 0 = none
+# Round 5: the halo weight gradient's split count from a time model that
+# prices the fp32 slabs (the fill-whole-waves rule gave e.g. the UNetResNet
+# 128^2 decoder conv1 256 splits = 377 MB of slabs written and re-read).
+WGRAD_SLAB_MODEL = True
+_W3_BLOCK_US = 3.0       # per-block fixed cost (first tile latency, slab write issue)
+_W3_CU_FLOPS = 4.5e12    # per-block (one CU) weight-gradient rate, measured 4.1-5.2 TFLOP/s
+_W3_SLAB_BPS = 5.0e12    # slab write + re-read (8 B per element and split) through L2 / MALL
+
+
+def _halo_splits(M, ni, nj, tiles, slots, smax, gran):
+    """argmin over s of waves(s) * (c0 + 2 (M / s) BI BJ / R) + s ni nj 8 / Bw
+    (ties: fewer splits); the per-block term uses the tile's share of ni*nj."""
+    per_tile = 2.0 * ni * nj / max(tiles, 1)
+    best = None
+    for s in range(1, smax + 1):
+        waves = -(-tiles * s // slots)
+        if waves > 16:
+            break
+        rows = -(-M // s)
+        rows = -(-rows // gran) * gran
+        t = waves * (_W3_BLOCK_US * 1e-6 + per_tile * rows / _W3_CU_FLOPS) + s * ni * nj * 8.0 / _W3_SLAB_BPS
+        if best is None or t < best[0] - 1e-12:
+            best = (t, s)
+    return best[1]
 
 
 def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
@@ -283,6 +307,8 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
         if eff > best[0] + 1e-9:
             best = (eff, s)
     splits = best[1]
+    if kind == 3 and WGRAD_SLAB_MODEL:
+        splits = _halo_splits(M, ni, nj, tiles, slots, smax, gran)
     if WGRAD_SPLIT_CAP > 0:
         splits = min(splits, WGRAD_SPLIT_CAP)
     # v2 (1x1 / ConvT): very long pixel ranges per block (> SPLIT_PIX) expose

@@ -623,7 +623,7 @@ def zbias_backward(M, zscs, parts):
     for i, z in enumerate(zscs):
         conv1 = z.blk.conv1[0]
         g, acc = z.sink
-        rs = torch.empty(K.query("vu_zbias_rs_floats", N, conv1.out_channels), dtype=torch.float32,
+        rs = torch.empty(K.query("vu_zbias_rs_floats", N, conv1.out_channels, z.H, z.W), dtype=torch.float32,
                          device=z.table.device)
         keep.append(rs)
         arr[i].dy, arr[i].dy_stride = z.dy.data_ptr(), K.pstride(z.dy)
