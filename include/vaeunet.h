@@ -237,6 +237,11 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
 /*   VU_TUNE_V6_XM: experiment modes of the resident-weight 64 -> 64 kernel
  *     (0 default; 1 = s_setprio around each tap's MFMAs). */
 #define VU_TUNE_V6_XM 29
+/*   VU_TUNE_PP_PERSIST: 1 = the ping-pong kernel's 128/256-column tiles as a
+ *     persistent walk (one block per CU; the next tile's first halo and
+ *     weights stream in during the current tile's epilogue), 0 (default) =
+ *     one tile per block. */
+#define VU_TUNE_PP_PERSIST 30
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was

@@ -236,6 +236,22 @@ def test_conv3x3_pingpong_kernel(case):
 
 
 TUNE_PP_FULL = 27
+TUNE_PP_PERSIST = 30
+
+
+@pytest.mark.parametrize("case", [c for c in V4_CASES if c[4] % 128 == 0])
+@pytest.mark.parametrize("grid", [2, 3])
+def test_conv3x3_pingpong_persistent(case, grid):
+    """The persistent ping-pong walk (VU_TUNE_PP_PERSIST, round 5): a grid of
+    2 or 3 blocks walking every tile (the next tile's first halo / weights
+    issued during the epilogue) gives the per-element-bounded forward, the
+    statistics, bias + accumulate into a channel slice and the input
+    gradient, as the one-tile-per-block launch does (grid: blocks walking)."""
+    _tune((TUNE_V4_MIN_BLOCKS, 0), (TUNE_V4_SPLITK, 0), (TUNE_PP_PERSIST, grid))
+    try:
+        _check_halo_conv(case, (128,))
+    finally:
+        _tune(*TUNE_DEFAULTS, (TUNE_PP_PERSIST, 0))
 
 
 @pytest.mark.parametrize("case", [c for c in V4_CASES if c[4] % 128 == 0])

@@ -33,8 +33,13 @@ def oracle(x, t, eps, state, autocast):
         loss = R.combined_loss(lg, t) + 1e-3 * R.kl_with_free_bits(mu, lv, 1e-3)
     loss.backward()
     dz = {k: v[1].grad.detach().float() for k, v in R.PROBE.items() if not k.startswith("gate:")}
+    xh = {k: v[0].detach().float() for k, v in R.PROBE.items() if not k.startswith("gate:") and k in FOCUS}
     R.PROBE = None
-    return dz, {k: v.grad.detach().double() for k, v in ref.p.items() if v.grad is not None}
+    return dz, {k: v.grad.detach().double() for k, v in ref.p.items() if v.grad is not None}, xh
+
+
+# BatchNorms whose affine-gradient drift is decomposed (dz error vs xhat error)
+FOCUS = ("encoder.bn1.", "encoder.layer1.0.bn2.", "encoder.layer1.0.bn1.", "encoder.layer2.0.bn1.")
 
 
 def main():
@@ -52,7 +57,7 @@ def main():
     model = model.cuda().to(memory_format=torch.channels_last).train()
     model.eps_override = eps.cuda()
     bn_name = {id(mod): n + "." for n, mod in model.named_modules() if isinstance(mod, torch.nn.BatchNorm2d)}
-    hip, order = {}, []
+    hip, order, hipx = {}, [], {}
     orig = E.bn_bwd
 
     def bn_bwd(dy, xx, coef, bn, relu, M, *a, **kw):
@@ -64,6 +69,9 @@ def main():
                 d = d * ((xx.float() * coef[0].view(1, C, 1, 1) + coef[1].view(1, C, 1, 1)) > 0).float()
             hip[pre] = d.cpu()
             order.append(pre)
+            if pre in FOCUS:   # HIP's xhat from its own stored BN input and statistics
+                C = xx.shape[1]
+                hipx[pre] = ((xx.float() - coef[2].view(1, C, 1, 1)) * coef[3].view(1, C, 1, 1)).cpu()
         return orig(dy, xx, coef, bn, relu, M, *a, **kw)
     E.bn_bwd = bn_bwd
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -74,9 +82,9 @@ def main():
     E.bn_bwd = orig
     params = {k: v.grad.detach().double().cpu() for k, v in model.named_parameters() if v.grad is not None}
     print("HIP done", flush=True)
-    dz32, g32 = oracle(x, m, eps, state, False)
+    dz32, g32, xh32 = oracle(x, m, eps, state, False)
     print("oracle fp32 done", flush=True)
-    dz16, g16 = oracle(x, m, eps, state, True)
+    dz16, g16, xh16 = oracle(x, m, eps, state, True)
     print("oracle CPU-bf16 done", flush=True)
     print(f"{'BatchNorm (backward order)':44s} {'dz HIP':>9s} {'dz bf16':>9s} | {'dgamma HIP':>10s} "
           f"{'CPU-bf16':>9s} | {'dbeta HIP':>9s} {'CPU-bf16':>9s}")
@@ -92,6 +100,26 @@ def main():
                       abs(float(g16[n].norm()) - float(ref.norm())) / float(ref.norm())))
         print(f"{pre:44s} {rel(hip[pre], dz32[pre]):9.2e} {rel(dz16[pre], dz32[pre]):9.2e} | "
               f"{r[0][0]:10.2e} {r[0][1]:9.2e} | {r[1][0]:9.2e} {r[1][1]:9.2e}", flush=True)
+    # decomposition of the dgamma = sum dz * xhat error (per channel, norm over channels)
+    print("dgamma decomposition, relative to the fp32 dgamma norm: A = HIP dz x HIP xhat, "
+          "C = HIP dz x fp32 xhat, D = fp32 dz x HIP xhat, E = bf16-ref dz x bf16-ref xhat, "
+          "F = bf16-ref dz x fp32 xhat; dbeta: HIP / bf16-ref")
+    for pre in FOCUS:
+        if pre not in hipx or pre not in xh32:
+            continue
+        d32, x32 = dz32[pre].double(), xh32[pre].double()
+        dh, xhh = hip[pre].double(), hipx[pre].double()
+        d16, x16 = dz16[pre].double(), xh16[pre].double()
+        B = (d32 * x32).sum((0, 2, 3))
+        nb = float(B.norm())
+
+        def e(a, b_):
+            return float(((a * b_).sum((0, 2, 3)) - B).norm()) / nb
+        db = d32.sum((0, 2, 3))
+        print(f"  {pre:28s} A {e(dh, xhh):.3e}  C {e(dh, x32):.3e}  D {e(d32, xhh):.3e}  E {e(d16, x16):.3e}  "
+              f"F {e(d16, x32):.3e} | dbeta {float((dh.sum((0, 2, 3)) - db).norm()) / float(db.norm()):.3e} / "
+              f"{float((d16.sum((0, 2, 3)) - db).norm()) / float(db.norm()):.3e}; xhat rel err HIP "
+              f"{rel(xhh, x32):.2e} bf16-ref {rel(x16, x32):.2e}", flush=True)
 
 
 if __name__ == "__main__":

@@ -86,7 +86,11 @@ VU_DEV float row16_sum(float v) { return ror_add<1>(ror_add<2>(ror_add<4>(ror_ad
 // registers (VU_TUNE_PP_FULL, A/B).
 // ZB: the latent-shortcut epilogue (VuGemmFwd.zbias) as its own
 // instantiation -- a runtime branch pushed the others to 256 VGPRs + scratch.
-template <int BN, bool SPLIT, bool BNB, bool RELU = false, bool FULL = false, bool ZB = false>
+// PERS (round 5, VU_TUNE_PP_PERSIST): a persistent grid (<= one block per CU)
+// walks its tiles; the next tile's first halo and first two weight slots are
+// issued before the current tile's epilogue (which stages through its own LDS
+// strips), so the per-tile prologue wait overlaps the epilogue.
+template <int BN, bool SPLIT, bool BNB, bool RELU = false, bool FULL = false, bool ZB = false, bool PERS = false>
 __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   constexpr int NBW = 3;                          // weight ring slots
   constexpr int WM = PP<BN>::WM, WN = PP<BN>::WN, TH = PP<BN>::TH, TW = PP<BN>::TW;
@@ -107,11 +111,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   // pixel rows
   constexpr int SPITCH = 144;                     // staged pixel row (128 B + pad)
   constexpr int STG = 32 * SPITCH;
-  static_assert(MAIN <= 163840 && 8 * STG <= MAIN, "LDS");
+  constexpr int SMEM = PERS ? MAIN + 8 * STG : MAIN;
+  static_assert(SMEM <= 163840 && 8 * STG <= MAIN, "LDS");
+  static_assert(!(PERS && SPLIT), "persistent walk: whole-K tiles only");
   static_assert(LB0 >= 1, "DMA schedule");
   static_assert(9 % NBW == 0, "ring slot = tap % NBW");
   static_assert(TW == 32, "fragment geometry");
-  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const VuGather& g = p.a;
   const int H = g.H, W = g.W;
@@ -124,12 +130,23 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int ksplit = SPLIT ? p.ksplit : 1;
   const int bid0 = xcd_remap(blockIdx.x, btiles * ksplit);
   const int kidx = SPLIT ? bid0 / btiles : 0;
-  const int bid = SPLIT ? bid0 - kidx * btiles : bid0;
-  const int mt = bid / ntiles, nt = bid - mt * ntiles;
-  const int img = mt / (ty_n * tx_n);
-  const int trem = mt - img * (ty_n * tx_n);
-  const int y0 = (trem / tx_n) * TH, x0 = (trem - (trem / tx_n) * tx_n) * TW;
-  const int n0 = nt * BN;
+  // the tile this block computes (mt, img, y0, x0, n0: epilogue) and the one
+  // its DMA streams (d*: the same, or -- PERS, during the epilogue -- the next)
+  int mt, img, y0, x0, n0, dimg, dy0, dx0, dn0;
+  auto tile_coords = [&](int b, int& m_, int& im_, int& y_, int& x_, int& n_) {
+    m_ = b / ntiles;
+    const int nt_ = b - m_ * ntiles;
+    im_ = m_ / (ty_n * tx_n);
+    const int tr = m_ - im_ * (ty_n * tx_n);
+    y_ = (tr / tx_n) * TH;
+    x_ = (tr - (tr / tx_n) * tx_n) * TW;
+    n_ = nt_ * BN;
+  };
+  int cur = SPLIT ? bid0 - kidx * btiles : bid0;
+  {
+    int mdum;
+    tile_coords(cur, mdum, dimg, dy0, dx0, dn0);
+  }
   // this block's contiguous range of 32-channel chunks
   const int call = g.C / 32;
   const int cbeg = SPLIT ? kidx * call / ksplit : 0, cend = SPLIT ? (kidx + 1) * call / ksplit : call;
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   // recomputed per chunk (a per-slot register array would stay live through
   // the MFMA loop: 19 registers at BN = 64)
   auto halo_chunk = [&](int c, int buf) {
-    int ib = img, yb = y0, xb = x0;
+    int ib = dimg, yb = dy0, xb = dx0;
     asm volatile("" : "+s"(ib), "+s"(yb), "+s"(xb));  // keep the slot math inside the loop
     const int cb = c * 32;
     const bf16_t* src;
@@ -202,7 +219,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       if (i < i0 || i >= i1) continue;
       const int P = i * 256 + gt;
       const int row = P >> 2;
-      const void* gp = (const void*)(bmat + (int64_t)(n0 + row) * p.ldb + k0 + (P & 3) * 8);
+      const void* gp = (const void*)(bmat + (int64_t)(dn0 + row) * p.ldb + k0 + (P & 3) * 8);
       __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * 256 + gw * 64) * 16), 16, 0, 0);
     }
   };
@@ -216,12 +233,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   const int brow = (wn * 64 + (lane & 15)) * 64 + (lane >> 4) * 16;
   const int cbase = wn * 64 + 4 * (lane >> 4);
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
-
   // ---- prologue: halo of chunk 0, weights of steps 0 and 1 -----------------
   if (grp) {
     halo_chunk(cbeg, 0);
@@ -229,6 +240,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     wstage(cbeg, 0, 0, 0, LB0);
     wstage(cbeg, 1, 1, 0, LB0);
   }
+  int kt = 0;  // PERS: tiles walked
+  for (;;) {
+  tile_coords(cur, mt, img, y0, x0, n0);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
   if (grp) pp_barrier();  // the stagger: half 1 runs one barrier behind
@@ -329,6 +348,25 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
     hb ^= 1;
   }
   if (!grp) pp_barrier();  // re-align the halves
+  // PERS: every wave is past its last fragment read -- the next tile's first
+  // halo (buffer 0) and weight slots 0, 1 stream in during this epilogue
+  bool more = false;
+  if constexpr (PERS) {
+    ++kt;
+    const int vb = (int)blockIdx.x + kt * (int)gridDim.x;
+    more = vb < btiles;
+    if (more) {
+      cur = xcd_remap(vb, btiles);
+      int mdum;
+      tile_coords(cur, mdum, dimg, dy0, dx0, dn0);
+      if (grp) {
+        halo_chunk(cbeg, 0);
+      } else {
+        wstage(cbeg, 0, 0, 0, LB0);
+        wstage(cbeg, 1, 1, 0, LB0);
+      }
+    }
+  }
 
   // ---- epilogue -------------------------------------------------------------
   // acc[i][j][r]: pixel wm*128 + i*16 + (lane&15), channel n0 + cbase + j*16 + r
@@ -467,13 +505,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
   // vmcnt(0), i.e. for the acknowledgement of the statistics stores just
   // issued (measured: the 17 forward layers 2.65 ms with statistics against
   // 2.44 ms without)
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  pp_barrier();
+  if constexpr (!PERS) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+  }
   // fragments 2h and 2h+1 are the 32 pixels of tile row wm*4 + h
   bf16_t* const orow0 = reinterpret_cast<bf16_t*>(ep->out) + ep->out_coff + n0 + wn * 64 +
                         (((int64_t)img * H + y0 + wm * 4) * W + x0) * ep->out_stride;
   const int64_t orow_y = (int64_t)W * ep->out_stride;
-  char* const stg = smem + wid * STG;
+  char* const stg = smem + (PERS ? MAIN : 0) + wid * STG;
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
 #pragma unroll
@@ -552,6 +592,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_pp_kernel(VuGemmFwd p) {
       *reinterpret_cast<f32x4*>(pr + ep->ncol + 4) = f32x4{bs1[4], bs1[5], bs1[6], bs1[7]};
     }
   }
+  if (!more) break;
+  }  // tile walk (one pass unless PERS)
 }
 
 // split-K epilogue: out = round(sum_k slab[k] + bias) (+ out if accumulate),
@@ -753,6 +795,8 @@ bool tiles_ok(const VuGemmFwd& p) {
 int g_min_blocks = 256;  // vu_gemm_set_tuning(VU_TUNE_V4_MIN_BLOCKS, ...)
 int g_splitk = 1;        // vu_gemm_set_tuning(VU_TUNE_V4_SPLITK, ...): 0 off, 1 auto, k >= 2 forced
 int g_pp_full = 1;       // VU_TUNE_PP_FULL: one phase per step (conv3x3_pp_kernel FULL; 0 = two halves)
+int g_pp_persist = 0;    // VU_TUNE_PP_PERSIST: persistent tile walk for 128/256-column tiles (PERS);
+                         // 1 = grids over one block per CU, k >= 2 = always, grid capped at k (tests)
 
 // Output-column tile the ping-pong kernel uses for this problem (0 = not served).
 int pick_bn(const VuGemmFwd& p) {
@@ -784,6 +828,7 @@ int g_split_min_chunks = 2;  // vu_gemm_set_tuning(VU_TUNE_V4_SPLIT_CHUNKS, ...)
 }  // namespace
 int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype);  // gemm_fwd2.hip
 int gemm_fwd_v7_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd7.hip
+int cu_count6();                                        // gemm_fwd6.hip
 namespace {
 
 template <int BN>
@@ -847,6 +892,12 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     else if (p.relu)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+    else if (BN != 64 && g_pp_full && (g_pp_persist >= 2 || (g_pp_persist == 1 && tiles > cu_count6()))) {
+      // persistent walk: one block per CU (g_pp_persist >= 2: the grid capped at that many blocks, tests)
+      const int64_t grid = g_pp_persist >= 2 ? (tiles < g_pp_persist ? tiles : g_pp_persist) : cu_count6();
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64, false, BN != 64>),
+                         dim3((unsigned)grid), dim3(512), 0, st, q);
+    }
     else if (BN != 64 && g_pp_full)  // (BN = 64 spills with the extra fragments)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64>), dim3((unsigned)tiles), dim3(512), 0,
                          st, q);
@@ -952,6 +1003,10 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
   }
   if (key == VU_TUNE_PP_FULL) {
     g_pp_full = value;
+    return 0;
+  }
+  if (key == VU_TUNE_PP_PERSIST) {
+    g_pp_persist = value;
     return 0;
   }
   if (key == VU_TUNE_V4_SPLIT_CHUNKS) {
