@@ -828,7 +828,15 @@ int g_split_min_chunks = 2;  // vu_gemm_set_tuning(VU_TUNE_V4_SPLIT_CHUNKS, ...)
 }  // namespace
 int gemm_fwd_v2_small(const VuGemmFwd& p, int dtype);  // gemm_fwd2.hip
 int gemm_fwd_v7_bm(const VuGemmFwd& p, int dtype);     // gemm_fwd7.hip
-int cu_count6();                                        // gemm_fwd6.hip
+int cu_count4() {  // compute units of the current device (persistent grid)
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
 namespace {
 
 template <int BN>
@@ -892,9 +900,9 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     else if (p.relu)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
-    else if (BN != 64 && g_pp_full && (g_pp_persist >= 2 || (g_pp_persist == 1 && tiles > cu_count6()))) {
+    else if (BN != 64 && g_pp_full && (g_pp_persist >= 2 || (g_pp_persist == 1 && tiles > cu_count4()))) {
       // persistent walk: one block per CU (g_pp_persist >= 2: the grid capped at that many blocks, tests)
-      const int64_t grid = g_pp_persist >= 2 ? (tiles < g_pp_persist ? tiles : g_pp_persist) : cu_count6();
+      const int64_t grid = g_pp_persist >= 2 ? (tiles < g_pp_persist ? tiles : g_pp_persist) : cu_count4();
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64, false, BN != 64>),
                          dim3((unsigned)grid), dim3(512), 0, st, q);
     }
