@@ -29,11 +29,17 @@ for step in "$@"; do
   arg=""; [[ "$step" == *:* ]] && arg=${step#*:}
   case $kind in
     tests)
-      sel="tests"
-      if [ -n "$arg" ]; then
-        if [[ "$arg" == tests/* ]]; then sel=${arg//,/ }; else sel="tests -k ${arg//,/ or }"; fi
+      # comma list: items under tests/ are files, the others -k name fragments (OR-ed)
+      files=""; keys=""
+      IFS=',' read -ra items <<< "$arg"
+      for it in "${items[@]}"; do
+        if [[ "$it" == tests/* ]]; then files="$files $it"; else keys="${keys:+$keys or }$it"; fi
+      done
+      sel="${files:-tests}"
+      if [ -n "$keys" ]; then
+        if [ -n "$files" ]; then sel="tests"; keys="$keys or $(for f in $files; do basename $f .py; done | paste -sd' ' | sed 's/ / or /g')"; fi
       fi
-      timeout -k 10 1000 python -u -m pytest $sel -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread \
+      timeout -k 10 1000 python -u -m pytest $sel ${keys:+-k "$keys"} -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread \
         > $O/tests_$n.log 2>&1 || { echo "TESTS_FAIL ($step)"; tail -40 $O/tests_$n.log; exit 1; }
       tail -1 $O/tests_$n.log ;;
     bench)

@@ -21,10 +21,11 @@
 //                   dc[n][l]              = sum_c sum_tap W[c][cz0+l][tap] R[n][c][tap]
 //                 -- dc is the pixel sum of d(map) the latent backward needs
 //                 (vu_latent_bwd_sums produced it from the map gradient).
-//                 Two launches: region partials per (sample, pixel chunk), then
-//                 one block per 32 output channels finishing R, writing its
-//                 dW rows and its dc partial into split `chunk` of the
-//                 consumer's part array (vu_latent_bwd sums the splits).
+//                 Three launches: region partials per (sample, pixel chunk);
+//                 per sample, R of every channel (to the workspace); per 32
+//                 output channels, the z columns of dW and the dc partial of
+//                 those channels into split `chunk` of the consumer's part
+//                 array (vu_latent_bwd sums the splits).
 // Every sum runs in a fixed order (reproducible run to run).
 #include "common.h"
 #include "../../include/vaeunet.h"
@@ -53,38 +54,50 @@ VU_DEV int find_job(const ZbJobs& jobs, int njobs) {
 VU_DEV bool tap_in(int cr, int k) { return !((cr == 0 && k == 0) || (cr == 2 && k == 2)); }
 
 // ---- forward: the bias tables -------------------------------------------
+// one block per (job, 32 output channels): that chunk's z weights [32][L][9]
+// and the vectors [N][L] staged in LDS (every global load issued up front),
+// then thread (n, c) forms its 9 tap sums and the 9 border-class rows
 __global__ __launch_bounds__(256) void zbias_fwd_kernel(const ZbJobs jobs, int njobs, int N) {
+  extern __shared__ float zsm[];
   const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
-  const int e = (int)((int64_t)blockIdx.x - J.block0) * 256 + threadIdx.x;
-  if (e >= N * J.co) return;
-  const int n = e / J.co, c = e - n * J.co;
-  float S[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) S[t] = 0.f;
-  const float* a = J.act + (int64_t)n * J.L;
-  const float* wr = J.w + (int64_t)c * J.ws_co + (int64_t)J.cz0 * J.ws_ci;
-  for (int l = 0; l < J.L; ++l) {
-    const float av = a[l];
-    const float* w = wr + (int64_t)l * J.ws_ci;
-    float wv[9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) wv[t] = w[(t / 3) * J.ws_ky + (t % 3) * J.ws_kx];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) S[t] += wv[t] * av;
+  const int chunk = (int)((int64_t)blockIdx.x - J.block0);
+  const int c0 = chunk * ZB_CW, cw = J.co - c0 < ZB_CW ? J.co - c0 : ZB_CW;
+  const int L = J.L, tid = threadIdx.x;
+  float* Wl = zsm;                 // [ZB_CW][L][9]
+  float* A = Wl + ZB_CW * L * 9;   // [N][L]
+  for (int e = tid; e < N * L; e += 256) A[e] = J.act[e];
+  for (int e = tid; e < ZB_CW * L * 9; e += 256) {
+    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
+    Wl[e] = c < cw ? J.w[(int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky +
+                         (t % 3) * J.ws_kx]
+                   : 0.f;
   }
-  const float sc = J.row_scale ? J.row_scale[c] : 1.f;
+  __syncthreads();
+  for (int e = tid; e < N * cw; e += 256) {
+    const int n = e / cw, c = e - n * cw;
+    float S[9];
 #pragma unroll
-  for (int cr = 0; cr < 3; ++cr)
+    for (int t = 0; t < 9; ++t) S[t] = 0.f;
+    const float* wr = Wl + c * L * 9;
+    for (int l = 0; l < L; ++l) {
+      const float av = A[n * L + l];
 #pragma unroll
-    for (int cc = 0; cc < 3; ++cc) {
-      float t = 0.f;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-          if (tap_in(cr, ky) && tap_in(cc, kx)) t += S[ky * 3 + kx];
-      J.table[((int64_t)n * 9 + cr * 3 + cc) * J.co + c] = t * sc;
+      for (int t = 0; t < 9; ++t) S[t] += wr[l * 9 + t] * av;
     }
+    const float sc = J.row_scale ? J.row_scale[c0 + c] : 1.f;
+#pragma unroll
+    for (int cr = 0; cr < 3; ++cr)
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        float t = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+            if (tap_in(cr, ky) && tap_in(cc, kx)) t += S[ky * 3 + kx];
+        J.table[((int64_t)n * 9 + cr * 3 + cc) * J.co + c0 + c] = t * sc;
+      }
+  }
 }
 
 // ---- backward 1: region partials per (sample, pixel chunk) ---------------
@@ -150,61 +163,41 @@ __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int nj
   }
 }
 
-// ---- backward 2: per 32 output channels, R -> dW rows, dc partial -------
+// ---- backward 2: per sample, R[c][tap] of every channel -> workspace ------
+// thread (c, statistic) sums its chunk column (16 loads in flight); the
+// corners are read directly
 template <typename T>
-__global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int njobs, int N) {
+__global__ __launch_bounds__(256) void zbias_r_kernel(const ZbJobs jobs, int njobs, int N) {
   extern __shared__ float zsm[];
   const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
-  const int chunk = (int)((int64_t)blockIdx.x - J.block0);
-  const int c0 = chunk * ZB_CW, cw = J.co - c0 < ZB_CW ? J.co - c0 : ZB_CW;
-  const int L = J.L, H = J.H, W = J.W, C = J.co;
-  const int nchunks = (C + ZB_CW - 1) / ZB_CW;
-  float* R = zsm;                        // [N][ZB_CW][9]
-  float* Wl = R + N * ZB_CW * 9;         // [ZB_CW][L][9]
-  float* A = Wl + ZB_CW * L * 9;         // [N][L]
-  const int tid = threadIdx.x;
-  for (int e = tid; e < N * L; e += 256) A[e] = J.act[e];
-  for (int e = tid; e < ZB_CW * L * 9; e += 256) {
-    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
-    Wl[e] = c < cw ? J.w[(int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky +
-                         (t % 3) * J.ws_kx]
-                   : 0.f;
-  }
-  // R[n][c][tap] from the chunk partials (fixed order) and the four corners:
-  // first one thread per (n, c, statistic) sums its chunk column with every
-  // load issued up front (a per-(n, c) loop over chunks and statistics was a
-  // chain of dependent round trips), the corners one thread per (n, c, corner)
-  const T* dy = reinterpret_cast<const T*>(J.dy);
+  const int n = (int)((int64_t)blockIdx.x - J.block0);
+  const int H = J.H, W = J.W, C = J.co, tid = threadIdx.x;
   const int nch = (H * W + ZB_PCH - 1) / ZB_PCH;
-  float* S = A + N * L;                  // [N][ZB_CW][ZB_NS + 4]
-  for (int e = tid; e < N * ZB_CW * ZB_NS; e += 256) {
-    const int n = e / (ZB_CW * ZB_NS), rem = e - n * (ZB_CW * ZB_NS), c = rem / ZB_NS, k = rem - c * ZB_NS;
+  float* S = zsm;                  // [C][ZB_NS + 4]
+  const float* rsn = J.rs + (int64_t)n * nch * ZB_NS * C;
+  for (int e = tid; e < C * ZB_NS; e += 256) {
+    const int c = e / ZB_NS, k = e - (e / ZB_NS) * ZB_NS;
+    const float* rp = rsn + (int64_t)k * C + c;
     float t = 0.f;
-    if (c < cw) {
-      const float* rp = J.rs + ((int64_t)n * nch * ZB_NS + k) * C + c0 + c;
-      for (int b0 = 0; b0 < nch; b0 += 16) {   // 16 loads in flight, summed in chunk order
-        float v[16];
+    for (int b0 = 0; b0 < nch; b0 += 16) {
+      float v[16];
 #pragma unroll
-        for (int b = 0; b < 16; ++b) v[b] = b0 + b < nch ? rp[(int64_t)(b0 + b) * ZB_NS * C] : 0.f;
+      for (int b = 0; b < 16; ++b) v[b] = b0 + b < nch ? rp[(int64_t)(b0 + b) * ZB_NS * C] : 0.f;
 #pragma unroll
-        for (int b = 0; b < 16; ++b) t += v[b];
-      }
+      for (int b = 0; b < 16; ++b) t += v[b];
     }
-    S[(n * ZB_CW + c) * (ZB_NS + 4) + k] = t;
+    S[c * (ZB_NS + 4) + k] = t;
   }
-  for (int e = tid; e < N * ZB_CW * 4; e += 256) {
-    const int n = e / (ZB_CW * 4), rem = e - n * (ZB_CW * 4), c = rem / 4, k = rem - c * 4;
-    float v = 0.f;
-    if (c < cw) {
-      const int y = (k >> 1) ? H - 1 : 0, x = (k & 1) ? W - 1 : 0;
-      v = ld1<T>(dy + ((int64_t)n * H * W + (int64_t)y * W + x) * J.dy_stride + c0 + c);
-    }
-    S[(n * ZB_CW + c) * (ZB_NS + 4) + ZB_NS + k] = v;
+  const T* dy = reinterpret_cast<const T*>(J.dy);
+  for (int e = tid; e < C * 4; e += 256) {
+    const int c = e >> 2, k = e & 3;
+    const int y = (k >> 1) ? H - 1 : 0, x = (k & 1) ? W - 1 : 0;
+    S[c * (ZB_NS + 4) + ZB_NS + k] = ld1<T>(dy + ((int64_t)n * H * W + (int64_t)y * W + x) * J.dy_stride + c);
   }
   __syncthreads();
-  for (int e = tid; e < N * ZB_CW; e += 256) {
-    const int n = e / ZB_CW, c = e - n * ZB_CW;
-    const float* q = S + (n * ZB_CW + c) * (ZB_NS + 4);
+  float* Rg = J.rs + (int64_t)N * nch * ZB_NS * C + (int64_t)n * C * 9;
+  for (int c = tid; c < C; c += 256) {
+    const float* q = S + c * (ZB_NS + 4);
     const float tot = q[0], col0 = q[1], colL = q[2], row0 = q[3], rowL = q[4];
     const float k00 = q[5], k0L = q[6], kL0 = q[7], kLL = q[8];
 #pragma unroll
@@ -220,11 +213,40 @@ __global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int n
         if (ky == 0 && kx == 2) r += k0L;
         if (ky == 2 && kx == 0) r += kL0;
         if (ky == 2 && kx == 2) r += kLL;
-        R[(n * ZB_CW + c) * 9 + ky * 3 + kx] = r;
+        Rg[c * 9 + ky * 3 + kx] = r;
       }
   }
+}
+
+// ---- backward 3: per 32 output channels: the z columns of dW and the dc
+// partial of these channels (into split `chunk` of part; chunk 0 also zeroes
+// the splits no chunk uses), from R, the z weights and the vectors in LDS
+//   dW[c0 + c][cz0 + l][tap] (+)= sum_n act[n][l] R[n][c][tap]
+//   dc_chunk[n][l]              = sum_{c, tap} W[c0 + c][cz0 + l][tap] R[n][c][tap]
+__global__ __launch_bounds__(256) void zbias_dw_kernel(const ZbJobs jobs, int njobs, int N) {
+  extern __shared__ float zsm[];
+  const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
+  const int chunk = (int)((int64_t)blockIdx.x - J.block0);
+  const int c0 = chunk * ZB_CW, cw = J.co - c0 < ZB_CW ? J.co - c0 : ZB_CW;
+  const int L = J.L, C = J.co, tid = threadIdx.x;
+  const int nch = (J.H * J.W + ZB_PCH - 1) / ZB_PCH;
+  const int nchunks = (C + ZB_CW - 1) / ZB_CW;
+  float* R = zsm;                  // [N][ZB_CW][9]
+  float* A = R + N * ZB_CW * 9;    // [N][L]
+  float* Wl = A + N * L;           // [ZB_CW][L][9]
+  const float* Rg = J.rs + (int64_t)N * nch * ZB_NS * C;
+  for (int e = tid; e < N * L; e += 256) A[e] = J.act[e];
+  for (int e = tid; e < ZB_CW * L * 9; e += 256) {
+    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
+    Wl[e] = c < cw ? J.w[(int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky +
+                         (t % 3) * J.ws_kx]
+                   : 0.f;
+  }
+  for (int e = tid; e < N * ZB_CW * 9; e += 256) {
+    const int n = e / (ZB_CW * 9), rem = e - n * (ZB_CW * 9), c = rem / 9, t = rem - c * 9;
+    R[e] = c < cw ? Rg[((int64_t)n * C + c0 + c) * 9 + t] : 0.f;
+  }
   __syncthreads();
-  // dW[c0 + c][cz0 + l][tap] (+)= sum_n act[n][l] R[n][c][tap]  (dw NULL: conv1 frozen)
   for (int e = tid; J.dw && e < cw * L; e += 256) {
     const int c = e / L, l = e - (e / L) * L;
     float s[9];
@@ -236,20 +258,21 @@ __global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int n
       for (int t = 0; t < 9; ++t) s[t] += a * R[(n * ZB_CW + c) * 9 + t];
     }
     float* d = J.dw + (int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci;
+    float old[9];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      float* p = d + (t / 3) * J.ws_ky + (t % 3) * J.ws_kx;
-      *p = J.grad_acc ? *p + s[t] : s[t];
-    }
+    for (int t = 0; t < 9; ++t) old[t] = J.grad_acc ? d[(t / 3) * J.ws_ky + (t % 3) * J.ws_kx] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) d[(t / 3) * J.ws_ky + (t % 3) * J.ws_kx] = J.grad_acc ? old[t] + s[t] : s[t];
   }
-  // dc partial of this chunk -> split `chunk` of part[n][split][l]; chunk 0
-  // also zeroes the splits no chunk uses
   for (int e = tid; e < N * L; e += 256) {
     const int n = e / L, l = e - (e / L) * L;
     float s = 0.f;
-    for (int c = 0; c < cw; ++c)
+    for (int c = 0; c < cw; ++c) {
+      const float* w = Wl + (c * L + l) * 9;
+      const float* r = R + (n * ZB_CW + c) * 9;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) s += Wl[(c * L + l) * 9 + t] * R[(n * ZB_CW + c) * 9 + t];
+      for (int t = 0; t < 9; ++t) s += w[t] * r[t];
+    }
     J.part[((int64_t)n * ZB_SPLITS + chunk) * L + l] = s;
     if (chunk == 0)
       for (int sp = nchunks; sp < ZB_SPLITS; ++sp) J.part[((int64_t)n * ZB_SPLITS + sp) * L + l] = 0.f;
@@ -259,9 +282,9 @@ __global__ __launch_bounds__(256) void zbias_bwd_kernel(const ZbJobs jobs, int n
 #define DISPATCH_T(dtype, ...) \
   if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
 
-size_t bwd_lds_bytes(int N, int L) {
-  return (size_t)(N * ZB_CW * 9 + ZB_CW * L * 9 + N * L + N * ZB_CW * (ZB_NS + 4)) * sizeof(float);
-}
+size_t fwd_lds_bytes(int N, int L) { return (size_t)(ZB_CW * L * 9 + N * L) * sizeof(float); }
+size_t r_lds_bytes(int C) { return (size_t)(C * (ZB_NS + 4)) * sizeof(float); }
+size_t dw_lds_bytes(int N, int L) { return (size_t)(N * ZB_CW * 9 + N * L + ZB_CW * L * 9) * sizeof(float); }
 
 int pack(const VuZbJob* jobs, int njobs, ZbJobs& J) {
   if (njobs < 1 || njobs > ZB_MAXJ) return (int)hipErrorInvalidValue;
@@ -273,25 +296,30 @@ int pack(const VuZbJob* jobs, int njobs, ZbJobs& J) {
 
 extern "C" int vu_zbias_supported(int N, int L, int co) {
   if (N < 1 || N > ZB_MAXN || L < 1 || L > 64 || co < 8 || co % 8 || co / 8 > 256) return 0;
-  if ((co + ZB_CW - 1) / ZB_CW > ZB_SPLITS) return 0;
-  return bwd_lds_bytes(N, L) <= 160 * 1024 ? 1 : 0;
+  const size_t cap = 160 * 1024;
+  if ((co + ZB_CW - 1) / ZB_CW > ZB_SPLITS) return 0;  // dc partials: one split per 32 channels
+  return fwd_lds_bytes(N, L) <= cap && r_lds_bytes(co) <= cap && dw_lds_bytes(N, L) <= cap ? 1 : 0;
 }
 
+// region partials [N][nch][5][co], then R [N][co][9]
 extern "C" int64_t vu_zbias_rs_floats(int N, int co, int H, int W) {
-  return (int64_t)N * (((int64_t)H * W + ZB_PCH - 1) / ZB_PCH) * ZB_NS * co;
+  return (int64_t)N * (((int64_t)H * W + ZB_PCH - 1) / ZB_PCH) * ZB_NS * co + (int64_t)N * co * 9;
 }
 
 extern "C" int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream) {
   ZbJobs J;
   if (int rc = pack(jobs, njobs, J)) return rc;
   int64_t blocks = 0;
+  int maxL = 1;
   for (int j = 0; j < njobs; ++j) {
     VuZbJob& q = J.j[j];
     if (!vu_zbias_supported(N, q.L, q.co) || !q.w || !q.act || !q.table) return (int)hipErrorInvalidValue;
     q.block0 = blocks;
-    blocks += ((int64_t)N * q.co + 255) / 256;
+    blocks += (q.co + ZB_CW - 1) / ZB_CW;
+    maxL = q.L > maxL ? q.L : maxL;
   }
-  hipLaunchKernelGGL(zbias_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J, njobs, N);
+  hipLaunchKernelGGL(zbias_fwd_kernel, dim3((unsigned)blocks), dim3(256), fwd_lds_bytes(N, maxL),
+                     (hipStream_t)stream, J, njobs, N);
   return (int)hipGetLastError();
 }
 
@@ -299,7 +327,7 @@ extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, vo
   ZbJobs J;
   if (int rc = pack(jobs, njobs, J)) return rc;
   int64_t rblocks = 0;
-  int maxL = 1;
+  int maxL = 1, maxC = 8;
   for (int j = 0; j < njobs; ++j) {
     VuZbJob& q = J.j[j];
     if (!vu_zbias_supported(N, q.L, q.co) || !q.w || !q.act || !q.dy || !q.rs || !q.part ||
@@ -309,19 +337,22 @@ extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, vo
     q.block0 = rblocks;
     rblocks += (int64_t)N * ((q.H * q.W + ZB_PCH - 1) / ZB_PCH);
     maxL = q.L > maxL ? q.L : maxL;
+    maxC = q.co > maxC ? q.co : maxC;
   }
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL((zbias_rs_kernel<T>), dim3((unsigned)rblocks), dim3(256), 0, st, J, njobs, N);
   })
-  int64_t fblocks = 0;
-  for (int j = 0; j < njobs; ++j) {
-    J.j[j].block0 = fblocks;
-    fblocks += (J.j[j].co + ZB_CW - 1) / ZB_CW;
-  }
-  const size_t lds = bwd_lds_bytes(N, maxL);
+  for (int j = 0; j < njobs; ++j) J.j[j].block0 = (int64_t)j * N;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((zbias_bwd_kernel<T>), dim3((unsigned)fblocks), dim3(256), lds, st, J, njobs, N);
+    hipLaunchKernelGGL((zbias_r_kernel<T>), dim3((unsigned)(njobs * N)), dim3(256), r_lds_bytes(maxC), st, J,
+                       njobs, N);
   })
+  int64_t dblocks = 0;
+  for (int j = 0; j < njobs; ++j) {
+    J.j[j].block0 = dblocks;
+    dblocks += (J.j[j].co + ZB_CW - 1) / ZB_CW;
+  }
+  hipLaunchKernelGGL(zbias_dw_kernel, dim3((unsigned)dblocks), dim3(256), dw_lds_bytes(N, maxL), st, J, njobs, N);
   return (int)hipGetLastError();
 }
