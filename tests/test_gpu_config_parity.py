@@ -147,6 +147,8 @@ def _ref_bf16_run(R, state, x, t, eps, names, probe=False):
         R.PROBE = None
     g16 = np.array([float(ref16.p[k].grad.double().norm()) if ref16.p[k].grad is not None else 0.0
                     for k in names])
+    ref16.vec1 = {k: ref16.p[k].grad.detach().double().reshape(-1) for k in names
+                  if ref16.p[k].grad is not None and ref16.p[k].grad.dim() == 1}
     return g16, l16.detach().float().contiguous(), mu16.detach().float(), lv16.detach().float(), loss16, dz, ref16
 
 
@@ -162,11 +164,15 @@ def _ref_bf16_run(R, state, x, t, eps, names, probe=False):
 # tools/bn_drift_probe.py, profiles/r5b_bn_drift_probe.log).  Round 5: both
 # paths run on the same seven-input ensemble (the bench input and six
 # copies perturbed by a relative 2^-13 ... 2^-10); a BatchNorm-affine
-# gradient's drift is its MEAN over the ensemble, the HIP path's within 1.5x
-# the reference's + 5 %; weights (>= 2-D, well conditioned) compare the bench
-# input's drift with the reference ensemble's max; and the elementwise dz drift
-# is compared at every BatchNorm (HIP must not drift more than the
-# reference's own bf16 path).
+# gradient's drift is the ensemble MEAN of its per-channel relative error
+# ||g - g32|| / ||g32|| (a sum over channels: a stable statistic, where the
+# norm drift |(||g|| - ||g32||)| / ||g32|| of a vector 80 % off elementwise is
+# one noise draw -- its ensemble mean still differed 2x between two paths
+# whose per-channel errors agree, profiles/r5k_bn_drift_probe.log), the HIP
+# path's within 1.5x the reference's + 5 %; weights (>= 2-D, well
+# conditioned) compare the bench input's norm drift with the reference
+# ensemble's max; and the elementwise dz drift is compared at every BatchNorm
+# (HIP must not drift more than the reference's own bf16 path).
 REF_PERTURB = (2.0 ** -13, 2.0 ** -12, 2.0 ** -11.5, 2.0 ** -11, 2.0 ** -10.5, 2.0 ** -10)
 DZ_VS_REF = 1.05
 
@@ -204,7 +210,11 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     ref_mu = max(_drift(mu16, muref)[0], _drift(lv16, lvref)[0])
     r = torch.rand(x.shape, generator=torch.Generator().manual_seed(5)) * 2 - 1
     xps = [(x * (1 + sc * r)).contiguous(memory_format=CL) for sc in REF_PERTURB]
-    g16_ens = [g16] + [_ref_bf16_run(R, state, xp, t, eps, names)[0] for xp in xps]
+    g16_ens, v16_ens = [g16], [ref16.vec1]
+    for xp in xps:
+        run = _ref_bf16_run(R, state, xp, t, eps, names)
+        g16_ens.append(run[0])
+        v16_ens.append(run[6].vec1)
 
     model = model.to(DEV).to(memory_format=CL).train()
     model.eps_override = eps
@@ -236,6 +246,8 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     params = dict(model.named_parameters())
     gn = np.array([float(params[k].grad.double().norm()) if params[k].grad is not None else 0.0 for k in names])
     ghip_ens = [gn]
+    vhip_ens = [{k: p.grad.detach().double().cpu().reshape(-1) for k, p in params.items()
+                 if p.grad is not None and p.dim() == 1}]
     for xp in xps:   # the same perturbed inputs through the HIP path (fresh model, same weights)
         mp = UNetResNet(3, 1, pretrained=False)
         mp.load_state_dict(state)
@@ -248,12 +260,24 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
         pp = dict(mp.named_parameters())
         ghip_ens.append(np.array([float(pp[k].grad.double().norm()) if pp[k].grad is not None else 0.0
                                   for k in names]))
+        vhip_ens.append({k: p.grad.detach().double().cpu().reshape(-1) for k, p in pp.items()
+                         if p.grad is not None and p.dim() == 1})
         del mp, pp
     big = gref > 1e-3 * gref.max()
     grel = np.abs(gn - gref) / np.maximum(gref, 1e-30)
     grel_ens = np.max([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in g16_ens], axis=0)
     mean_ref = np.mean([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in g16_ens], axis=0)
     mean_hip = np.mean([np.abs(g - gref) / np.maximum(gref, 1e-30) for g in ghip_ens], axis=0)
+    g32v = {k: p.grad.detach().double().reshape(-1) for k, p in ref.p.items() if p.grad is not None}
+
+    def vrel(ens):   # ensemble mean of the per-channel relative error, per 1-D parameter
+        out = np.zeros(len(names))
+        for i, k in enumerate(names):
+            if k in ens[0] and k in g32v:
+                den = max(float(g32v[k].norm()), 1e-30)
+                out[i] = np.mean([float((v[k] - g32v[k]).norm()) / den for v in ens])
+        return out
+    vmean_ref, vmean_hip = vrel(v16_ens), vrel(vhip_ens)
     grel16 = np.abs(g16 - gref) / np.maximum(gref, 1e-30)   # the reference's own bf16 gradient drift
     # per parameter: excess over the reference's own bf16 drift (ensemble max)
     excess = grel - BF16_VS_REF_DRIFT * grel_ens
@@ -294,13 +318,15 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     bbig = [i for i in np.where(big)[0] if dims[names[i]] == 1]
     worst_w = max(excess[i] for i in wbig)
     assert worst_w < BF16_GNORM, [w for w in worst if dims[w[1]] >= 2]
-    excess_b = mean_hip - BF16_VS_REF_DRIFT * mean_ref
-    worst_bl = sorted(((excess_b[i], names[i], mean_hip[i], mean_ref[i]) for i in bbig), reverse=True)[:3]
+    excess_b = vmean_hip - BF16_VS_REF_DRIFT * vmean_ref
+    worst_bl = sorted(((excess_b[i], names[i], vmean_hip[i], vmean_ref[i]) for i in bbig), reverse=True)[:3]
     worst_b = worst_bl[0][0]
     for _, nm, _, _ in worst_bl:
         i = names.index(nm)
-        print(f"  {nm}: HIP ensemble drifts {[round(float(abs(g[i] - gref[i]) / gref[i]), 4) for g in ghip_ens]}, "
-              f"CPU-bf16 {[round(float(abs(g[i] - gref[i]) / gref[i]), 4) for g in g16_ens]}")
+        print(f"  {nm}: per-channel error HIP {vmean_hip[i]:.4f} vs CPU-bf16 {vmean_ref[i]:.4f} (ensemble means); "
+              f"norm drifts HIP {[round(float(abs(g[i] - gref[i]) / gref[i]), 4) for g in ghip_ens]} "
+              f"(mean {mean_hip[i]:.4f}), CPU-bf16 {[round(float(abs(g[i] - gref[i]) / gref[i]), 4) for g in g16_ens]} "
+              f"(mean {mean_ref[i]:.4f})")
     assert worst_b < BF16_GNORM, worst_bl
     vecs = {k: (params[k].grad.double().cpu().reshape(-1), ref.p[k].grad.double().reshape(-1),
                 ref16.p[k].grad.double().reshape(-1)) for k in (names[i] for i in bbig)}
@@ -308,7 +334,7 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
     num16 = sum(float((c - r_).pow(2).sum()) for _, r_, c in vecs.values()) ** 0.5
     den = sum(float(r_.pow(2).sum()) for _, r_, _ in vecs.values()) ** 0.5
     print(f"config3 bf16: BN-affine gradients, relative L2 error HIP {num / den:.3e} vs CPU-bf16 "
-          f"{num16 / den:.3e}; worst weight excess {worst_w:.3e}; BN-affine ensemble-mean drift worst "
+          f"{num16 / den:.3e}; worst weight excess {worst_w:.3e}; BN-affine ensemble-mean per-channel error worst "
           f"(excess, name, HIP, CPU-bf16) {[(round(float(a_), 4), b_, round(float(c_), 4), round(float(d_), 4)) for a_, b_, c_, d_ in worst_bl]}; "
           f"bench-input-only CPU-bf16 drift of the worst: {grel16[names.index(worst[0][1])]:.3f}")
     assert num / den <= BF16_VS_REF_DRIFT * num16 / den + BF16_GNORM

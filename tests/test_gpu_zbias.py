@@ -107,7 +107,8 @@ def test_zbias_forward_matches_concat_conv(case):
 
 
 @pytest.mark.parametrize("mode", ["bf16", "f32"])
-@pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96), (2, 16, 48, 72, 64)])
+@pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96), (2, 16, 48, 72, 64),
+                                   (2, 16, 9, 40, 1024)])
 @pytest.mark.parametrize("acc", [False, True])
 def test_zbias_backward_matches_map_gradient(mode, shape, acc):
     """From conv1's pre-BN gradient dy: the weight gradient's z columns

@@ -110,11 +110,11 @@ def main():
         d32, x32 = dz32[pre].double(), xh32[pre].double()
         dh, xhh = hip[pre].double(), hipx[pre].double()
         d16, x16 = dz16[pre].double(), xh16[pre].double()
-        B = (d32 * x32).sum((0, 2, 3))
-        nb = float(B.norm())
+        G = (d32 * x32).sum((0, 2, 3))
+        nb = float(G.norm())
 
         def e(a, b_):
-            return float(((a * b_).sum((0, 2, 3)) - B).norm()) / nb
+            return float(((a * b_).sum((0, 2, 3)) - G).norm()) / nb
         db = d32.sum((0, 2, 3))
         print(f"  {pre:28s} A {e(dh, xhh):.3e}  C {e(dh, x32):.3e}  D {e(d32, xhh):.3e}  E {e(d16, x16):.3e}  "
               f"F {e(d16, x32):.3e} | dbeta {float((dh.sum((0, 2, 3)) - db).norm()) / float(db.norm()):.3e} / "

@@ -9,7 +9,8 @@
 #   bench[:<model>]        the default bench line (model unet: CPU leg + config-3 secondary)
 #   ab[:<model>[:<reps>]]  whole-tree A/B vs the tree copied to ab/tree (alternating, same box)
 #   flag:<module.NAME>[:<model>]  A/B of an engine flag (0 vs 1) on the current tree
-#   prof[:<model>]         rocprofv3 --kernel-trace --stats of a short bench -> <model>_kernel_stats.csv
+#   prof[:<model>[:<module.NAME=v>]]  rocprofv3 --kernel-trace --stats of a short bench
+#                          (optionally with an engine flag set) -> <model>[_<flag>]_kernel_stats.csv
 #   evidence               tools/gpu_evidence.sh (both benches profiled + PMC traffic + tables)
 #   sq[:<model>]           tools/gpu_sq_timing.sh (SQ wave-cycle / MFMA-busy counters per kernel)
 #   conv[:<args>]          tools/conv_bench.py with the given args (spaces as '+')
@@ -68,13 +69,16 @@ for step in "$@"; do
         python tools/ab_line.py "$f $m rep$i (0 vs 1)" $O/flag_${f}_${m}_0_$i.log $O/flag_${f}_${m}_1_$i.log | tee -a $O/ab_summary.txt
       done ;;
     prof)
-      m=${arg:-unet}
-      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$m -o p -- \
-        python -u $R/bench.py --model $m --steps 10 --warmup 3 --no-cpu-baseline --no-roofline > $O/prof_$m.log 2>&1) \
-        || { echo "PROF_FAIL $m"; tail -5 $O/prof_$m.log; exit 1; }
-      find $O/prof_$m -name "*kernel_stats.csv" -exec cp {} $O/${m}_kernel_stats.csv \;
-      rm -rf $O/prof_$m
-      echo "prof $m done" ;;
+      m=${arg%%:*}; m=${m:-unet}
+      fl=""; [[ "$arg" == *:* ]] && fl=${arg#*:}
+      t=$m${fl:+_$fl}
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$t -o p -- \
+        python -u $R/bench.py --model $m --steps 10 --warmup 3 --no-cpu-baseline --no-roofline \
+        ${fl:+--engine-flag $fl} > $O/prof_$t.log 2>&1) \
+        || { echo "PROF_FAIL $t"; tail -5 $O/prof_$t.log; exit 1; }
+      find $O/prof_$t -name "*kernel_stats.csv" -exec cp {} $O/${t}_kernel_stats.csv \;
+      rm -rf $O/prof_$t
+      echo "prof $t done" ;;
     evidence)
       bash tools/gpu_evidence.sh $tag || exit 1 ;;
     sq)

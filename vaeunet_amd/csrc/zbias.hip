@@ -21,11 +21,12 @@
 //                   dc[n][l]              = sum_c sum_tap W[c][cz0+l][tap] R[n][c][tap]
 //                 -- dc is the pixel sum of d(map) the latent backward needs
 //                 (vu_latent_bwd_sums produced it from the map gradient).
-//                 Three launches: region partials per (sample, pixel chunk);
-//                 per sample, R of every channel (to the workspace); per 32
-//                 output channels, the z columns of dW and the dc partial of
-//                 those channels into split `chunk` of the consumer's part
-//                 array (vu_latent_bwd sums the splits).
+//                 Three launches: region partials per (sample, pixel chunk
+//                 of ~64 KB of dy); per (sample, 64 statistics) the sum of those
+//                 partials; per 32 output channels, R from the sums and the
+//                 corner pixels, the z columns of dW and the dc partial of those
+//                 channels into split `chunk` of the consumer's part array
+//                 (vu_latent_bwd sums the splits).
 // Every sum runs in a fixed order (reproducible run to run).
 #include "common.h"
 #include "../../include/vaeunet.h"
@@ -34,8 +35,7 @@ namespace {
 
 constexpr int ZB_MAXJ = 8;
 constexpr int ZB_SPLITS = 32;  // == latent.hip LAT_SPLITS: the part array is [N][32][L]
-constexpr int ZB_PCH = 1024;   // pixels per region-pass block (a contiguous range of rows)
-constexpr int ZB_MAXCH = 1024; // pixel chunks per sample (HW <= 1024 * 1024)
+constexpr int ZB_CHUNK_ELEMS = 32768;  // dy elements per region-pass block (64 KB in bf16)
 constexpr int ZB_CW = 32;      // output channels per finish block
 constexpr int ZB_NS = 5;       // region partials: total, col 0, col W-1, row 0, row H-1
 constexpr int ZB_MAXN = 64;
@@ -53,6 +53,39 @@ VU_DEV int find_job(const ZbJobs& jobs, int njobs) {
 // tap k (0..2) of a row / column is inside the image for border class cr
 VU_DEV bool tap_in(int cr, int k) { return !((cr == 0 && k == 0) || (cr == 2 && k == 2)); }
 
+// pixels per region-pass block: ~ZB_CHUNK_ELEMS elements of dy whatever co is
+// (a fixed pixel count left the wide-channel jobs with a handful of 1 MB blocks)
+__host__ __device__ inline int pix_chunk(int co) { return co >= ZB_CHUNK_ELEMS / 16 ? 16 : ZB_CHUNK_ELEMS / co; }
+__host__ __device__ inline int n_chunks(int co, int H, int W) { return (H * W + pix_chunk(co) - 1) / pix_chunk(co); }
+
+// dst[0, n) = src(e) staged into LDS by the block, 8 independent loads in
+// flight per thread (a load -> store loop waits out one latency per element)
+template <typename F>
+VU_DEV void stage(float* dst, int n, F src) {
+  for (int b = threadIdx.x; b < n; b += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = b + u * 256;
+      v[u] = src(e < n ? e : n - 1);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b + u * 256 < n) dst[b + u * 256] = v[u];
+  }
+}
+
+// the block's z weights [ZB_CW][L][9] (zero past co)
+VU_DEV void stage_w(float* Wl, const VuZbJob& J, int c0, int cw) {
+  const int L = J.L;
+  stage(Wl, ZB_CW * L * 9, [&](int e) {
+    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
+    const int cc = c < cw ? c0 + c : c0;
+    const float v = J.w[(int64_t)cc * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky + (t % 3) * J.ws_kx];
+    return c < cw ? v : 0.f;
+  });
+}
+
 // ---- forward: the bias tables -------------------------------------------
 // one block per (job, 32 output channels): that chunk's z weights [32][L][9]
 // and the vectors [N][L] staged in LDS (every global load issued up front),
@@ -65,13 +98,8 @@ __global__ __launch_bounds__(256) void zbias_fwd_kernel(const ZbJobs jobs, int n
   const int L = J.L, tid = threadIdx.x;
   float* Wl = zsm;                 // [ZB_CW][L][9]
   float* A = Wl + ZB_CW * L * 9;   // [N][L]
-  for (int e = tid; e < N * L; e += 256) A[e] = J.act[e];
-  for (int e = tid; e < ZB_CW * L * 9; e += 256) {
-    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
-    Wl[e] = c < cw ? J.w[(int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky +
-                         (t % 3) * J.ws_kx]
-                   : 0.f;
-  }
+  stage(A, N * L, [&](int e) { return J.act[e]; });
+  stage_w(Wl, J, c0, cw);
   __syncthreads();
   for (int e = tid; e < N * cw; e += 256) {
     const int n = e / cw, c = e - n * cw;
@@ -101,20 +129,20 @@ __global__ __launch_bounds__(256) void zbias_fwd_kernel(const ZbJobs jobs, int n
 }
 
 // ---- backward 1: region partials per (sample, pixel chunk) ---------------
-// rs[((n * nch + chunk) * ZB_NS + k) * co + c], nch = ceil(HW / ZB_PCH); a
-// chunk is ZB_PCH consecutive pixels of one sample, 8 loads in flight per
-// thread (a row-band version with 4 loads in flight was latency-bound)
+// rs[((n * nch + chunk) * ZB_NS + k) * co + c], nch = n_chunks(co, H, W); a
+// chunk is pix_chunk(co) consecutive pixels of one sample, 8 loads in flight
+// per thread
 template <typename T>
 __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int njobs, int N) {
   __shared__ float sh[ZB_NS * 2048];
   const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
   const int H = J.H, W = J.W, C = J.co;
-  const int HW = H * W, nch = (HW + ZB_PCH - 1) / ZB_PCH;
+  const int HW = H * W, pch = pix_chunk(C), nch = (HW + pch - 1) / pch;
   const int lb = (int)((int64_t)blockIdx.x - J.block0);
   const int n = lb / nch, chunk = lb - (lb / nch) * nch;
   const int V = C >> 3, slots = 256 / V;
   const int tid = threadIdx.x, cv = tid % V, slot = tid / V;
-  const int p0 = chunk * ZB_PCH, p1 = min(HW, p0 + ZB_PCH);
+  const int p0 = chunk * pch, p1 = min(HW, p0 + pch);
   constexpr int U = 8;
   float s[ZB_NS][8];
 #pragma unroll
@@ -163,43 +191,69 @@ __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int nj
   }
 }
 
-// ---- backward 2: per sample, R[c][tap] of every channel -> workspace ------
-// thread (c, statistic) sums its chunk column (16 loads in flight); the
-// corners are read directly
+// ---- backward 2: per (sample, 64 statistics): the sum of the chunk
+// partials -> S[n][k][c] (after the partials in rs); 4 lanes per statistic,
+// 8 loads in flight each, then a fixed-order LDS reduction
+__global__ __launch_bounds__(256) void zbias_sum_kernel(const ZbJobs jobs, int njobs, int N) {
+  __shared__ float red[4][64];
+  const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
+  const int C = J.co, nv = ZB_NS * C, ngrp = (nv + 63) / 64;
+  const int lb = (int)((int64_t)blockIdx.x - J.block0);
+  const int n = lb / ngrp, grp = lb - (lb / ngrp) * ngrp;
+  const int nch = n_chunks(C, J.H, J.W);
+  const int v = threadIdx.x & 63, lane = threadIdx.x >> 6, q = grp * 64 + v;
+  float t = 0.f;
+  if (q < nv) {
+    const float* rp = J.rs + (int64_t)n * nch * nv + q;
+    for (int b0 = lane; b0 < nch; b0 += 4 * 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * 4;
+        x[u] = rp[(int64_t)(b < nch ? b : lane) * nv];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u * 4 < nch) t += x[u];
+    }
+  }
+  red[lane][v] = t;
+  __syncthreads();
+  if (lane == 0 && q < nv)
+    J.rs[(int64_t)N * nch * nv + (int64_t)n * nv + q] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+}
+
+// ---- backward 3: per 32 output channels: R[n][c][tap] from the sums and the
+// four corner pixels of dy, then the z columns of dW and the dc partial of
+// these channels (into split `chunk` of part; chunk 0 also zeroes the splits
+// no chunk uses), from R, the z weights and the vectors in LDS
+//   dW[c0 + c][cz0 + l][tap] (+)= sum_n act[n][l] R[n][c][tap]
+//   dc_chunk[n][l]              = sum_{c, tap} W[c0 + c][cz0 + l][tap] R[n][c][tap]
 template <typename T>
-__global__ __launch_bounds__(256) void zbias_r_kernel(const ZbJobs jobs, int njobs, int N) {
+__global__ __launch_bounds__(256) void zbias_dw_kernel(const ZbJobs jobs, int njobs, int N) {
   extern __shared__ float zsm[];
   const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
-  const int n = (int)((int64_t)blockIdx.x - J.block0);
-  const int H = J.H, W = J.W, C = J.co, tid = threadIdx.x;
-  const int nch = (H * W + ZB_PCH - 1) / ZB_PCH;
-  float* S = zsm;                  // [C][ZB_NS + 4]
-  const float* rsn = J.rs + (int64_t)n * nch * ZB_NS * C;
-  for (int e = tid; e < C * ZB_NS; e += 256) {
-    const int c = e / ZB_NS, k = e - (e / ZB_NS) * ZB_NS;
-    const float* rp = rsn + (int64_t)k * C + c;
-    float t = 0.f;
-    for (int b0 = 0; b0 < nch; b0 += 16) {
-      float v[16];
-#pragma unroll
-      for (int b = 0; b < 16; ++b) v[b] = b0 + b < nch ? rp[(int64_t)(b0 + b) * ZB_NS * C] : 0.f;
-#pragma unroll
-      for (int b = 0; b < 16; ++b) t += v[b];
-    }
-    S[c * (ZB_NS + 4) + k] = t;
-  }
+  const int chunk = (int)((int64_t)blockIdx.x - J.block0);
+  const int c0 = chunk * ZB_CW, cw = J.co - c0 < ZB_CW ? J.co - c0 : ZB_CW;
+  const int L = J.L, C = J.co, H = J.H, W = J.W, tid = threadIdx.x;
+  const int nch = n_chunks(C, H, W);
+  const int nchunks = (C + ZB_CW - 1) / ZB_CW;
+  float* R = zsm;                  // [N][ZB_CW][9]
+  float* A = R + N * ZB_CW * 9;    // [N][L]
+  float* Wl = A + N * L;           // [ZB_CW][L][9]
+  const float* S = J.rs + (int64_t)N * nch * ZB_NS * C;
   const T* dy = reinterpret_cast<const T*>(J.dy);
-  for (int e = tid; e < C * 4; e += 256) {
-    const int c = e >> 2, k = e & 3;
-    const int y = (k >> 1) ? H - 1 : 0, x = (k & 1) ? W - 1 : 0;
-    S[c * (ZB_NS + 4) + ZB_NS + k] = ld1<T>(dy + ((int64_t)n * H * W + (int64_t)y * W + x) * J.dy_stride + c);
-  }
-  __syncthreads();
-  float* Rg = J.rs + (int64_t)N * nch * ZB_NS * C + (int64_t)n * C * 9;
-  for (int c = tid; c < C; c += 256) {
-    const float* q = S + c * (ZB_NS + 4);
-    const float tot = q[0], col0 = q[1], colL = q[2], row0 = q[3], rowL = q[4];
-    const float k00 = q[5], k0L = q[6], kL0 = q[7], kLL = q[8];
+  stage(A, N * L, [&](int e) { return J.act[e]; });
+  stage_w(Wl, J, c0, cw);
+  for (int e = tid; e < N * ZB_CW; e += 256) {
+    const int n = e / ZB_CW, c = e - n * ZB_CW;
+    const int cc = c0 + (c < cw ? c : 0);
+    const float* sp = S + (int64_t)n * ZB_NS * C + cc;
+    const T* dn = dy + (int64_t)n * H * W * J.dy_stride + cc;
+    const float tot = sp[0], col0 = sp[C], colL = sp[2 * C], row0 = sp[3 * C], rowL = sp[4 * C];
+    const float k00 = ld1<T>(dn), k0L = ld1<T>(dn + (int64_t)(W - 1) * J.dy_stride);
+    const float kL0 = ld1<T>(dn + (int64_t)(H - 1) * W * J.dy_stride);
+    const float kLL = ld1<T>(dn + ((int64_t)(H - 1) * W + W - 1) * J.dy_stride);
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -213,38 +267,8 @@ __global__ __launch_bounds__(256) void zbias_r_kernel(const ZbJobs jobs, int njo
         if (ky == 0 && kx == 2) r += k0L;
         if (ky == 2 && kx == 0) r += kL0;
         if (ky == 2 && kx == 2) r += kLL;
-        Rg[c * 9 + ky * 3 + kx] = r;
+        R[e * 9 + ky * 3 + kx] = c < cw ? r : 0.f;
       }
-  }
-}
-
-// ---- backward 3: per 32 output channels: the z columns of dW and the dc
-// partial of these channels (into split `chunk` of part; chunk 0 also zeroes
-// the splits no chunk uses), from R, the z weights and the vectors in LDS
-//   dW[c0 + c][cz0 + l][tap] (+)= sum_n act[n][l] R[n][c][tap]
-//   dc_chunk[n][l]              = sum_{c, tap} W[c0 + c][cz0 + l][tap] R[n][c][tap]
-__global__ __launch_bounds__(256) void zbias_dw_kernel(const ZbJobs jobs, int njobs, int N) {
-  extern __shared__ float zsm[];
-  const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
-  const int chunk = (int)((int64_t)blockIdx.x - J.block0);
-  const int c0 = chunk * ZB_CW, cw = J.co - c0 < ZB_CW ? J.co - c0 : ZB_CW;
-  const int L = J.L, C = J.co, tid = threadIdx.x;
-  const int nch = (J.H * J.W + ZB_PCH - 1) / ZB_PCH;
-  const int nchunks = (C + ZB_CW - 1) / ZB_CW;
-  float* R = zsm;                  // [N][ZB_CW][9]
-  float* A = R + N * ZB_CW * 9;    // [N][L]
-  float* Wl = A + N * L;           // [ZB_CW][L][9]
-  const float* Rg = J.rs + (int64_t)N * nch * ZB_NS * C;
-  for (int e = tid; e < N * L; e += 256) A[e] = J.act[e];
-  for (int e = tid; e < ZB_CW * L * 9; e += 256) {
-    const int c = e / (L * 9), rem = e - c * (L * 9), l = rem / 9, t = rem - l * 9;
-    Wl[e] = c < cw ? J.w[(int64_t)(c0 + c) * J.ws_co + (int64_t)(J.cz0 + l) * J.ws_ci + (t / 3) * J.ws_ky +
-                         (t % 3) * J.ws_kx]
-                   : 0.f;
-  }
-  for (int e = tid; e < N * ZB_CW * 9; e += 256) {
-    const int n = e / (ZB_CW * 9), rem = e - n * (ZB_CW * 9), c = rem / 9, t = rem - c * 9;
-    R[e] = c < cw ? Rg[((int64_t)n * C + c0 + c) * 9 + t] : 0.f;
   }
   __syncthreads();
   for (int e = tid; J.dw && e < cw * L; e += 256) {
@@ -283,7 +307,6 @@ __global__ __launch_bounds__(256) void zbias_dw_kernel(const ZbJobs jobs, int nj
   if ((dtype) == VU_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
 
 size_t fwd_lds_bytes(int N, int L) { return (size_t)(ZB_CW * L * 9 + N * L) * sizeof(float); }
-size_t r_lds_bytes(int C) { return (size_t)(C * (ZB_NS + 4)) * sizeof(float); }
 size_t dw_lds_bytes(int N, int L) { return (size_t)(N * ZB_CW * 9 + N * L + ZB_CW * L * 9) * sizeof(float); }
 
 int pack(const VuZbJob* jobs, int njobs, ZbJobs& J) {
@@ -298,12 +321,13 @@ extern "C" int vu_zbias_supported(int N, int L, int co) {
   if (N < 1 || N > ZB_MAXN || L < 1 || L > 64 || co < 8 || co % 8 || co / 8 > 256) return 0;
   const size_t cap = 160 * 1024;
   if ((co + ZB_CW - 1) / ZB_CW > ZB_SPLITS) return 0;  // dc partials: one split per 32 channels
-  return fwd_lds_bytes(N, L) <= cap && r_lds_bytes(co) <= cap && dw_lds_bytes(N, L) <= cap ? 1 : 0;
+  return fwd_lds_bytes(N, L) <= cap && dw_lds_bytes(N, L) <= cap ? 1 : 0;
 }
 
-// region partials [N][nch][5][co], then R [N][co][9]
+// region partials [N][nch][5][co], then their sums [N][5][co]
 extern "C" int64_t vu_zbias_rs_floats(int N, int co, int H, int W) {
-  return (int64_t)N * (((int64_t)H * W + ZB_PCH - 1) / ZB_PCH) * ZB_NS * co + (int64_t)N * co * 9;
+  if (co < 8) return 0;
+  return (int64_t)N * ((int64_t)n_chunks(co, H, W) + 1) * ZB_NS * co;
 }
 
 extern "C" int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream) {
@@ -327,32 +351,35 @@ extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, vo
   ZbJobs J;
   if (int rc = pack(jobs, njobs, J)) return rc;
   int64_t rblocks = 0;
-  int maxL = 1, maxC = 8;
+  int maxL = 1;
   for (int j = 0; j < njobs; ++j) {
     VuZbJob& q = J.j[j];
     if (!vu_zbias_supported(N, q.L, q.co) || !q.w || !q.act || !q.dy || !q.rs || !q.part ||
         q.H < 2 || q.W < 2 || q.dy_stride % 8)
       return (int)hipErrorInvalidValue;
-    if ((int64_t)q.H * q.W > (int64_t)ZB_MAXCH * ZB_PCH) return (int)hipErrorInvalidValue;
+    if ((int64_t)q.H * q.W > (1 << 30) / q.co) return (int)hipErrorInvalidValue;
     q.block0 = rblocks;
-    rblocks += (int64_t)N * ((q.H * q.W + ZB_PCH - 1) / ZB_PCH);
+    rblocks += (int64_t)N * n_chunks(q.co, q.H, q.W);
     maxL = q.L > maxL ? q.L : maxL;
-    maxC = q.co > maxC ? q.co : maxC;
   }
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
     hipLaunchKernelGGL((zbias_rs_kernel<T>), dim3((unsigned)rblocks), dim3(256), 0, st, J, njobs, N);
   })
-  for (int j = 0; j < njobs; ++j) J.j[j].block0 = (int64_t)j * N;
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((zbias_r_kernel<T>), dim3((unsigned)(njobs * N)), dim3(256), r_lds_bytes(maxC), st, J,
-                       njobs, N);
-  })
+  int64_t sblocks = 0;
+  for (int j = 0; j < njobs; ++j) {
+    J.j[j].block0 = sblocks;
+    sblocks += (int64_t)N * ((ZB_NS * J.j[j].co + 63) / 64);
+  }
+  hipLaunchKernelGGL(zbias_sum_kernel, dim3((unsigned)sblocks), dim3(256), 0, st, J, njobs, N);
   int64_t dblocks = 0;
   for (int j = 0; j < njobs; ++j) {
     J.j[j].block0 = dblocks;
     dblocks += (J.j[j].co + ZB_CW - 1) / ZB_CW;
   }
-  hipLaunchKernelGGL(zbias_dw_kernel, dim3((unsigned)dblocks), dim3(256), dw_lds_bytes(N, maxL), st, J, njobs, N);
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((zbias_dw_kernel<T>), dim3((unsigned)dblocks), dim3(256), dw_lds_bytes(N, maxL), st, J,
+                       njobs, N);
+  })
   return (int)hipGetLastError();
 }
