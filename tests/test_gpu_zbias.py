@@ -70,6 +70,12 @@ def test_zbias_forward_matches_concat_conv(case):
     w = (torch.randn(co, lead + L, 3, 3, generator=g) / (3 * (lead + L) ** 0.5)).to(DEV)
     act = torch.rand(N, L, generator=g).to(dt).float().to(DEV)   # ReLU'd vectors, storage-rounded
     table = _table(w, lead, L, H, W, act)
+    # the table from a channels_last copy of the weight (the model's layout) is the same
+    table_cl = _table(w.contiguous(memory_format=CL), lead, L, H, W, act)
+    torch.testing.assert_close(table_cl, table, rtol=1e-6, atol=1e-7)
+    w_odd = torch.empty(co, lead + L + 1, 3, 3, device=DEV)[:, 1:]   # unaligned rows: the scalar staging path
+    w_odd.copy_(w)
+    torch.testing.assert_close(_table(w_odd, lead, L, H, W, act), table, rtol=1e-6, atol=1e-7)
     srcs = [x.to(DEV, dt).contiguous(memory_format=CL) for x in xs]
     out = K.empty_act(N, co, H, W, dt, DEV)
     _tune(*tune)
@@ -110,7 +116,8 @@ def test_zbias_forward_matches_concat_conv(case):
 @pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96), (2, 16, 48, 72, 64),
                                    (2, 16, 9, 40, 1024)])
 @pytest.mark.parametrize("acc", [False, True])
-def test_zbias_backward_matches_map_gradient(mode, shape, acc):
+@pytest.mark.parametrize("cl", [False, True])
+def test_zbias_backward_matches_map_gradient(mode, shape, acc, cl):
     """From conv1's pre-BN gradient dy: the weight gradient's z columns
     (written / accumulated; the other columns untouched) and the pixel sums
     of the z map's gradient (the split partials the latent backward sums)
@@ -120,11 +127,12 @@ def test_zbias_backward_matches_map_gradient(mode, shape, acc):
     lead = 64
     dt = torch.bfloat16 if mode == "bf16" else torch.float32
     g = torch.Generator().manual_seed(23)
-    w = (torch.randn(co, lead + L, 3, 3, generator=g) / 10).to(DEV)
+    fmt = CL if cl else torch.contiguous_format   # the model's weights are channels_last after .to(CL)
+    w = (torch.randn(co, lead + L, 3, 3, generator=g) / 10).to(DEV).contiguous(memory_format=fmt)
     act = torch.rand(N, L, generator=g).to(DEV)
     dy = torch.randn(N, co, H, W, generator=g).to(dt)
     dyd = dy.to(DEV).contiguous(memory_format=CL)
-    dw = torch.randn(co, lead + L, 3, 3, generator=g).to(DEV)
+    dw = torch.randn(co, lead + L, 3, 3, generator=g).to(DEV).contiguous(memory_format=fmt)
     dw0 = dw.clone()
     part = torch.full((N * 32 * L,), float("nan"), dtype=torch.float32, device=DEV)
     rs = torch.empty(K.query("vu_zbias_rs_floats", N, co, H, W), dtype=torch.float32, device=DEV)

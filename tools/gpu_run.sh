@@ -16,6 +16,7 @@
 #   conv[:<args>]          tools/conv_bench.py with the given args (spaces as '+')
 #   enc[:<args>]           tools/enc_bench.py with the given args (spaces as '+')
 #   py:<script>[:<args>]   any python tool under tools/ (args: spaces as '+')
+#   rprof:<script>[:<args>]  the same under rocprofv3 --kernel-trace --stats -> rprof_<script>_kernel_stats.csv
 set -o pipefail
 export TMPDIR=/tmp
 tag=$1; shift
@@ -97,6 +98,15 @@ for step in "$@"; do
       timeout -k 10 500 python -u tools/$s ${a//+/ } > $O/py_${n}_${s%.py}.log 2>&1 \
         || { echo "PY_FAIL $s"; tail -15 $O/py_${n}_${s%.py}.log; exit 1; }
       tail -3 $O/py_${n}_${s%.py}.log ;;
+    rprof)
+      s=${arg%%:*}; a=""; [[ "$arg" == *:* ]] && a=${arg#*:}
+      t=${s%.py}
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rprof_$t -o p -- \
+        python -u $R/tools/$s ${a//+/ } > $O/rprof_$t.log 2>&1) \
+        || { echo "RPROF_FAIL $s"; tail -10 $O/rprof_$t.log; exit 1; }
+      find $O/rprof_$t -name "*kernel_stats.csv" -exec cp {} $O/rprof_${t}_kernel_stats.csv \;
+      rm -rf $O/rprof_$t
+      echo "rprof $t done" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -619,10 +619,16 @@ def zbias_backward(M, zscs, parts):
     weight reported to the DP reducer (behind its GEMM weight gradient)."""
     N = zscs[0].table.shape[0]
     arr = _zb_jobs(zscs)
-    keep = []
+    keep, fix = [], []
     for i, z in enumerate(zscs):
         conv1 = z.blk.conv1[0]
         g, acc = z.sink
+        if g is not None and g.stride() != conv1.weight.stride():
+            # the kernel addresses dW with the weight's strides: a gradient of
+            # another layout takes the z columns through a weight-layout buffer
+            tmp = torch.empty_like(conv1.weight)
+            fix.append((g, acc, tmp, z.lead, z.lead + z.cons.conv.out_channels))
+            g, acc = tmp, False
         rs = torch.empty(K.query("vu_zbias_rs_floats", N, conv1.out_channels, z.H, z.W), dtype=torch.float32,
                          device=z.table.device)
         keep.append(rs)
@@ -630,6 +636,11 @@ def zbias_backward(M, zscs, parts):
         arr[i].rs, arr[i].part = rs.data_ptr(), parts[i].data_ptr()
         arr[i].dw, arr[i].grad_acc = K.ptr(g), 1 if acc else 0
     K.call("vu_zbias_bwd", arr, len(zscs), N, K.dcode(zscs[0].dy.dtype), K.stream())
+    for g, acc, tmp, a, b in fix:
+        if acc:
+            g[:, a:b].add_(tmp[:, a:b])
+        else:
+            g[:, a:b].copy_(tmp[:, a:b])
     ws = [z.blk.conv1[0].weight for z in zscs if z.sink[0] is not None]
     M.side(lambda: M.notify(ws), *[z.dy for z in zscs])
     for z in zscs:
