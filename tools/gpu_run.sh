@@ -41,7 +41,7 @@ for step in "$@"; do
       if [ -n "$keys" ]; then
         if [ -n "$files" ]; then sel="tests"; keys="$keys or $(for f in $files; do basename $f .py; done | paste -sd' ' | sed 's/ / or /g')"; fi
       fi
-      timeout -k 10 1000 python -u -m pytest $sel ${keys:+-k "$keys"} -m gpu --maxfail=10 -q --timeout 300 --timeout-method thread \
+      timeout -k 10 1000 python -u -m pytest $sel ${keys:+-k "$keys"} -m gpu --maxfail=10 -q -rP --timeout 300 --timeout-method thread \
         > $O/tests_$n.log 2>&1 || { echo "TESTS_FAIL ($step)"; tail -40 $O/tests_$n.log; exit 1; }
       tail -1 $O/tests_$n.log ;;
     bench)
