@@ -755,7 +755,7 @@ typedef struct VuZbJob {
   float* table;                /* forward: [N][9][co] */
   const void* dy;              /* backward: conv1's pre-BN output gradient, NHWC, co channels */
   int64_t dy_stride;
-  float* rs;                   /* region-sum partials, vu_zbias_rs_floats(N, co) */
+  float* rs;                   /* backward workspace, vu_zbias_rs_floats(N, co, H, W) floats */
   float* part;                 /* the consumer's VuLatentJob.part ([N][32][L]) */
   float* dw;                   /* conv1.weight.grad (strides of w): z columns written, or added when grad_acc */
   int32_t grad_acc;
@@ -767,8 +767,9 @@ int vu_zbias_supported(int N, int L, int co);
 int64_t vu_zbias_rs_floats(int N, int co, int H, int W);
 /* the [N][9][co] tables of every job (one launch) */
 int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream);
-/* region sums of every job's dy, then dW's z columns and the dc partials
- * (two launches); dtype: dy's storage (VU_BF16 / VU_F32) */
+/* region sums of every job's dy (partials per ~64 KB pixel chunk, then their
+ * sums), then dW's z columns and the dc partials (three launches); dtype:
+ * dy's storage (VU_BF16 / VU_F32) */
 int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, void* stream);
 /* 0 when a consumer of this geometry is served (co = 8 * 2^k <= 2048, cpad % 8,
  * stride % 8), else hipErrorInvalidValue */
