@@ -9,6 +9,7 @@
 #   bench[:<model>]        the default bench line (model unet: CPU leg + config-3 secondary)
 #   ab[:<model>[:<reps>]]  whole-tree A/B vs the tree copied to ab/tree (alternating, same box)
 #   flag:<module.NAME>[:<model>]  A/B of an engine flag (0 vs 1) on the current tree
+#   tune:<KEY>:<A>:<B>[:<model>]   A/B of a library tuning key (vu_gemm_set_tuning) A vs B
 #   prof[:<model>[:<module.NAME=v>]]  rocprofv3 --kernel-trace --stats of a short bench
 #                          (optionally with an engine flag set) -> <model>[_<flag>]_kernel_stats.csv
 #   evidence               tools/gpu_evidence.sh (both benches profiled + PMC traffic + tables)
@@ -68,6 +69,15 @@ for step in "$@"; do
             --engine-flag $f=$v > $O/flag_${f}_${m}_${v}_$i.log 2>&1 || { echo "FLAG_FAIL $f=$v"; tail -5 $O/flag_${f}_${m}_${v}_$i.log; exit 1; }
         done
         python tools/ab_line.py "$f $m rep$i (0 vs 1)" $O/flag_${f}_${m}_0_$i.log $O/flag_${f}_${m}_1_$i.log | tee -a $O/ab_summary.txt
+      done ;;
+    tune)
+      IFS=':' read -r key va vb tm <<< "$arg"; tm=${tm:-unet}
+      for i in 1 2; do
+        for v in $va $vb; do
+          timeout -k 10 300 python -u bench.py --model $tm --no-cpu-baseline --no-roofline --steps 40 \
+            --tune $key=$v > $O/tune_${key}_${tm}_${v}_$i.log 2>&1 || { echo "TUNE_FAIL $key=$v"; tail -5 $O/tune_${key}_${tm}_${v}_$i.log; exit 1; }
+        done
+        python tools/ab_line.py "tune $key $tm rep$i ($va vs $vb)" $O/tune_${key}_${tm}_${va}_$i.log $O/tune_${key}_${tm}_${vb}_$i.log | tee -a $O/ab_summary.txt
       done ;;
     prof)
       m=${arg%%:*}; m=${m:-unet}
