@@ -129,8 +129,11 @@ VU_DEV void bfly16_bcast(float m, int lane, float (&out)[16]) {
 
 // RELU: the epilogue ReLU (VuGemmFwd.relu) as a separate instantiation: the
 // runtime block spilled the statistics variant (+16 % in the training step)
-// XM (experiment modes, VU_TUNE_V6_XM): 1 = s_setprio(1) around each tap's
-// 16 MFMAs (the two waves of a SIMD otherwise free-run in the same phase)
+// XM (experiment modes, VU_TUNE_V6_XM; A/B timing only, 0 in production):
+// 1 = s_setprio(1) around each tap's 16 MFMAs (the two waves of a SIMD
+// otherwise free-run in the same phase); 2 = no halo DMA after the first
+// (every group computes on stale buffers: the DMA-latency share); 3 = no
+// epilogue stores / statistics (the epilogue's share); results wrong in 2, 3
 template <bool STATS, bool RELU = false, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -263,10 +266,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   int t = lb, b = 0;
   for (int ti = 0; ti < ntile_blk; ++ti) {
     // ---- group (t, chunk 0): the other buffer takes chunk 1 of this tile ----
-    halo(t, 1, b ^ 1);
-    taps(b, 0, have_pend);
+    if (XM != 2) halo(t, 1, b ^ 1);
+    taps(b, 0, have_pend && XM != 3);
     // the halo was issued before the previous tile's 8 stores
-    if (have_pend) {
+    if (have_pend && XM != 3) {
       have_pend = false;
       if (STATS) wait_vm<10>(); else wait_vm<8>();
     } else {
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     // ---- group (t, chunk 1): the other buffer takes chunk 0 of the next tile ----
     const int img = t / per_img, r0 = t - (t / per_img) * per_img;
     const int ty = r0 / txn, tx = r0 - (r0 / txn) * txn;
-    if (ti + 1 < ntile_blk) halo(t + G, 0, b ^ 1);
+    if (ti + 1 < ntile_blk && XM != 2) halo(t + G, 0, b ^ 1);
     taps(b, 1, false);
     // ---- epilogue of tile t from registers: acc[i][j][r] = pixel fragment
     //      i (row 2*wid + i/2, column (i&1)*16 + l16), channel 16kg + 4j + r ----
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     if constexpr (RELU)
 #pragma unroll
       for (int i = 0; i < 4; ++i) epi_relu(acc[i]);
-    if (STATS) {
+    if (STATS && XM != 3) {
       // per-wave (sum, centered M2) of its 64 pixels: slot 4j + r of a lane
       // is channel 16*kg + 4j + r; after the butterfly lane (kg, l16) holds
       // slot l16, i.e. channel lane: one store per statistic
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     b ^= 1;
     t += G;
   }
-  if (have_pend) {
+  if (have_pend && XM != 3) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) store_pend(q);
     if (STATS) store_stats();
@@ -435,17 +438,21 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
   if (p.stat_sum)
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<true, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 2) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 2>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 3>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
   else
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 2) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 2>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 3>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
 int gemm_fwd_v6_tune(int key, int value) {
   if (key == VU_TUNE_V6_XM) {
-    if (value < 0 || value > 1) return (int)hipErrorInvalidValue;
+    if (value < 0 || value > 3) return (int)hipErrorInvalidValue;
     g_v6_xm = value;
     return 0;
   }
