@@ -133,7 +133,10 @@ VU_DEV void bfly16_bcast(float m, int lane, float (&out)[16]) {
 // 1 = s_setprio(1) around each tap's 16 MFMAs (the two waves of a SIMD
 // otherwise free-run in the same phase); 2 = no halo DMA after the first
 // (every group computes on stale buffers: the DMA-latency share); 3 = no
-// epilogue stores / statistics (the epilogue's share); results wrong in 2, 3
+// statistics and the output stores predicated off by a value test the
+// compiler cannot fold (the MFMAs stay live: the epilogue's share); 4 = the
+// fragments read once per group, not per tap (the LDS-read share); results
+// wrong in 2-4
 template <bool STATS, bool RELU = false, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   };
   auto store_pend = [&](int q) {  // piece q = 2 * fragment + half
     bf16_t* o = pdst + ((q >> 2) * (int64_t)W + ((q >> 1) & 1) * 16) * p.out_stride + 32 * (q & 1);
-    *reinterpret_cast<u32x4*>(o) = pend[q];
+    if (XM != 3 || pend[q][0] == 0x7fc17fc1u) *reinterpret_cast<u32x4*>(o) = pend[q];
   };
 
   // the 9 taps of one group over halo buffer b, chunk c; `pending` stores
@@ -236,18 +239,20 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   auto taps = [&](int b, int c, bool pending) {
     const char* hb = hl + b * HBUF;
     const int cx = c << 6;  // (c*4) XORed into the piece index: 4 pieces = 64 bytes
+    u32x4 bf[4], af[4];
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ty = tap / 3, tx = tap - (tap / 3) * 3;
       if (tap < 8 && pending) store_pend(tap);
-      if (STATS && tap == 8 && pending) store_stats();
-      u32x4 bf[4], af[4];
+      if (STATS && XM != 3 && tap == 8 && pending) store_stats();
+      if (XM != 4 || tap == 0) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(wl + (boff[j] ^ cx) + tap * 128);
+        for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(wl + (boff[j] ^ cx) + tap * 128);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int P = (2 * wid + (i >> 1) + ty) * HWD + (i & 1) * 16 + tx + l16;
-        af[i] = *reinterpret_cast<const u32x4*>(hb + P * 64 + (((kg + ((P >> 1) & 2)) & 3) << 4));
+        for (int i = 0; i < 4; ++i) {
+          const int P = (2 * wid + (i >> 1) + ty) * HWD + (i & 1) * 16 + tx + l16;
+          af[i] = *reinterpret_cast<const u32x4*>(hb + P * 64 + (((kg + ((P >> 1) & 2)) & 3) << 4));
+        }
       }
       if constexpr (XM == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -267,12 +272,13 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   for (int ti = 0; ti < ntile_blk; ++ti) {
     // ---- group (t, chunk 0): the other buffer takes chunk 1 of this tile ----
     if (XM != 2) halo(t, 1, b ^ 1);
-    taps(b, 0, have_pend && XM != 3);
+    taps(b, 0, have_pend);
     // the halo was issued before the previous tile's 8 stores
     if (have_pend && XM != 3) {
       have_pend = false;
       if (STATS) wait_vm<10>(); else wait_vm<8>();
     } else {
+      have_pend = false;
       wait_vm<0>();
     }
     raw_barrier();
@@ -362,10 +368,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
     b ^= 1;
     t += G;
   }
-  if (have_pend && XM != 3) {
+  if (have_pend) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) store_pend(q);
-    if (STATS) store_stats();
+    if (STATS && XM != 3) store_stats();
   }
 }
 
@@ -440,19 +446,21 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
     else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 2) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 2>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 3>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 4) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 4>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
   else
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 2) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 2>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 3>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 4) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 4>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
 int gemm_fwd_v6_tune(int key, int value) {
   if (key == VU_TUNE_V6_XM) {
-    if (value < 0 || value > 3) return (int)hipErrorInvalidValue;
+    if (value < 0 || value > 4) return (int)hipErrorInvalidValue;
     g_v6_xm = value;
     return 0;
   }
