@@ -235,13 +235,20 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     gradients with both dimensions >= 256 (0 = 128 x 256) */
 #define VU_TUNE_W2_BIG 28
 /*   VU_TUNE_V6_XM: experiment modes of the resident-weight 64 -> 64 kernel
- *     (0 default; 1 = s_setprio around each tap's MFMAs). */
+ *     (0 default; 1 = s_setprio around each tap's MFMAs; 2-4 = timing
+ *     decompositions with wrong results: no in-loop halo DMA, no epilogue
+ *     statistics / stores, fragments read once per group). */
 #define VU_TUNE_V6_XM 29
 /*   VU_TUNE_PP_PERSIST: 1 = the ping-pong kernel's 128/256-column tiles as a
  *     persistent walk (one block per CU; the next tile's first halo and
  *     weights stream in during the current tile's epilogue), 0 (default) =
  *     one tile per block. */
 #define VU_TUNE_PP_PERSIST 30
+/*   VU_TUNE_BN_ONEPASS: 1 (default) = vu_bn_bwd_fused runs tensors of at
+ *     most 8192 pixels (the ResNet34 layer3/4 and the 32^2 / 16^2 decoder
+ *     levels) as ONE launch (a block per 8 channels reduces and applies from
+ *     registers); 0 = the two-launch path. */
+#define VU_TUNE_BN_ONEPASS 31
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was

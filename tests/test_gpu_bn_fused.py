@@ -102,14 +102,17 @@ BWD_CASES = [
     (8, 512, 16, 16, False, True),
     (8, 128, 64, 64, True, True),    # 128 partial blocks: the largest the fused path takes
     (2, 64, 10, 12, True, False),    # eval-mode statistics (constants), ragged pixel count
+    (3, 96, 7, 9, True, True),       # bf16 one-launch path (P <= 8192): P not a multiple of its 512 lanes
+    (2, 64, 64, 64, True, True),     # P = 8192: the largest the bf16 one-launch path takes
 ]
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("case", BWD_CASES)
 def test_bn_bwd_fused_matches_three_launch_path(case, dt):
-    """vu_bn_bwd_fused (partial pass + fp64 finish folded into the apply) vs
-    vu_bn_bwd_reduce + vu_bn_bwd_apply, and vs torch autograd of BN(+ReLU)."""
+    """vu_bn_bwd_fused (partial pass + fp64 finish folded into the apply; bf16
+    tensors of <= 8192 pixels: the one-launch kernel) vs vu_bn_bwd_reduce +
+    vu_bn_bwd_apply, and vs torch autograd of BN(+ReLU)."""
     K = _k()
     from vaeunet_amd import _lib
     N, C, H, W, relu, train = case

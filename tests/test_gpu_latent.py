@@ -6,7 +6,10 @@ bottleneck heads, reparameterize, z_initial and every DecoderBlock z_proj
 gradient of every parameter and the same BatchNorm running statistics as the
 1x1 conv + BatchNorm + ReLU over the broadcast maps (fp32: to summation-order
 noise; bf16: within the storage rounding the map path adds), for each latent
-injection mode, in train and eval mode."""
+injection mode, in train and eval mode -- with the DecoderBlock latent
+shortcut (vae_engine.LATENT_SHORTCUT, csrc/zbias.hip: the z part of conv1
+as a per-sample border-class bias) and without it (the vector path writing
+the maps)."""
 import copy
 
 import pytest
@@ -25,11 +28,12 @@ def _model(inj, seed=0):
     return m.to(DEV).to(memory_format=CL)
 
 
-def _run(model, x, t, eps, vec, bf16, train=True, steps=1):
+def _run(model, x, t, eps, vec, bf16, train=True, steps=1, shortcut=True):
     from vaeunet_amd import vae_engine as V
     from vaeunet_amd.loss import CombinedLoss, kl_with_free_bits
-    old = V.LATENT_VECTORS
+    old, old_sc = V.LATENT_VECTORS, V.LATENT_SHORTCUT
     V.LATENT_VECTORS = vec
+    V.LATENT_SHORTCUT = shortcut
     try:
         model.train(train)
         model.eps_override = eps
@@ -44,6 +48,7 @@ def _run(model, x, t, eps, vec, bf16, train=True, steps=1):
         torch.cuda.synchronize()
     finally:
         V.LATENT_VECTORS = old
+        V.LATENT_SHORTCUT = old_sc
     return outs
 
 
@@ -90,7 +95,8 @@ def _oracle64(model, x, t, eps, inj):
 
 @pytest.mark.parametrize("inj", ["all", "first", "bottleneck", "none", "inject_no_bottleneck"])
 @pytest.mark.parametrize("bf16", [False, True])
-def test_latent_vector_path_matches_map_path(inj, bf16):
+@pytest.mark.parametrize("sc", [True, False])
+def test_latent_vector_path_matches_map_path(inj, bf16, sc):
     """Both paths against the fp64 oracle (one micro-step): every parameter
     gradient of the vector path is at least as close to fp64 as the map
     path's (within a factor), forward outputs and BatchNorm running
@@ -103,7 +109,7 @@ def test_latent_vector_path_matches_map_path(inj, bf16):
     a = _model(inj)
     b = copy.deepcopy(a)
     g64, sigma = _oracle64(a, x, t, eps, inj)
-    ra = _run(a, x, t, eps, True, bf16, steps=1)
+    ra = _run(a, x, t, eps, True, bf16, steps=1, shortcut=sc)
     rb = _run(b, x, t, eps, False, bf16, steps=1)
     tol = 3e-2 if bf16 else 1e-4
     for (la, ma, va, lsa), (lb, mb, vb, lsb) in zip(ra, rb):
@@ -121,7 +127,7 @@ def test_latent_vector_path_matches_map_path(inj, bf16):
         bound[k] = fac * (db + sigma.get(k, 0.0)) + floor * gmax
         worst.append((da / bound[k], k, da, db))
     worst.sort(reverse=True)
-    print(f"{inj} bf16={bf16}: worst (err / bound, name, |vec - fp64|, |map - fp64|) {worst[:3]}")
+    print(f"{inj} bf16={bf16} shortcut={sc}: worst (err / bound, name, |vec - fp64|, |map - fp64|) {worst[:3]}")
     assert worst[0][0] <= 1.0, worst[:5]
     for k in pa:
         if k not in g64:   # no gradient reaches it (z_initial without the bottleneck)
@@ -133,7 +139,7 @@ def test_latent_vector_path_matches_map_path(inj, bf16):
         else:
             assert torch.equal(ba[k], bb[k]), k
     # a second micro-step accumulates into the existing .grad buffers
-    ra = _run(a, x, t, eps, True, bf16, steps=1)
+    ra = _run(a, x, t, eps, True, bf16, steps=1, shortcut=sc)
     rb = _run(b, x, t, eps, False, bf16, steps=1)
     assert _rel(ra[0][0], rb[0][0]) < tol
     for k in g64:
@@ -142,7 +148,8 @@ def test_latent_vector_path_matches_map_path(inj, bf16):
 
 
 @pytest.mark.parametrize("inj", ["all", "bottleneck"])
-def test_latent_vector_path_eval_forward(inj):
+@pytest.mark.parametrize("sc", [True, False])
+def test_latent_vector_path_eval_forward(inj, sc):
     torch.manual_seed(2)
     B, S = 3, 128
     x = torch.rand(B, 3, S, S, device=DEV).contiguous(memory_format=CL)
@@ -153,7 +160,7 @@ def test_latent_vector_path_eval_forward(inj):
     a.zero_grad(set_to_none=True)
     b = copy.deepcopy(a)
     with torch.no_grad():
-        ra = _run(a, x, t, eps, True, False, train=False)
+        ra = _run(a, x, t, eps, True, False, train=False, shortcut=sc)
         rb = _run(b, x, t, eps, False, False, train=False)
     for u, v in zip(ra[0][:3], rb[0][:3]):
         assert _rel(u, v) < 2e-4

@@ -935,6 +935,7 @@ inline unsigned chan_grid16(int64_t P, int C, int maxblk) {
 // dependent load rounds was latency-bound (9 us for the 4 MB of a ResNet34
 // layer3 BN backward).  VU_TUNE_BN_MINBLK, 0 = the 16-row grid only.
 int g_bn_minblk = 256;
+int g_bn_onepass = 1;  // VU_TUNE_BN_ONEPASS (vu_bn_bwd_fused below)
 inline unsigned chan_grid(int64_t P, int C, int maxblk) {
   int R = 256 / (C / 8);
   int64_t g = (P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
@@ -993,6 +994,10 @@ int launch_partial(const RedArgs& r, hipStream_t st, int& nblk, int maxblk = RED
 int bn_tune(int key, int value) {
   if (key == VU_TUNE_BN_NT_MB) {
     g_bn_nt_mb = value;
+    return 0;
+  }
+  if (key == VU_TUNE_BN_ONEPASS) {
+    g_bn_onepass = value ? 1 : 0;
     return 0;
   }
   if (key == VU_TUNE_BN_MINBLK) {
@@ -1271,6 +1276,127 @@ extern "C" int vu_bn_fwd_fused(const float* psum, const float* pm2, int tiles, i
 
 // BatchNorm(+ReLU) backward for small tensors in two launches (the partial
 // pass, then the fused fp64 finish + apply) instead of three.
+// ---- one-launch BatchNorm(+ReLU) backward of a small tensor ---------------
+// (P <= ONEPASS_MAXP: ResNet34 layer3 / layer4 and the 32^2 / 16^2 decoder
+// levels of config 3, where the two launches of the fused path were ~7 us
+// each of mostly latency; bf16): one 512-thread block per 8 channels
+// reduces sum dz and sum dz * xhat over all P pixels (thread t: pixels
+// t + 512 k; fp32 per thread, a fixed-order lane butterfly per wave, fp64
+// across the 8 waves), writes dgamma / dbeta and applies dx.  Deterministic;
+// the same per-element formulas as chan_partial_kernel<.., 1> +
+// bn_bwd_fused_apply_kernel.
+constexpr int ONEPASS_T = 512, ONEPASS_B = 8, ONEPASS_MAXP = 8192;
+constexpr int ONEPASS_W = ONEPASS_T / 64;
+
+VU_DEV float bfly_sum64(float v) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(ONEPASS_T) void bn_bwd_onepass_kernel(BnBwdFusedArgs a) {
+  __shared__ float wsum[2][ONEPASS_W][8];
+  __shared__ float sk[3][8];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int c = blockIdx.x * 8;
+  // 32-bit element offsets from the uniform bases (P * stride < 2^31, host
+  // check) and clamped unconditional loads, ONEPASS_B pixels per thread in
+  // flight; the apply pass re-reads its pixels (L2-resident: <= 256 KB per
+  // block) rather than holding all of them in registers (that spilled)
+  const int P = (int)a.P, dys = (int)a.dys, xs = (int)a.xs;
+  const T* dyc = reinterpret_cast<const T*>(a.dy) + c;
+  const T* xc = reinterpret_cast<const T*>(a.x) + c;
+  float sc[8], sf[8], mu[8], is[8], s0[8], s1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = a.scale[c + i]; sf[i] = a.shift[c + i]; mu[i] = a.mean[c + i]; is[i] = a.invstd[c + i];
+    s0[i] = 0.f; s1[i] = 0.f;
+  }
+  const bool wr = a.accumulate && tid < 8;
+  const float g = tid < 8 ? (a.gamma ? a.gamma[c + tid] : 1.f) : 0.f;
+  const float dg0 = (wr && a.dgamma) ? a.dgamma[c + tid] : 0.f;
+  const float db0 = (wr && a.dbeta) ? a.dbeta[c + tid] : 0.f;
+  for (int p0 = tid; p0 < P; p0 += ONEPASS_T * ONEPASS_B) {
+    Vec8<T> vd[ONEPASS_B], vx[ONEPASS_B];
+#pragma unroll
+    for (int k = 0; k < ONEPASS_B; ++k) {
+      const int p = min(p0 + k * ONEPASS_T, P - 1);
+      vd[k].load(dyc + p * dys);
+      vx[k].load(xc + p * xs);
+    }
+#pragma unroll
+    for (int k = 0; k < ONEPASS_B; ++k) {
+      if (p0 + k * ONEPASS_T >= P) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = vx[k].get(i);
+        float dz = vd[k].get(i);
+        if (a.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+        s0[i] += dz;
+        s1[i] += dz * ((xv - mu[i]) * is[i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float t0 = bfly_sum64(s0[i]), t1 = bfly_sum64(s1[i]);
+    if (lane == 0) {
+      wsum[0][wv][i] = t0;
+      wsum[1][wv][i] = t1;
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    double S0 = 0.0, S1 = 0.0;
+#pragma unroll
+    for (int w = 0; w < ONEPASS_W; ++w) {
+      S0 += (double)wsum[0][w][tid];
+      S1 += (double)wsum[1][w][tid];
+    }
+    const float isc = a.invstd[c + tid];
+    const float k1 = g * isc;
+    sk[0][tid] = k1;
+    sk[1][tid] = a.train ? (float)(-(double)k1 * isc * S1 / (double)a.P) : 0.f;
+    sk[2][tid] = a.train ? (float)(-(double)k1 * S0 / (double)a.P) : 0.f;
+    if (a.dgamma) a.dgamma[c + tid] = a.accumulate ? dg0 + (float)S1 : (float)S1;
+    if (a.dbeta) a.dbeta[c + tid] = a.accumulate ? db0 + (float)S0 : (float)S0;
+  }
+  __syncthreads();
+  float k1[8], k2[8], k3[8];   // block-uniform: scalar registers
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    k1[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sk[0][i])));
+    k2[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sk[1][i])));
+    k3[i] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sk[2][i])));
+  }
+  T* dxc = reinterpret_cast<T*>(a.dx) + c;
+  const int dxs = (int)a.dxs;
+  for (int p0 = tid; p0 < P; p0 += ONEPASS_T * ONEPASS_B) {
+    Vec8<T> vd[ONEPASS_B], vx[ONEPASS_B];
+#pragma unroll
+    for (int k = 0; k < ONEPASS_B; ++k) {
+      const int p = min(p0 + k * ONEPASS_T, P - 1);
+      vd[k].load(dyc + p * dys);
+      vx[k].load(xc + p * xs);
+    }
+#pragma unroll
+    for (int k = 0; k < ONEPASS_B; ++k) {
+      const int p = p0 + k * ONEPASS_T;
+      if (p >= P) continue;
+      Vec8<T> vo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xv = vx[k].get(i);
+        float dz = vd[k].get(i);
+        if (a.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+        vo.set(i, k1[i] * dz + k2[i] * (xv - mu[i]) + k3[i]);
+      }
+      vo.store(dxc + p * dxs);
+    }
+  }
+}
+
 extern "C" int vu_bn_bwd_fused_supported(int64_t P, int C, int64_t dys, int64_t xs, int64_t dxs) {
   return C % 32 == 0 && chanmap_ok(C, dys, xs) && dxs % 8 == 0 && P >= 1 &&
          (int)chan_grid16(P, C, RED_MAXBLK) <= BNB_FUSED_MAXBLK;
@@ -1282,6 +1408,12 @@ extern "C" int vu_bn_bwd_fused(const void* dy, int64_t dys, const void* x, int64
                                int accumulate, void* dx, int64_t dxs, float* workspace, int dtype, void* stream) {
   if (!vu_bn_bwd_fused_supported(P, C, dys, xs, dxs)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  if (g_bn_onepass && dtype == VU_BF16 && P <= ONEPASS_MAXP && dys % 8 == 0 && xs % 8 == 0 && P * (dys > xs ? (dys > dxs ? dys : dxs) : (xs > dxs ? xs : dxs)) < ((int64_t)1 << 31)) {
+    BnBwdFusedArgs a{dy, dys, x, xs, P, C, scale, shift, mean, invstd, gamma, relu, train, nullptr, 0,
+                     dgamma, dbeta, accumulate, dx, dxs, 1};
+    hipLaunchKernelGGL(bn_bwd_onepass_kernel<bf16_t>, dim3((unsigned)(C / 8)), dim3(ONEPASS_T), 0, st, a);
+    return (int)hipGetLastError();
+  }
   RedArgs r{dy, dys, x, xs, P, C, scale, shift, mean, invstd, relu, workspace, 0, 0, 0, 0, 0, 0};
   int nblk = 0, rc;
   rc = dtype == VU_BF16 ? launch_partial<bf16_t, 1>(r, st, nblk, BNB_FUSED_MAXBLK)
