@@ -102,7 +102,7 @@ BWD_CASES = [
     (8, 512, 16, 16, False, True),
     (8, 128, 64, 64, True, True),    # 128 partial blocks: the largest the fused path takes
     (2, 64, 10, 12, True, False),    # eval-mode statistics (constants), ragged pixel count
-    (3, 96, 7, 9, True, True),       # bf16 one-launch path (P <= 8192): P not a multiple of its 512 lanes
+    (3, 128, 7, 9, True, True),      # bf16 one-launch path (P <= 8192): P not a multiple of its 512 lanes
     (2, 64, 64, 64, True, True),     # P = 8192: the largest the bf16 one-launch path takes
 ]
 
