@@ -244,10 +244,10 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     weights stream in during the current tile's epilogue), 0 (default) =
  *     one tile per block. */
 #define VU_TUNE_PP_PERSIST 30
-/*   VU_TUNE_BN_ONEPASS: 1 (default) = vu_bn_bwd_fused runs tensors of at
- *     most 8192 pixels (the ResNet34 layer3/4 and the 32^2 / 16^2 decoder
- *     levels) as ONE launch (a block per 8 channels reduces and applies from
- *     registers); 0 = the two-launch path. */
+/*   VU_TUNE_BN_ONEPASS: 1 = vu_bn_bwd_fused runs bf16 tensors of at most
+ *     8192 pixels as ONE launch (a block per 8 channels reduces and
+ *     applies); 0 (default) = the two-launch path (the one-launch form
+ *     measured 12 % slower on config 3: uncoalesced channel slices). */
 #define VU_TUNE_BN_ONEPASS 31
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,

@@ -935,7 +935,7 @@ inline unsigned chan_grid16(int64_t P, int C, int maxblk) {
 // dependent load rounds was latency-bound (9 us for the 4 MB of a ResNet34
 // layer3 BN backward).  VU_TUNE_BN_MINBLK, 0 = the 16-row grid only.
 int g_bn_minblk = 256;
-int g_bn_onepass = 1;  // VU_TUNE_BN_ONEPASS (vu_bn_bwd_fused below)
+int g_bn_onepass = 0;  // VU_TUNE_BN_ONEPASS (vu_bn_bwd_fused below; measured slower, off)
 inline unsigned chan_grid(int64_t P, int C, int maxblk) {
   int R = 256 / (C / 8);
   int64_t g = (P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
@@ -1284,7 +1284,11 @@ extern "C" int vu_bn_fwd_fused(const float* psum, const float* pm2, int tiles, i
 // t + 512 k; fp32 per thread, a fixed-order lane butterfly per wave, fp64
 // across the 8 waves), writes dgamma / dbeta and applies dx.  Deterministic;
 // the same per-element formulas as chan_partial_kernel<.., 1> +
-// bn_bwd_fused_apply_kernel.
+// bn_bwd_fused_apply_kernel.  MEASURED SLOWER (VAE -12 %, off by default,
+// profiles/r5w_ab_bn_onepass.txt): a block per 8 channels of a channels-last
+// tensor reads 16 bytes per 128-byte line per pixel (every line fetched by
+// C / 8 blocks), and wider channel slices leave C / 64 = 4-8 blocks -- the
+// reduction needs the cross-block stage of the two-launch path.
 constexpr int ONEPASS_T = 512, ONEPASS_B = 8, ONEPASS_MAXP = 8192;
 constexpr int ONEPASS_W = ONEPASS_T / 64;
 
