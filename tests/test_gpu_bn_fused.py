@@ -107,9 +107,10 @@ BWD_CASES = [
 ]
 
 
+@pytest.mark.parametrize("onepass", [0, 1])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("case", BWD_CASES)
-def test_bn_bwd_fused_matches_three_launch_path(case, dt):
+def test_bn_bwd_fused_matches_three_launch_path(case, dt, onepass):
     """vu_bn_bwd_fused (partial pass + fp64 finish folded into the apply; bf16
     tensors of <= 8192 pixels: the one-launch kernel) vs vu_bn_bwd_reduce +
     vu_bn_bwd_apply, and vs torch autograd of BN(+ReLU)."""
@@ -129,12 +130,16 @@ def test_bn_bwd_fused_matches_three_launch_path(case, dt):
     coef = torch.stack([gamma * invstd, beta - mean * gamma * invstd, mean, invstd]).contiguous()
     assert K.query("vu_bn_bwd_fused_supported", N * H * W, C, K.pstride(dy), K.pstride(x), K.pstride(x))
     outs = []
-    for fused in (True, False):
-        dx = torch.empty_like(x)
-        dg, db = torch.full((C,), 0.25, device=DEV), torch.full((C,), -0.5, device=DEV)
-        K.bn_backward(dy, x, coef, gamma, relu, dg, db, True, dx, d, train=train, fused=fused)
-        outs.append((dx, dg, db))
-    torch.cuda.synchronize()
+    _lib.call("vu_gemm_set_tuning", 31, onepass)   # VU_TUNE_BN_ONEPASS (bf16, P <= 8192; off by default)
+    try:
+        for fused in (True, False):
+            dx = torch.empty_like(x)
+            dg, db = torch.full((C,), 0.25, device=DEV), torch.full((C,), -0.5, device=DEV)
+            K.bn_backward(dy, x, coef, gamma, relu, dg, db, True, dx, d, train=train, fused=fused)
+            outs.append((dx, dg, db))
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("vu_gemm_set_tuning", 31, 0)
     (dx1, dg1, db1), (dx2, dg2, db2) = outs
     torch.testing.assert_close(dg1, dg2, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(db1, db2, rtol=1e-5, atol=1e-4)
