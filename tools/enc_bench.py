@@ -2,7 +2,9 @@
 UNetResNet and the UNet(3,2) bottleneck, B=8, 3x512^2 input) through the
 C-ABI: forward and input gradient.
 
-usage: python tools/enc_bench.py [--tune KEY=VAL,...]
+usage: python tools/enc_bench.py [--tune KEY=VAL,...] [--phases]
+--phases: one forward per layer on the small-grid kernel's timing mode
+(VU_TUNE_V7_XM = 5): the share of each phase of its waves' cycles
 (also times the UNet(3,2) small-grid layers: down4 and up1 at B=8)
 """
 import argparse
@@ -48,7 +50,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tune", default="")
     ap.add_argument("--wsplit", type=int, default=0, help="cap on the weight-gradient split-K ways (A/B)")
+    ap.add_argument("--phases", action="store_true")
     args = ap.parse_args()
+    if args.phases:
+        return phases()
     K.WGRAD_SPLIT_CAP = args.wsplit
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
@@ -84,6 +89,46 @@ def main():
               f"dgrad {tb * 1e3:7.1f}us {fl / tb / 1e9:6.0f}TF | wgrad+reduce {tw * 1e3:7.1f}us "
               f"{fl / tw / 1e9:6.0f}TF | row_tile,ws {diag}", flush=True)
     print(f"TOTAL {tot:.3f} ms")
+
+
+def phases():
+    import ctypes as C
+    import numpy as np
+    dev, d = torch.device("cuda"), _lib.BF16
+    lib = _lib.lib()
+    names = ("prologue", "reads+DMA wait", "barrier 1", "MFMA issue", "barrier 2", "epilogue")
+    for name, ci, co, S in LAYERS[:4] + LAYERS[5:6]:
+        x = K.empty_act(B, ci, S, S, torch.bfloat16, dev).normal_()
+        w = torch.randn(co, ci, 3, 3, device=dev) / (3 * ci ** 0.5)
+        y = K.empty_act(B, co, S, S, torch.bfloat16, dev)
+        a = _lib.VuGemmFwd()
+        a.a = K.gather3x3([x])
+        a.b = w3x3_fwd(w, d).data_ptr()
+        a.ldb, a.ncol, a.out, a.out_stride, a.out_mode = 9 * ci, co, y.data_ptr(), K.pstride(y), 0
+        kern = K.query("vu_gemm_fwd_kernel", C.byref(a), d)
+        if kern != 7:
+            print(f"{name}: kernel {kern}, not the small-grid kernel (7)")
+            continue
+        _lib.call("vu_gemm_set_tuning", 18, 5)   # VU_TUNE_V7_XM
+        try:
+            for _ in range(3):
+                K.gemm_fwd(K.gather3x3([x]), w3x3_fwd(w, d), co, y, d, stats=True)
+            torch.cuda.synchronize()
+            buf = (C.c_ulonglong * (64 * 64))()
+            _lib.call("vu_sg_debug_read", buf, 64 * 64)
+        finally:
+            _lib.call("vu_gemm_set_tuning", 18, 0)
+        v = np.frombuffer(buf, dtype=np.uint64).reshape(64, 8, 8).astype(np.float64)
+        tot = v[:, :, :6].sum(-1)
+        ok = tot > 0
+        if not ok.any():
+            print(f"{name}: no counters (split-K launch: the timing mode is unsplit only)")
+            continue
+        share = (v[:, :, :6][ok] / tot[ok][:, None]).mean(0)
+        steps = v[:, :, 6][ok].mean()
+        print(f"{name} {ci}->{co} @{S}: kernel {kern}, {steps:.0f} steps, {tot[ok].mean():.0f} cycles/wave: " +
+              ", ".join(f"{n} {100 * f:.1f}%" for n, f in zip(names, share)) +
+              f" | per step {(v[:, :, 1:5].sum(-1)[ok] / np.maximum(v[:, :, 6][ok], 1)).mean():.0f} cycles", flush=True)
 
 
 if __name__ == "__main__":

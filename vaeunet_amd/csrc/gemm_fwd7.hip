@@ -41,6 +41,11 @@
 #include "../../include/vaeunet.h"
 
 static __device__ __attribute__((aligned(16))) uint32_t vu_zero_page7[16];
+// XM 5 (timing diagnostic): per wave of blocks < SG_DBG_BLOCKS, cycle totals of
+// the phases [prologue, fragment reads + DMA waits, barrier 1, MFMA issue,
+// barrier 2, epilogue, steps, 0] (tools/enc_bench.py --phases)
+constexpr int SG_DBG_BLOCKS = 64;
+static __device__ unsigned long long vu_sg_dbg[SG_DBG_BLOCKS * 8 * 8];
 
 namespace {
 
@@ -108,9 +113,20 @@ struct SG {
 };
 
 // XM (experiment modes, A/B runs only; 0 in production): 2 = no DMA inside
-// the loop, 4 = no loop (launch + prologue + epilogue)
+// the loop, 4 = no loop (launch + prologue + epilogue), 5 = production
+// schedule with per-phase cycle counters (vu_sg_dbg)
 template <int TW, int BN, int NBW, bool SPLIT, int XM = 0, bool RELU = false>  // RELU: epilogue ReLU
 __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
+  constexpr bool TMR = XM == 5;
+  unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto tmark = [&](int k) {
+    if constexpr (TMR) {
+      const unsigned long long t = __builtin_readcyclecounter();
+      tph[k] += t - tlast;
+      tlast = t;
+    }
+  };
+  if constexpr (TMR) tlast = __builtin_readcyclecounter();
   using G = SG<TW, BN, NBW>;
   constexpr int TH = G::TH, HW = G::HW, HALO = G::HALO, HPIECES = G::HPIECES, NH = G::NH;
   constexpr int WTAP = G::WTAP, SLOT = G::SLOT, LB = G::LB, NJ = G::NJ;
@@ -285,6 +301,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
   //   phase 2: the MFMAs.
   // (One tap per step measured 2.5x slower: 8 MFMAs between two barriers do
   // not cover the barrier and LDS-latency cost of a phase.)
+  tmark(0);
   u32x4 fr[18];
   int r = 0, k = 0, hb = 0, slot = 0;
   int pk = PD / 3, pr = PD % 3;  // (pair, row) of step s + PD
@@ -306,7 +323,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int j = 0; j < 18; ++j) tie(fr[j]);
+    tmark(1);
     sg_barrier();
+    tmark(2);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int x = 0; x < 3; ++x)
@@ -318,7 +337,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
                                                               __builtin_bit_cast(bf16x8, fr[6 * x + 4 + i]), acc[i][j],
                                                               0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+    tmark(3);
     sg_barrier();
+    tmark(4);
+    if constexpr (TMR) tph[6] += 1;
     slot = slot == NBW - 1 ? 0 : slot + 1;
     if (++r == 3) {
       r = 0;
@@ -445,6 +467,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_sg_kernel(VuGemmFwd p) {
     ep->stat_sum[(int64_t)mt * ep->ncol + n0 + tid] = tot;
     ep->stat_m2[(int64_t)mt * ep->ncol + n0 + tid] = m2;
   }
+  if constexpr (TMR) {
+    tmark(5);
+    if (blockIdx.x < SG_DBG_BLOCKS && lane == 0) {
+      unsigned long long* d = vu_sg_dbg + ((int64_t)blockIdx.x * 8 + wid) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = tph[i];
+    }
+  }
 }
 
 int g_v7 = 1;      // vu_gemm_set_tuning(VU_TUNE_V7, ...): 0 off, 1 auto, 2 every small grid incl. C >= 512
@@ -494,6 +524,8 @@ int launch7(const VuGemmFwd& p, const Plan7& r, hipStream_t st) {
     hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 4, false, 2>), gr, dim3(512), 0, st, q);
   else if (r.ks <= 1 && g_v7_xm == 4)
     hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 4, false, 4>), gr, dim3(512), 0, st, q);
+  else if (r.ks <= 1 && g_v7_xm == 5 && !p.relu)
+    hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 3, false, 5>), gr, dim3(512), 0, st, q);
   else if (r.ks <= 1 && p.relu)
     hipLaunchKernelGGL((conv3x3_sg_kernel<TW, 64, 3, false, 0, true>), gr, dim3(512), 0, st, q);
   else if (r.ks <= 1 && g_v7_nbw == 3)
@@ -538,6 +570,12 @@ int gemm_fwd_v7_launch(const VuGemmFwd& p, hipStream_t st) {
   VuGemmFwd q = p;
   q.ksplit = r.ks;
   return splitk_finish_launch(q, st);
+}
+
+// XM 5's counters: n = 8 phases x 8 waves x SG_DBG_BLOCKS blocks max
+extern "C" int vu_sg_debug_read(unsigned long long* out, int n) {
+  if (n > SG_DBG_BLOCKS * 64) n = SG_DBG_BLOCKS * 64;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(vu_sg_dbg), (size_t)n * sizeof(unsigned long long));
 }
 
 int gemm_fwd_v7_tune(int key, int value) {
