@@ -249,6 +249,10 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     applies); 0 (default) = the two-launch path (the one-launch form
  *     measured 12 % slower on config 3: uncoalesced channel slices). */
 #define VU_TUNE_BN_ONEPASS 31
+/*   VU_TUNE_STREAM_PD: tiles of operand loads each wave of the 1x1 stream
+ *     kernel (gemm_stream.hip) keeps in flight beyond the one it computes:
+ *     1 or 2. */
+#define VU_TUNE_STREAM_PD 32
 int vu_gemm_set_tuning(int key, int value);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was

@@ -39,8 +39,11 @@ VU_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)
 constexpr int NT = 256;  // 4 waves
 
 // KS: k-steps of 32 (K = 32*KS); NJ: 16-column fragments (N = 16*NJ);
-// NF: 16-pixel fragments per wave tile.
-template <int KS, int NJ, int NF, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
+// NF: 16-pixel fragments per wave tile; PD: tiles of loads in flight per wave
+// beyond the one being computed (1, or 2 = VU_TUNE_STREAM_PD: with 8 waves per
+// CU one tile of loads in flight is ~32 KB per CU, which by Little's law at
+// ~2 us of loaded HBM latency caps the kernel near 4 TB/s).
+template <int KS, int NJ, int NF, bool RELU = false, int PD = 1>  // RELU: epilogue ReLU (VuGemmFwd.relu)
 __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
   constexpr int K = 32 * KS, N = 16 * NJ, PX = 16 * NF;
   constexpr int GS = NJ < 4 ? NJ : 4;   // fragments per column group (4*GS consecutive columns per lane)
@@ -90,9 +93,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
       for (int ks = 0; ks < KS; ++ks)
         dst[f][ks] = *reinterpret_cast<const u32x4*>(src + (pb + 16 * f + r16) * st + 32 * ks + 8 * gq);
   };
-  u32x4 pn[NF][KS];
+  u32x4 pn[NF][KS], pn2[NF][KS];
   int tile = blockIdx.x * (NT / 64) + wid;
   if (tile < ntiles) load(tile, pn);
+  if (PD == 2 && tile + tstride < ntiles) load(tile + tstride, pn2);
   for (; tile < ntiles; tile += tstride) {
     const int64_t pb = (int64_t)tile * PX;
     // opaque LDS offset: the weight fragments and bias are re-read per tile
@@ -105,7 +109,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_stream_kernel(VuGemmFwd p) {
     for (int f = 0; f < NF; ++f)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) pf[f][ks] = pn[f][ks];
-    if (tile + tstride < ntiles) load(tile + tstride, pn);
+    if constexpr (PD == 2) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) pn[f][ks] = pn2[f][ks];
+      if (tile + 2 * tstride < ntiles) load(tile + 2 * tstride, pn2);
+    } else {
+      if (tile + tstride < ntiles) load(tile + tstride, pn);
+    }
     f32x4 acc[NF][NJ];
 #pragma unroll
     for (int f = 0; f < NF; ++f)
@@ -279,6 +291,8 @@ constexpr int nf_of(int ks, int nj) {
   return (16 / nj < 4 ? 16 / nj : 4) < (8 / ks) ? (16 / nj < 4 ? 16 / nj : 4) : 8 / ks;
 }
 
+int g_pd = 1;  // VU_TUNE_STREAM_PD
+
 template <int KS, int NJ>
 int launch_nj(const VuGemmFwd& p, hipStream_t st) {
   constexpr int NF = nf_of(KS, NJ);
@@ -289,6 +303,8 @@ int launch_nj(const VuGemmFwd& p, hipStream_t st) {
   if (nblk > cap) nblk = cap;
   if (p.relu)
     hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF, true>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
+  else if (g_pd == 2)
+    hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF, false, 2>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
   else
     hipLaunchKernelGGL((gemm_stream_kernel<KS, NJ, NF>), dim3((unsigned)nblk), dim3(NT), 0, st, p);
   return (int)hipGetLastError();
@@ -348,6 +364,11 @@ int gemm_stream_launch(const VuGemmFwd& p, hipStream_t st) {
 int gemm_stream_tune(int key, int value) {
   if (key == VU_TUNE_STREAM) {
     g_enabled = value != 0;
+    return 0;
+  }
+  if (key == VU_TUNE_STREAM_PD) {
+    if (value != 1 && value != 2) return (int)hipErrorInvalidValue;
+    g_pd = value;
     return 0;
   }
   return -1;
