@@ -136,7 +136,7 @@ VU_DEV void bfly16_bcast(float m, int lane, float (&out)[16]) {
 // statistics and the output stores predicated off by a value test the
 // compiler cannot fold (the MFMAs stay live: the epilogue's share); 4 = the
 // fragments read once per group, not per tap (the LDS-read share); results
-// wrong in 2-4
+// wrong in 2-4; 5 = the output stores non-temporal (results exact)
 template <bool STATS, bool RELU = false, int XM = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -231,7 +231,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   };
   auto store_pend = [&](int q) {  // piece q = 2 * fragment + half
     bf16_t* o = pdst + ((q >> 2) * (int64_t)W + ((q >> 1) & 1) * 16) * p.out_stride + 32 * (q & 1);
-    if (XM != 3 || pend[q][0] == 0x7fc17fc1u) *reinterpret_cast<u32x4*>(o) = pend[q];
+    if constexpr (XM == 5)
+      __builtin_nontemporal_store(pend[q], reinterpret_cast<u32x4*>(o));
+    else if (XM != 3 || pend[q][0] == 0x7fc17fc1u)
+      *reinterpret_cast<u32x4*>(o) = pend[q];
   };
 
   // the 9 taps of one group over halo buffer b, chunk c; `pending` stores
@@ -447,6 +450,7 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
     else if (g_v6_xm == 2) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 2>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 3>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 4) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 4>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 5) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 5>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
   else
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
@@ -454,13 +458,14 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
     else if (g_v6_xm == 2) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 2>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 3) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 3>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 4) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 4>), dim3((unsigned)grid), dim3(512), 0, st, p);
+    else if (g_v6_xm == 5) hipLaunchKernelGGL((conv3x3_c64_kernel<false, false, 5>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else hipLaunchKernelGGL(conv3x3_c64_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
   return (int)hipGetLastError();
 }
 
 int gemm_fwd_v6_tune(int key, int value) {
   if (key == VU_TUNE_V6_XM) {
-    if (value < 0 || value > 4) return (int)hipErrorInvalidValue;
+    if (value < 0 || value > 5) return (int)hipErrorInvalidValue;
     g_v6_xm = value;
     return 0;
   }
