@@ -75,6 +75,9 @@ def parse():
                          "MODULE.NAME for another vaeunet_amd module, e.g. vae_engine.LATENT_VECTORS=0")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VAL",
                     help="vu_gemm_set_tuning(KEY, VAL) before the run (library A/B runs; include/vaeunet.h)")
+    ap.add_argument("--unsafe-experiment", action="store_true",
+                    help="allow --tune experiment modes (VU_TUNE_UNSAFE + *_XM: wrong results by design); "
+                         "the JSON line then carries experiment_modes")
     ap.add_argument("--overlap", action="store_true",
                     help="weight gradients on a side stream (engine.OVERLAP_WGRAD; measured slower, A/B only)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
@@ -398,8 +401,22 @@ def main():
             raise SystemExit(f"bench: no engine switch {name}")
         old = getattr(mod, name)
         # keep the knob's type: a bool switch stays a bool, an integer knob
-        # (e.g. kernels.WGRAD_SPLIT_CAP=4) keeps its value
-        setattr(mod, name, bool(int(val)) if isinstance(old, bool) else type(old)(int(val)))
+        # (e.g. kernels.WGRAD_SPLIT_CAP=4) an int, a float knob (e.g.
+        # kernels._W3_SLAB_BPS=4.5e12) a float
+        if isinstance(old, bool):
+            new = bool(int(val))
+        elif isinstance(old, int):
+            new = int(val)
+        elif isinstance(old, float):
+            new = float(val)
+        else:
+            raise SystemExit(f"bench: engine knob {name} has type {type(old).__name__}; bool/int/float only")
+        setattr(mod, name, new)
+    from vaeunet_amd import _lib as _L
+    xm = _L.query("vu_gemm_experiment_modes")
+    if xm and not args.unsafe_experiment:
+        raise SystemExit(f"bench: experiment modes active (mask {xm}): results are not valid; "
+                         "pass --unsafe-experiment for a timing decomposition run")
     from vaeunet_amd.loss import CombinedLoss
     from vaeunet_amd import parallel
 
@@ -546,6 +563,8 @@ def main():
                 "roofline": roof, "cpu_baseline": cpu, "parity": parity}
         if secondary is not None:
             line["secondary"] = secondary
+        if xm:
+            line["experiment_modes"] = xm  # --unsafe-experiment: a timing decomposition, not a result
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

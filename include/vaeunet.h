@@ -253,7 +253,15 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     kernel (gemm_stream.hip) keeps in flight beyond the one it computes:
  *     1 or 2. */
 #define VU_TUNE_STREAM_PD 32
+/*   VU_TUNE_UNSAFE: 1 = allow the experiment modes (VU_TUNE_V6_XM,
+ *     VU_TUNE_V7_XM, VU_TUNE_FP8_XM) to be set non-zero; several of them
+ *     produce wrong results by design (timing decompositions).  Without it a
+ *     non-zero experiment mode is refused (hipErrorInvalidValue). */
+#define VU_TUNE_UNSAFE 33
 int vu_gemm_set_tuning(int key, int value);
+/* Bit mask of the experiment modes currently non-zero (bit 0 V6_XM, 1 V7_XM,
+ * 2 FP8_XM): 0 in production.  bench.py refuses to report while it is not. */
+int vu_gemm_experiment_modes(void);
 /* ABI check: out[0..7] = sizeof VuGather, VuGemmFwd, VuGemmWgrad, VuConvFp8,
  * VuPermJob, VuMtEntry, VuLatentJob, VuLatentHeads as this library was
  * compiled (bindings compare their own struct sizes against it;

@@ -35,18 +35,20 @@ def _run(model, x, fold, bf16):
     return out if isinstance(out, tuple) else (out,)
 
 
-@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("bf16,batch", [(False, 2), (True, 2), (True, 8)])
 @pytest.mark.parametrize("family", ["unet", "vae"])
-def test_eval_bn_folding_matches_unfolded(family, bf16):
+def test_eval_bn_folding_matches_unfolded(family, bf16, batch):
+    """batch 8 at 512^2 puts the VAE decoder blocks' conv1 (latent shortcut
+    table + folded BN + ReLU) on the ping-pong kernel."""
     from vaeunet_amd import UNet, UNetResNet
     from vaeunet_amd.init import seeded_init_
     g = torch.Generator().manual_seed(3)
     if family == "unet":
         model = UNet(3, 2)
-        x = torch.randn(2, 3, 128, 128, generator=g)
+        x = torch.randn(batch, 3, 128, 128, generator=g)
     else:
         model = UNetResNet(3, 1, pretrained=False)
-        x = torch.randn(2, 3, 512, 512, generator=g)
+        x = torch.randn(batch, 3, 512, 512, generator=g)
     model = seeded_init_(model, 0)
     _randomise_bn(model, g)
     model = model.to(DEV).to(memory_format=torch.channels_last).eval()

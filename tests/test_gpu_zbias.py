@@ -55,11 +55,14 @@ FWD_CASES = [
 ]
 
 
+@pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("case", FWD_CASES)
-def test_zbias_forward_matches_concat_conv(case):
+def test_zbias_forward_matches_concat_conv(case, relu):
     """conv over [sources] + zbias == conv over [sources, broadcast z map]
     (the map holds the storage-rounded vectors), per element within the
-    GEMM bound, with the BatchNorm statistics of the stored output."""
+    GEMM bound, with the BatchNorm statistics of the stored output.  relu:
+    the folded eval-BN inference form (VuGemmFwd.relu with the table, ADVICE
+    r5: the ping-pong kernel's ZB instantiation ignored p.relu)."""
     from vaeunet_amd import kernels as K, engine as E
     N, cins, L, H, W, co, mode, tune, kern = case
     dt = torch.bfloat16 if mode == "bf16" else torch.float32
@@ -87,8 +90,9 @@ def test_zbias_forward_matches_concat_conv(case):
         a.b, a.ldb, a.ncol = wm.data_ptr(), wm.shape[-1], co
         a.out, a.out_stride, a.out_mode = out.data_ptr(), K.pstride(out), 0
         a.zbias = table.data_ptr()
+        a.relu = 1 if relu else 0
         assert K.query("vu_gemm_fwd_kernel", C.byref(a), d) == kern
-        st = K.gemm_fwd(K.gather3x3(srcs), wm, co, out, d, stats=True, zbias=table)
+        st = K.gemm_fwd(K.gather3x3(srcs), wm, co, out, d, stats=True, zbias=table, relu=relu)
     finally:
         _tune(*TUNE_DEFAULTS)
     zmap = act.cpu()[:, :, None, None].expand(N, L, H, W)
@@ -98,6 +102,9 @@ def test_zbias_forward_matches_concat_conv(case):
     wz = torch.cat([wq[:, :lead], w.cpu()[:, lead:]], 1)
     ref = F.conv2d(xcat.double(), wz.double(), padding=1)
     sab = F.conv2d(xcat.abs().double(), wz.abs().double(), padding=1)
+    if relu:
+        assert float(ref.min()) < 0  # the case exercises the clamp
+        ref = ref.clamp_min(0)
     got = out.double().cpu()
     u = 2.0 ** -8 if mode == "bf16" else 2.0 ** -24
     bound = u * torch.maximum(ref.abs(), got.abs()) + 1e-5 * sab + 1e-7 * float(ref.abs().max())

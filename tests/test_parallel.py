@@ -163,3 +163,60 @@ def test_grad_accumulation_no_sync_gloo():
                 # sum over the two micro-batches, averaged over the two ranks
                 want = sum(float(10 * rr + mb + 1 + opt_step) for rr in range(world) for mb in range(2)) / world * k
                 assert torch.allclose(torch.from_numpy(g), torch.full_like(torch.from_numpy(g), want)), (r, opt_step, i)
+
+
+def _late_worker(rank, world, port, out_q):
+    """A parameter the engine never reports (grad_ready) whose gradient is
+    zero on step 0 and non-zero from step 1 on: the reducer must drop it only
+    while it is zero (the round-5 reducer cached "unused" from the
+    first step and dropped the later gradients for good)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vaeunet_amd.parallel import GradBucketReducer
+        m = _model()
+        red = GradBucketReducer(m.parameters(), bucket_bytes=4096)
+        params = list(m.parameters())
+        late = params[2]  # never reported
+        out = []
+        for step in range(3):
+            for q in params:
+                q.grad = None
+            red.prepare()
+            for i, p in enumerate(reversed(params)):
+                if p is late:
+                    if step >= 1:
+                        p.grad.add_(float(rank + 1 + step))
+                    continue
+                p.grad.add_(torch.full_like(p, float(rank + 1)))
+                red.grad_ready([p])
+            red.finish()
+            out.append(None if late.grad is None else late.grad.detach().numpy().copy())
+        out_q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unreported_parameter_late_gradient_gloo():
+    world = 2
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.environ["PYTHONPATH"] = os.pathsep.join(
+        [os.path.dirname(here), here] + [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_late_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        g0, g1, g2 = res[r]
+        assert g0 is None, "a zero, unreported gradient must be reset to None"
+        for step, g in ((1, g1), (2, g2)):
+            assert g is not None, f"late gradient dropped on step {step}"
+            want = sum(float(rr + 1 + step) for rr in range(world)) / world
+            assert torch.allclose(torch.from_numpy(g), torch.full_like(torch.from_numpy(g), want)), (r, step)

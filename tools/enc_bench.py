@@ -109,6 +109,7 @@ def phases():
         if kern != 7:
             print(f"{name}: kernel {kern}, not the small-grid kernel (7)")
             continue
+        _lib.call("vu_gemm_set_tuning", 33, 1)   # VU_TUNE_UNSAFE: experiment modes allowed
         _lib.call("vu_gemm_set_tuning", 18, 5)   # VU_TUNE_V7_XM
         try:
             for _ in range(3):

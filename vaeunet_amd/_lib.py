@@ -104,6 +104,7 @@ _SIGS = {
     "vu_gemm_wgrad": (_i, [C.POINTER(VuGemmWgrad), _i, _p]),
     "vu_gemm_wgrad_tile": (_i, [C.POINTER(VuGemmWgrad), _i, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "vu_gemm_set_tuning": (_i, [_i, _i]),
+    "vu_gemm_experiment_modes": (_i, []),
     "vu_slab_reduce": (_i, [_p, _i, _i, _i, _i, _i, _l, _l, _l, _p, _i, _p]),
     "vu_amax": (_i, [_p, _l, _l, _i, _p, _i, _i, _p]),
     "vu_quant_fp8": (_i, [_p, _l, _l, _i, _p, _p, _l, _p, _i, _p]),

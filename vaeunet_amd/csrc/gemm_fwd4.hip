@@ -893,7 +893,10 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
   if (ks <= 1) {
     VuGemmFwd q = p;
     q.ksplit = 1;
-    if (p.zbias)
+    if (p.zbias && p.relu)  // folded eval-BN DecoderBlock conv1 (inference): bias table + ReLU epilogue
+      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true, BN != 64, true>), dim3((unsigned)tiles),
+                         dim3(512), 0, st, q);
+    else if (p.zbias)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64, true>), dim3((unsigned)tiles),
                          dim3(512), 0, st, q);
     else if (p.bnb_part)
@@ -1000,7 +1003,34 @@ extern int g_tune_gen;                     // gemm_fwd.hip
 extern int g_tune_slab4;                   // gemm_wgrad.hip
 extern int g_v2_cfg;                       // gemm_fwd2.hip
 
+namespace {
+int g_tune_unsafe = 0;  // VU_TUNE_UNSAFE
+int g_xm_modes = 0;     // vu_gemm_experiment_modes()
+int xm_bit(int key) {
+  return key == VU_TUNE_V6_XM ? 1 : key == VU_TUNE_V7_XM ? 2 : key == VU_TUNE_FP8_XM ? 4 : 0;
+}
+int set_tuning(int key, int value);
+}  // namespace
+
+// Experiment modes (timing decompositions, several with wrong results by
+// design) are refused unless VU_TUNE_UNSAFE was set first, and
+// tracked so that a benchmark can refuse to report while one is active.
 extern "C" int vu_gemm_set_tuning(int key, int value) {
+  if (key == VU_TUNE_UNSAFE) {
+    g_tune_unsafe = value != 0;
+    return 0;
+  }
+  const int bit = xm_bit(key);
+  if (bit && value != 0 && !g_tune_unsafe) return (int)hipErrorInvalidValue;
+  const int r = set_tuning(key, value);
+  if (r == 0 && bit) g_xm_modes = value != 0 ? (g_xm_modes | bit) : (g_xm_modes & ~bit);
+  return r;
+}
+
+extern "C" int vu_gemm_experiment_modes(void) { return g_xm_modes; }
+
+namespace {
+int set_tuning(int key, int value) {
   if (key == VU_TUNE_V4_MIN_BLOCKS) {
     g_min_blocks = value;
     return 0;
@@ -1042,3 +1072,4 @@ extern "C" int vu_gemm_set_tuning(int key, int value) {
     return 0;
   return (int)hipErrorInvalidValue;
 }
+}  // namespace

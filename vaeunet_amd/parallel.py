@@ -52,7 +52,8 @@ class GradBucketReducer:
         self._pending = None
         self._handles = []
         self._sync = True
-        self._unused = {}          # id(param) -> reported-never AND zero slot (finish())
+        self._unused = {}          # id(param) -> unreported AND zero slot on the last eager step (finish())
+        self._used = set()         # id(param) of unreported parameters once seen non-zero (kept for good)
         with torch.no_grad():
             for p in self.params:
                 dist.broadcast(p.data, src=0, group=group)
@@ -150,14 +151,17 @@ class GradBucketReducer:
 
         A parameter the engine never reported during a synchronised backward
         AND whose reduced gradient slot is exactly zero on every rank received
-        no gradient (UNetResNet's z_initial when use_bottleneck is False): its
-        ``.grad`` is reset to None afterwards -- torch semantics, so the
-        optimizer skips it (no AdamW state, no weight decay) as it would
-        without the reducer.  A non-zero slot is kept: a backward path that
-        forgot to report a parameter only delays its bucket, it never drops a
-        real gradient.  The zero test is a host read, made once
-        per parameter on an eager step and cached; while a graph is being
-        captured an undecided parameter keeps its gradient."""
+        no gradient this step (UNetResNet's z_initial when use_bottleneck is
+        False): its ``.grad`` is reset to None afterwards -- torch semantics,
+        so the optimizer skips it (no AdamW state, no weight decay) as it
+        would without the reducer.  A non-zero slot is kept: a backward path
+        that forgot to report a parameter only delays its bucket, it never
+        drops a real gradient.  Only "used" is cached: a parameter found zero
+        is re-tested (one host read) on every later eager step until its slot
+        is non-zero once, so a gradient that first arrives on step k > 1
+        (zero-initialised downstream weight, a dead ReLU, a branch warming up)
+        is kept from step k on.  While a graph is being captured
+        the last eager observation decides."""
         if not self._sync:
             return
         unseen = []
@@ -176,12 +180,18 @@ class GradBucketReducer:
         self._pending = None
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         for p in unseen:
-            unused = self._unused.get(id(p))
-            if unused is None and not capturing and p.grad is not None:
-                unused = bool(torch.count_nonzero(p.grad).item() == 0)
-                self._unused[id(p)] = unused
-            if unused:
+            if id(p) in self._used:
+                continue
+            if capturing or p.grad is None:
+                if self._unused.get(id(p)):
+                    p.grad = None
+                continue
+            if bool(torch.count_nonzero(p.grad).item() == 0):
+                self._unused[id(p)] = True
                 p.grad = None
+            else:
+                self._used.add(id(p))
+                self._unused.pop(id(p), None)
 
 
 def attach(model, **kw):
