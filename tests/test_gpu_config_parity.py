@@ -175,6 +175,41 @@ def _ref_bf16_run(R, state, x, t, eps, names, probe=False):
 # (HIP must not drift more than the reference's own bf16 path).
 REF_PERTURB = (2.0 ** -13, 2.0 ** -12, 2.0 ** -11.5, 2.0 ** -11, 2.0 ** -10.5, 2.0 ** -10)
 DZ_VS_REF = 1.05
+# per-gradient norm drift cap of the config-3 bf16 test (VERDICT r5 "do this"
+# 1): every BatchNorm-affine gradient's bench-input norm drift within 2x the
+# reference's own bf16 ensemble max + 5 %
+BF16_GNORM_VS_ENS = 2.0
+
+
+class _DzRecorder:
+    """Records dz = dL/d(BatchNorm output) (the ReLU mask applied) at every
+    BatchNorm the engine's bn_bwd serves, keyed by the module's state_dict
+    prefix (the oracle PROBE's key), as CPU fp64/fp32 tensors."""
+
+    def __init__(self, model, dtype=torch.float32):
+        from vaeunet_amd import engine as E
+        self.E, self.dtype, self.dz = E, dtype, {}
+        self.names = {id(mod): n + "." for n, mod in model.named_modules() if isinstance(mod, torch.nn.BatchNorm2d)}
+
+    def __enter__(self):
+        E = self.E
+        self.orig = orig = E.bn_bwd
+
+        def bn_bwd(dy, xx, coef, bn, relu, M, *a, **kw):
+            pre = self.names.get(id(bn))
+            if pre is not None:
+                d = (dy.materialize(M) if isinstance(dy, E.PoolGrad) else dy).detach().float()
+                if relu:
+                    C_ = xx.shape[1]
+                    d = d * ((xx.float() * coef[0].view(1, C_, 1, 1) + coef[1].view(1, C_, 1, 1)) > 0).float()
+                self.dz[pre] = d.to(self.dtype).cpu()
+            return orig(dy, xx, coef, bn, relu, M, *a, **kw)
+        E.bn_bwd = bn_bwd
+        return self
+
+    def __exit__(self, *a):
+        self.E.bn_bwd = self.orig
+        return False
 
 
 @pytest.mark.timeout(900)
@@ -218,27 +253,12 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
 
     model = model.to(DEV).to(memory_format=CL).train()
     model.eps_override = eps
-    bn_name = {id(mod): n + "." for n, mod in model.named_modules() if isinstance(mod, torch.nn.BatchNorm2d)}
-    dz_hip = {}
-    orig = E.bn_bwd
-
-    def bn_bwd(dy, xx, coef, bn, relu, M, *a, **kw):   # records dz = dL/d(BN output) per BatchNorm
-        pre = bn_name.get(id(bn))
-        if pre is not None and not isinstance(dy, E.PoolGrad):
-            d = dy.detach().float()
-            if relu:
-                C_ = xx.shape[1]
-                d = d * ((xx.float() * coef[0].view(1, C_, 1, 1) + coef[1].view(1, C_, 1, 1)) > 0).float()
-            dz_hip[pre] = d.cpu()
-        return orig(dy, xx, coef, bn, relu, M, *a, **kw)
-    E.bn_bwd = bn_bwd
-    try:
+    with _DzRecorder(model) as rec:
         with torch.autocast("cuda", dtype=torch.bfloat16):
             lg, mu, lv = model(x.to(DEV))
             loss = CombinedLoss()(lg, t.to(DEV)) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
         loss.backward()
-    finally:
-        E.bn_bwd = orig
+    dz_hip = rec.dz
     lg = lg.detach().float().cpu().contiguous()
     max_rel, rms_rel = _drift(lg, lref)
     flips = int(((lg > 0) != (lref > 0)).sum())
@@ -328,6 +348,13 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
               f"(mean {mean_hip[i]:.4f}), CPU-bf16 {[round(float(abs(g[i] - gref[i]) / gref[i]), 4) for g in g16_ens]} "
               f"(mean {mean_ref[i]:.4f})")
     assert worst_b < BF16_GNORM, worst_bl
+    # and each BatchNorm-affine gradient's own bench-input norm drift (round 4's
+    # per-gradient cap, restored at 2x the reference's ensemble max + 5 %)
+    capv = sorted(((grel[i] - BF16_GNORM_VS_ENS * grel_ens[i], names[i], grel[i], grel_ens[i]) for i in bbig),
+                  reverse=True)
+    print(f"config3 bf16: BN-affine norm drift worst (excess over {BF16_GNORM_VS_ENS}x ensemble max, name, HIP, "
+          f"CPU-bf16 ensemble max) {[(round(float(a_), 4), b_, round(float(c_), 4), round(float(d_), 4)) for a_, b_, c_, d_ in capv[:3]]}")
+    assert capv[0][0] <= BF16_GNORM, capv[:3]
     vecs = {k: (params[k].grad.double().cpu().reshape(-1), ref.p[k].grad.double().reshape(-1),
                 ref16.p[k].grad.double().reshape(-1)) for k in (names[i] for i in bbig)}
     num = sum(float((a - r_).pow(2).sum()) for a, r_, _ in vecs.values()) ** 0.5
@@ -371,13 +398,22 @@ def test_unetresnet_config3_bf16_b8_vs_oracle():
 # floor 1e-5 * max ||g||" instead, and the exact zeros are counted.
 # ---------------------------------------------------------------------------
 GRAD_ERR_FACTOR = 4.0
+GRAD_VS_ORACLE = 1.5
+SIGMA_CAP = 0.5
 U32 = 2.0 ** -24
 BW_B = 2
 
 
 def _grad_adjudicate(tag, names, g_hip, g32, g64, sigma):
+    """Every gradient k: ||g_hip - g64|| <= GRAD_VS_ORACLE * (||g32 - g64|| +
+    u32 ||g64||) -- the HIP fp32 path within 1.5x the fp32 oracle's own error.
+    A gradient outside it is re-judged on the term-spread bound
+    GRAD_ERR_FACTOR * (||g32 - g64|| + sigma_k + u32 ||g64||) ONLY when that
+    bound stays below SIGMA_CAP * ||g64|| (a sigma-dominated bound
+    of ~1.2 |g| passed a 100 %-wrong gradient); one whose bound would exceed
+    it is 'unpinnable' and fails."""
     gmax = max(float(g.norm()) for g in g64.values())
-    worst, zero = [], []
+    rows, zero, spread, unpin = [], [], [], []
     for k in names:
         r = float(g64[k].norm())
         if r <= 1e-9 * gmax:
@@ -388,15 +424,24 @@ def _grad_adjudicate(tag, names, g_hip, g32, g64, sigma):
         d_h = float((g_hip[k] - g64[k]).norm())
         d_32 = float((g32[k] - g64[k]).norm())
         s = sigma.get(k, 0.0)
-        # > 1: outside the bound
-        worst.append((d_h / (GRAD_ERR_FACTOR * (d_32 + s + U32 * r)), k, d_h / r, d_32 / r, s / r))
-    worst.sort(reverse=True)
-    print(f"{tag}: {len(worst)} gradients adjudicated vs fp64 ({len(sigma)} BatchNorm-affine with a term "
-          f"spread), {len(zero)} mathematically zero ({sum(zero)} written as exact zeros); worst "
-          f"(err / bound, name, HIP rel err, fp32-oracle rel err, term spread / |g|): "
-          f"{[(f'{a:.2e}', b, f'{c:.2e}', f'{d:.2e}', f'{e:.2e}') for a, b, c, d, e in worst[:4]]}")
-    assert worst[0][0] <= 1.0, worst[:4]
-    return worst
+        ratio = d_h / (GRAD_VS_ORACLE * (d_32 + U32 * r))   # > 1: outside the primary bound
+        rows.append((ratio, k, d_h / r, d_32 / r, s / r))
+        if ratio > 1.0:
+            b2 = GRAD_ERR_FACTOR * (d_32 + s + U32 * r)
+            if b2 > SIGMA_CAP * r:
+                unpin.append((k, d_h / r, d_32 / r, s / r))
+            else:
+                spread.append((d_h / b2, k, d_h / r, d_32 / r, s / r))
+    rows.sort(reverse=True)
+    print(f"{tag}: {len(rows)} gradients vs fp64, {len(zero)} mathematically zero ({sum(zero)} written as exact "
+          f"zeros); worst (HIP err / ({GRAD_VS_ORACLE} x fp32-oracle err), name, HIP rel, fp32-oracle rel, term "
+          f"spread / |g|): {[(f'{a:.2f}', b, f'{c:.2e}', f'{d:.2e}', f'{e:.2e}') for a, b, c, d, e in rows[:5]]}; "
+          f"median HIP/oracle {sorted(r[2] / max(r[3], 1e-300) for r in rows)[len(rows) // 2]:.3f}; "
+          f"{len(spread)} judged on the capped term spread {[(f'{a:.2f}', b) for a, b, *_ in sorted(spread, reverse=True)[:4]]}; "
+          f"unpinnable {unpin}")
+    assert not unpin, unpin
+    assert all(a <= 1.0 for a, *_ in spread), sorted(spread, reverse=True)[:4]
+    return rows
 
 
 def _bw_batch(classes):
@@ -433,12 +478,41 @@ def _oracle_grads(fwd, state, dtype, probe=False):
 
 
 def _oracle_pair(fwd, state):
-    """fp64 and fp32 oracle gradients + the per-BatchNorm term spreads sigma."""
+    """fp64 and fp32 oracle gradients, the per-BatchNorm term spreads sigma,
+    the fp64 dz at every BatchNorm and the fp32 oracle's own error on it."""
     g64, loss64, t64 = _oracle_grads(fwd(torch.float64), state, torch.float64, probe=True)
     g32, _, t32 = _oracle_grads(fwd(torch.float32), state, torch.float32, probe=True)
     sigma = {k: float((t32[k] - t64[k]).norm()) for k in t64 if k in t32}
+    dz64 = {k[:-4]: t64[k] for k in t64 if k.endswith("bias")}
+    dzerr32 = {pre: float((t32[pre + "bias"] - d).norm()) for pre, d in dz64.items() if pre + "bias" in t32}
     del t32, t64
-    return g32, g64, loss64, sigma
+    return g32, g64, loss64, sigma, dz64, dzerr32
+
+
+# dz = dL/d(BatchNorm output) at every BatchNorm the engine's backward serves,
+# elementwise vs fp64: the HIP fp32 path's error within DZ32_FACTOR x the fp32
+# oracle's own (VERDICT r5 "do this" 1: the error a gradient carries arrives
+# with dz -- tools/psi_probe.py -- so this pins its source directly, at every
+# depth, independent of how ill-conditioned the affine sums over it are)
+DZ32_FACTOR = 1.5
+
+
+def _dz_adjudicate(tag, dz_hip, dz64, dzerr32):
+    rows = []
+    for pre, d64 in dz64.items():
+        if pre not in dz_hip or pre not in dzerr32:
+            continue
+        nrm = float(d64.norm())
+        if nrm == 0:
+            continue
+        e_h = float((dz_hip[pre].double() - d64).norm())
+        rows.append((e_h / (DZ32_FACTOR * dzerr32[pre] + U32 * nrm), pre, e_h / nrm, dzerr32[pre] / nrm))
+    rows.sort(reverse=True)
+    print(f"{tag}: dz at {len(rows)} BatchNorms vs fp64, worst (HIP err / ({DZ32_FACTOR} x fp32-oracle err), "
+          f"name, HIP rel, fp32-oracle rel): {[(f'{a:.3f}', b, f'{c:.2e}', f'{d:.2e}') for a, b, c, d in rows[:4]]}; "
+          f"median ratio HIP/oracle {sorted(r[2] / r[3] for r in rows)[len(rows) // 2]:.3f}")
+    assert rows and rows[0][0] <= 1.0, rows[:4]
+    return rows
 
 
 @pytest.mark.timeout(900)
@@ -455,13 +529,16 @@ def test_unet_config2_fp32_backward_512_vs_fp64():
 
     def fwd(dtype):
         return lambda p, b: R.combined_loss(R.unet_forward(x.to(dtype), p, b, True), t.to(dtype))
-    g32, g64, loss64, sigma = _oracle_pair(fwd, state)
+    g32, g64, loss64, sigma, dz64, dzerr32 = _oracle_pair(fwd, state)
     model = model.to(DEV).to(memory_format=CL).train()
-    loss = CombinedLoss()(model(x.to(DEV)), t.to(DEV))
-    loss.backward()
+    with _DzRecorder(model) as rec:
+        loss = CombinedLoss()(model(x.to(DEV)), t.to(DEV))
+        loss.backward()
     assert abs(float(loss.detach()) - loss64) < 1e-5
     params = dict(model.named_parameters())
     gh = {k: params[k].grad.detach().double().cpu() for k in names}
+    dzrows = _dz_adjudicate("config2 fp32 backward B=2 512^2", rec.dz, dz64, dzerr32)
+    assert len(dzrows) >= 18   # every DoubleConv BatchNorm (the attention-gate BNs run inside their kernels)
     _grad_adjudicate("config2 fp32 backward B=2 512^2", names, gh, g32, g64, sigma)
 
 
@@ -483,13 +560,16 @@ def test_unetresnet_config3_fp32_backward_512_vs_fp64():
             lg, mu, lv = R.unet_resnet_forward(x.to(dtype), p, b, eps=eps.to(dtype))
             return R.combined_loss(lg, t.to(dtype)) + 1e-3 * R.kl_with_free_bits(mu, lv, 1e-3)
         return f
-    g32, g64, loss64, sigma = _oracle_pair(fwd, state)
+    g32, g64, loss64, sigma, dz64, dzerr32 = _oracle_pair(fwd, state)
     model = model.to(DEV).to(memory_format=CL).train()
     model.eps_override = eps.to(DEV)
-    lg, mu, lv = model(x.to(DEV))
-    loss = CombinedLoss()(lg, t.to(DEV)) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
-    loss.backward()
+    with _DzRecorder(model) as rec:
+        lg, mu, lv = model(x.to(DEV))
+        loss = CombinedLoss()(lg, t.to(DEV)) + 1e-3 * kl_with_free_bits(mu, lv, free_bits=1e-3)
+        loss.backward()
     assert abs(float(loss.detach()) - loss64) < 1e-5
+    dzrows = _dz_adjudicate("config3 fp32 backward B=2 512^2", rec.dz, dz64, dzerr32)
+    assert len(dzrows) >= 50
     params = dict(model.named_parameters())
     gh = {k: (params[k].grad.detach().double().cpu() if params[k].grad is not None
               else torch.zeros_like(params[k], dtype=torch.float64, device="cpu")) for k in names}

@@ -62,6 +62,17 @@ struct FastDiv {
   VU_DEV uint32_t div(uint32_t n) const { return (__umulhi(n, m) + n) >> l; }
 };
 
+// Kahan-compensated acc += part (fp32 parity-mode GEMMs: the per-K-step MFMA
+// partials summed with an error that does not grow with K).  c carries the
+// negative of the low-order bits lost so far; the caller finishes with
+// acc -= c.  (No fast-math in this library: the compiler keeps the order.)
+VU_DEV void kahan_add(f32x4& acc, f32x4& c, const f32x4& part) {
+  const f32x4 y = part - c;
+  const f32x4 t = acc + y;
+  c = (t - acc) - y;
+  acc = t;
+}
+
 // border class of a row / column index (VuGemmFwd.zbias): 0 first, 2 last, 1 inside
 VU_DEV int zb_class(int v, int L) { return v == 0 ? 0 : (v == L - 1 ? 2 : 1); }
 

@@ -154,11 +154,23 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
       *reinterpret_cast<u32x4*>(B + swz((tid >> 3) + 32 * i, chunk)) = rb[i];
   };
 
-  f32x4 acc[TM][TN];
+  // fp32 (parity mode): two-level accumulation.  Each 32-element K-step is
+  // summed by its own MFMA chain into a fresh tile, which is then added to the
+  // running sum with Kahan compensation: the rounding error no longer grows
+  // with K (a single MFMA chain over K = 9*Cin = 576-9216 carried 1.4-4.4x the
+  // error of the blocked CPU GEMMs the fp32 oracle runs on, VERDICT r5 item 1,
+  // tools/fp32_err_probe.py).  bf16 (speed mode) keeps the single chain.
+  constexpr bool CMP = sizeof(T) == 4;
+  f32x4 acc[TM][TN], cmp[CMP ? TM : 1][CMP ? TN : 1];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+  if constexpr (CMP)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) cmp[i][j] = f32x4{0, 0, 0, 0};
 
   const int nk = (K + BKE - 1) / BKE;
   load(0);
@@ -169,6 +181,12 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
     if (kt + 1 < nk) load(kt + 1);
     const char* A = smem + cur * (BM + BN) * KB;
     const char* B = A + BM * KB;
+    f32x4 part[CMP ? TM : 1][CMP ? TN : 1];
+    if constexpr (CMP)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) part[i][j] = f32x4{0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       u32x4 af[TM], bf[TN];
@@ -182,11 +200,24 @@ __global__ __launch_bounds__(256, 2) void gemm_fwd_kernel(VuGemmFwd p) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = Mma<T>::run(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (CMP) part[i][j] = Mma<T>::run(af[i], bf[j], part[i][j]);
+          else acc[i][j] = Mma<T>::run(af[i], bf[j], acc[i][j]);
+        }
     }
+    if constexpr (CMP)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) kahan_add(acc[i][j], cmp[i][j], part[i][j]);
     if (kt + 1 < nk) store_lds(cur ^ 1);
     __syncthreads();
   }
+  if constexpr (CMP)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] -= cmp[i][j];
 
   // ---- epilogue: stage fp32 tile (+bias, rounded to T) in LDS ----
   float* E = reinterpret_cast<float*>(smem);
@@ -323,8 +354,10 @@ template <typename T>
 int dispatch_fwd(const VuGemmFwd& p, hipStream_t st) {
   int bm = pick_bm(p);
   if (bm == 128) {
-    if (p.ncol <= 64) return launch_fwd<T, 128, 64>(p, st);
-    return launch_fwd<T, 128, 128>(p, st);
+    // fp32: 128 x 64 tiles only (the compensated accumulators of a 128 x 128
+    // tile spill)
+    if (sizeof(T) == 4 || p.ncol <= 64) return launch_fwd<T, 128, 64>(p, st);
+    if constexpr (sizeof(T) == 2) return launch_fwd<T, 128, 128>(p, st);
   }
   return launch_fwd<T, 64, 64>(p, st);
 }

@@ -163,11 +163,17 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_kernel(VuGemmWgrad p) {
       *reinterpret_cast<u32x4*>(Qb + IQ::chunk_off(qrow + k * QSTEP, qcol)) = rq[k];
   };
 
-  f32x4 acc[TI][TJ];
+  constexpr bool CMP = sizeof(T) == 4;  // fp32: compensated sum of per-step partials
+  f32x4 acc[TI][TJ], cmp[CMP ? TI : 1][CMP ? TJ : 1];
 #pragma unroll
   for (int a = 0; a < TI; ++a)
 #pragma unroll
     for (int b = 0; b < TJ; ++b) acc[a][b] = f32x4{0, 0, 0, 0};
+  if constexpr (CMP)
+#pragma unroll
+    for (int a = 0; a < TI; ++a)
+#pragma unroll
+      for (int b = 0; b < TJ; ++b) cmp[a][b] = f32x4{0, 0, 0, 0};
 
   const int nsteps = mend > mbeg ? (int)((mend - mbeg + BMR - 1) / BMR) : 0;
   if (nsteps > 0) {
@@ -216,6 +222,14 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_kernel(VuGemmWgrad p) {
                 __builtin_bit_cast(bf16x8, af[a]), __builtin_bit_cast(bf16x8, bf[b]), acc[a][b], 0, 0, 0);
       }
     } else {
+      // fp32 (parity mode): the step's 64 pixels summed by their own MFMA
+      // chain, then added to the running sum with Kahan compensation (the
+      // split's chain otherwise grows with m_per_split; gemm_fwd.hip)
+      f32x4 part[TI][TJ];
+#pragma unroll
+      for (int a = 0; a < TI; ++a)
+#pragma unroll
+        for (int b = 0; b < TJ; ++b) part[a][b] = f32x4{0, 0, 0, 0};
 #pragma unroll 4
       for (int ks = 0; ks < BMR / 4; ++ks) {
         float af[TI], bf[TJ];
@@ -230,13 +244,22 @@ __global__ __launch_bounds__(256, 2) void gemm_wgrad_kernel(VuGemmWgrad p) {
         for (int a = 0; a < TI; ++a)
 #pragma unroll
           for (int b = 0; b < TJ; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+            part[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf[b], part[a][b], 0, 0, 0);
       }
+#pragma unroll
+      for (int a = 0; a < TI; ++a)
+#pragma unroll
+        for (int b = 0; b < TJ; ++b) kahan_add(acc[a][b], cmp[a][b], part[a][b]);
     }
     if (st + 1 < nsteps) store_lds(cur ^ 1);
     __syncthreads();
   }
 
+  if constexpr (CMP)
+#pragma unroll
+    for (int a = 0; a < TI; ++a)
+#pragma unroll
+      for (int b = 0; b < TJ; ++b) acc[a][b] -= cmp[a][b];
   // ---- store fp32 partial tile: lane holds C[4*g4 + r][li] ----
   float* out = p.out + (int64_t)split * p.ni * p.nj;
 #pragma unroll
