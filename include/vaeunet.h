@@ -258,6 +258,10 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     produce wrong results by design (timing decompositions).  Without it a
  *     non-zero experiment mode is refused (hipErrorInvalidValue). */
 #define VU_TUNE_UNSAFE 33
+/*   VU_TUNE_V6_STAG: 1 (default) = the resident-weight 64 -> 64 kernel with
+ *     the two wave halves' epilogues staggered into the next tile's first
+ *     group (bit-identical results), 0 = the round-5 lock-step kernel. */
+#define VU_TUNE_V6_STAG 34
 int vu_gemm_set_tuning(int key, int value);
 /* Bit mask of the experiment modes currently non-zero (bit 0 V6_XM, 1 V7_XM,
  * 2 FP8_XM): 0 in production.  bench.py refuses to report while it is not. */

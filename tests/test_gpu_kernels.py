@@ -572,6 +572,46 @@ def test_conv3x3_c64_resident(case):
         _tune((TUNE_V6, 1))
 
 
+TUNE_V6_STAG = 34
+
+
+@pytest.mark.parametrize("cap", [1, 2, 3, 5])
+@pytest.mark.parametrize("variant", ["stats_bias", "plain", "relu"])
+def test_conv3x3_c64_staggered_bit_identical(variant, cap):
+    """The staggered-epilogue resident-weight kernel (conv3x3_c64s_kernel,
+    VU_TUNE_V6_STAG = 1, round 6) against the round-5 lock-step kernel on the
+    same operands: outputs and BatchNorm partials bit for bit (the same MFMAs
+    and additions; only the statistics' store order differs), for 1-9 tiles
+    per block (odd and even walks, the last tile's epilogue after the loop)."""
+    K, E = _k()
+    N, H, W = 2, 48, 96   # 18 tiles
+    g = torch.Generator().manual_seed(47)
+    x = torch.randn(N, 64, H, W, generator=g).to(torch.bfloat16)
+    w = torch.randn(64, 64, 3, 3, generator=g) / 24.0
+    b = torch.randn(64, generator=g) if variant == "stats_bias" else None
+    d = _code("bf16")
+    xs = x.to(DEV).contiguous(memory_format=CL)
+    wf = E.w3x3_fwd(w.to(DEV), d)
+    res = []
+    for stag in (0, 1):
+        _tune((TUNE_V6, cap), (TUNE_V6_STAG, stag))
+        try:
+            out = K.empty_act(N, 64, H, W, torch.bfloat16, DEV)
+            out.fill_(7.0)
+            st = K.gemm_fwd(K.gather3x3([xs]), wf, 64, out, d, bias=None if b is None else b.to(DEV),
+                            stats=variant == "stats_bias", relu=variant == "relu")
+            torch.cuda.synchronize()
+            res.append((out.clone(), None if st is None else (st.psum.clone(), st.pm2.clone())))
+        finally:
+            _tune((TUNE_V6, 1), (TUNE_V6_STAG, 1))
+    (o0, s0), (o1, s1) = res
+    assert torch.equal(o0.view(torch.int16), o1.view(torch.int16))
+    if variant == "relu":
+        assert float(o1.float().min()) == 0.0
+    if s0 is not None:
+        assert torch.equal(s0[0], s1[0]) and torch.equal(s0[1], s1[1])
+
+
 @pytest.mark.parametrize("co", [128, 192])
 def test_conv3x3_c64_column_slices(co):
     """64 input channels, 128/192 outputs, no statistics (the input gradient of

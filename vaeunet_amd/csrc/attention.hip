@@ -51,6 +51,18 @@ VU_DEV float group_sum(float v, int lpp) {
   return v;
 }
 
+// psi = sigmoid(BN(q)).  fp32 (parity mode): the correctly rounded-ish libm
+// exp -- the fast __expf carries a small SYSTEMATIC error, and the psi
+// BatchNorm(1) affine gradients are sums over every pixel of terms that
+// cancel to 1e-3 of their magnitude, where a bias adds up coherently (the
+// HIP path had 2-3x the fp32 oracle's error on psi.1.weight, round 6).
+// bf16 (speed mode): __expf.
+template <typename T>
+VU_DEV float gate_sigmoid(float z) {
+  if constexpr (sizeof(T) == 4) return 1.f / (1.f + expf(-z));
+  else return 1.f / (1.f + __expf(-z));
+}
+
 template <typename T>
 VU_DEV void load8(const T* p, float* f) {
   Vec8<T> v; v.load(p);
@@ -210,7 +222,7 @@ __global__ __launch_bounds__(256) void gate_fwd_u_kernel(const float* q, const f
       if (e >= tot) break;
       const int64_t p = e >> vsh;
       const int c = (int)(e & vm) * 8;
-      const float pv = 1.f / (1.f + __expf(-(qv[u] * s + t)));
+      const float pv = gate_sigmoid<T>(qv[u] * s + t);
       if (c == 0 && pmap) pmap[p] = pv;
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[u].set(k, v[u].get(k) * pv);
@@ -229,7 +241,7 @@ __global__ void gate_fwd_kernel(const float* q, const float* st, const T* x, int
     int64_t p = e / V;
     int c = (int)(e - p * V) * 8;
     float z = q[p] * s + t;
-    float pv = 1.f / (1.f + __expf(-z));
+    float pv = gate_sigmoid<T>(z);
     if (c == 0 && pmap) pmap[p] = pv;
     Vec8<T> v; v.load(x + p * xs + c);
 #pragma unroll

@@ -378,6 +378,246 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_kernel(VuGemmFwd p) {
   }
 }
 
+// ---- the same tile stream with the two wave halves' epilogues staggered ----
+//
+// In conv3x3_c64_kernel all eight waves run the epilogue of a tile (bias,
+// rounding, packing, the statistics butterflies: VALU only) together at the
+// end of the chunk-1 group, so the matrix pipe of every SIMD idles through it
+// while the two waves of the SIMD contend for VALU issue.  Here it is split:
+//
+//   * light part, end of the chunk-1 group (all waves): bias, rounding, ReLU,
+//     bf16 packing into the 8 output pieces (the same registers the round-5
+//     kernel kept its deferred stores in), accumulators cleared;
+//   * heavy part, in the NEXT tile's chunk-0 group: the 8 output stores and
+//     the BatchNorm statistics computed from the packed pieces -- placed at
+//     opposite ends by the two waves of a SIMD (w and w + 4):
+//
+//       waves 4-7:  [heavy part of t] [chunk-0 taps of t+1]
+//       waves 0-3:  [chunk-0 taps of t+1] [heavy part of t]
+//
+//     so each half's heavy part runs beside the partner's MFMAs
+//     (MI355X_MICROARCH.md "Two waves per SIMD" item 9: split roles by wave
+//     number >= 4).
+//
+// After the permlane regroup a lane holds channels 32h + 8kg + e (piece h,
+// element e) of its pixel, 16 channels as before, so the butterfly over the 16
+// lanes of a row gives lane m the sums of slot m = channel 32(m >> 3) + 8kg +
+// (m & 7): the same additions in the same tree order as the round-5 kernel
+// (which kept slot m = channel 16kg + m) -- bit-identical outputs and
+// statistics, only the statistics' store addresses are permuted.
+template <bool STATS, bool RELU = false>
+__global__ __launch_bounds__(512, 1) void conv3x3_c64s_kernel(VuGemmFwd p) {
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES + 64 * 4];
+  char* const wl = smem;
+  char* const hl = smem + WBYTES;
+  float* const bias_l = reinterpret_cast<float*>(smem + LDS_BYTES);
+
+  const VuGather& g = p.a;
+  const int H = g.H, W = g.W;
+  const int txn = W / TW, per_img = txn * (H / TH);
+  const int T = g.N * per_img;
+  const int G = gridDim.x;  // <= T (host)
+  const int lb = xcd_remap(blockIdx.x, G);
+  const int ntile_blk = (T - lb + G - 1) / G;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool late = wid >= 4;  // waves 4-7: heavy part first in the chunk-0 group
+  const int l16 = lane & 15, kg = lane >> 4;
+  const bf16_t* const src = reinterpret_cast<const bf16_t*>(g.src[0]);
+  const int64_t st = g.stride[0];
+  const void* const zp = (const void*)v6_zero_page;
+  const bool has_bias = p.bias != nullptr;
+  if (tid < 64) bias_l[tid] = has_bias ? p.bias[tid] : 0.f;  // read from LDS in the epilogue
+
+  {
+    const bf16_t* bm = reinterpret_cast<const bf16_t*>(p.b);
+#pragma unroll
+    for (int i = 0; i < WROUNDS; ++i) {
+      const int s = i * 512 + tid;
+      const int n = s / 72, pc = s - (s / 72) * 72;
+      const void* gp = (const void*)(bm + (int64_t)n * p.ldb + (pc ^ wswz(n)) * 8);
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(wl + (i * 512 + wid * 64) * 16), 16, 0, 0);
+    }
+  }
+  auto halo = [&](int t, int c, int b) {
+    const int img = t / per_img, r = t - (t / per_img) * per_img;
+    const int ty = r / txn, tx = r - (r / txn) * txn;
+    const int y0 = ty * TH - 1, x0 = tx * TW - 1;
+    const bf16_t* s0 = src + (int64_t)img * H * W * st + c * 32;
+    char* dst = hl + b * HBUF;
+#pragma unroll
+    for (int i = 0; i < NHR; ++i) {
+      if (i * 512 + wid * 64 >= HPIECES) continue;  // wave-uniform
+      const int s = i * 512 + tid;
+      const int P = s >> 2, pos = s & 3;
+      const int hy = P / HWD, hx = P - (P / HWD) * HWD;
+      const int y = y0 + hy, x = x0 + hx;
+      const int k = (pos - ((P >> 1) & 2)) & 3;
+      const bool ok = s < HPIECES && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const void* gp = ok ? (const void*)(s0 + (int64_t)(y * W + x) * st + k * 8) : zp;
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(dst + (i * 512 + wid * 64) * 16), 16, 0, 0);
+    }
+  };
+
+  halo(lb, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (+ the bias_l stores)
+  raw_barrier();
+
+  int boff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = 16 * (l16 >> 2) + 4 * j + (l16 & 3);
+    boff[j] = n * WROW + ((kg ^ wswz(n)) << 4);
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+  u32x4 pend[8];  // tile t's packed output pieces (q = 2 * fragment + half)
+
+  auto taps = [&](int b, int c) {
+    const char* hb = hl + b * HBUF;
+    const int cx = c << 6;
+    u32x4 bf[4], af[4];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ty = tap / 3, tx = tap - (tap / 3) * 3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = *reinterpret_cast<const u32x4*>(wl + (boff[j] ^ cx) + tap * 128);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int P = (2 * wid + (i >> 1) + ty) * HWD + (i & 1) * 16 + tx + l16;
+        af[i] = *reinterpret_cast<const u32x4*>(hb + P * 64 + (((kg + ((P >> 1) & 2)) & 3) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
+                                                              __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // light part: acc -> pend (bias, bf16 rounding, ReLU, 64-byte regroup); acc cleared
+  auto light = [&]() {
+    if (has_bias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 bvj = *reinterpret_cast<const f32x4*>(bias_l + 16 * kg + 4 * j);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] += bvj;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (RELU) {
+        f32x4 z[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[j][r] = rnd<bf16_t>(acc[i][j][r]);
+        epi_relu(z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = z[j];
+      }
+      u32x4 cv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = acc[i][2 * h], e = acc[i][2 * h + 1];
+        cv[h] = u32x4{(uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16), (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16),
+                      (uint32_t)f2bf(e[0]) | ((uint32_t)f2bf(e[1]) << 16), (uint32_t)f2bf(e[2]) | ((uint32_t)f2bf(e[3]) << 16)};
+      }
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const auto r1 = __builtin_amdgcn_permlane16_swap(cv[0][w], cv[1][w], false, false);
+        const auto r2 = __builtin_amdgcn_permlane32_swap(r1[0], r1[1], false, false);
+        cv[0][w] = r2[0];
+        cv[1][w] = r2[1];
+      }
+      pend[2 * i] = cv[0];
+      pend[2 * i + 1] = cv[1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0, 0, 0, 0};
+    }
+  };
+
+  // heavy part of tile t from pend: the 8 output stores, then the statistics
+  auto heavy = [&](int t) {
+    const int img = t / per_img, r0 = t - (t / per_img) * per_img;
+    const int ty = r0 / txn, tx = r0 - (r0 / txn) * txn;
+    bf16_t* const pdst = reinterpret_cast<bf16_t*>(p.out) + p.out_coff + 8 * kg +
+                         (((int64_t)img * H + ty * TH + 2 * wid) * W + tx * TW + l16) * p.out_stride;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      bf16_t* o = pdst + ((q >> 2) * (int64_t)W + ((q >> 1) & 1) * 16) * p.out_stride + 32 * (q & 1);
+      *reinterpret_cast<u32x4*>(o) = pend[q];
+    }
+    if (STATS) {
+      // slot 8h + e of a lane = channel 32h + 8kg + e of its pixel, pixel
+      // fragments i = q >> 1 (piece q = 2i + h)
+      auto val = [&](int i, int h, int e) {
+        const uint32_t w = pend[2 * i + h][e >> 1];
+        return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+      };
+      float v[16];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[8 * h + e] = (val(0, h, e) + val(1, h, e)) + (val(2, h, e) + val(3, h, e));
+      const float ms = bfly16_reduce(v, lane);
+      float mb[16];
+      bfly16_bcast(ms * (1.f / 64), lane, mb);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float q = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = val(i, h, e) - mb[8 * h + e];
+            q += d * d;
+          }
+          v[8 * h + e] = q;
+        }
+      const float mq = bfly16_reduce(v, lane);
+      const int ch = 32 * (l16 >> 3) + 8 * kg + (l16 & 7);
+      const int64_t so = (int64_t)(t * 8 + wid) * p.ncol + ch;
+      p.stat_sum[so] = ms;
+      p.stat_m2[so] = mq;
+    }
+  };
+
+  int t = lb, b = 0;
+  for (int ti = 0; ti < ntile_blk; ++ti) {
+    // ---- chunk-0 group (+ the previous tile's heavy part) ----
+    halo(t, 1, b ^ 1);
+    const bool ep = ti > 0;
+    if (ep && late) heavy(t - G);
+    taps(b, 0);
+    if (ep && !late) heavy(t - G);
+    // the halo was issued before the heavy part's 8 output (+ 2 statistics) stores
+    if (ep) {
+      if (STATS) wait_vm<10>(); else wait_vm<8>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();
+    b ^= 1;
+    // ---- chunk-1 group, then the light part of this tile ----
+    if (ti + 1 < ntile_blk) halo(t + G, 0, b ^ 1);
+    taps(b, 1);
+    light();
+    wait_vm<0>();
+    raw_barrier();
+    b ^= 1;
+    t += G;
+  }
+  if (ntile_blk > 0) heavy(t - G);
+}
+
 int cu_count6() {
   static int n = 0;
   if (n == 0) {
@@ -389,6 +629,7 @@ int cu_count6() {
 }
 
 int g_v6_xm = 0;  // VU_TUNE_V6_XM (experiment modes of conv3x3_c64_kernel)
+int g_v6_stag = 1;  // VU_TUNE_V6_STAG: 1 = the staggered-epilogue kernel (conv3x3_c64s_kernel)
 int g_v6 = 1;  // VU_TUNE_V6: 0 off, 1 on (grids of >= 1 tile per CU), k >= 2 on with the grid capped at k
 
 }  // namespace
@@ -444,6 +685,16 @@ int gemm_fwd_v6_launch(const VuGemmFwd& p, hipStream_t st) {
     }
     return 0;
   }
+  if (g_v6_stag && g_v6_xm == 0) {
+    if (p.stat_sum) {
+      if (p.relu) hipLaunchKernelGGL((conv3x3_c64s_kernel<true, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
+      else hipLaunchKernelGGL(conv3x3_c64s_kernel<true>, dim3((unsigned)grid), dim3(512), 0, st, p);
+    } else {
+      if (p.relu) hipLaunchKernelGGL((conv3x3_c64s_kernel<false, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
+      else hipLaunchKernelGGL(conv3x3_c64s_kernel<false>, dim3((unsigned)grid), dim3(512), 0, st, p);
+    }
+    return (int)hipGetLastError();
+  }
   if (p.stat_sum)
     if (p.relu) hipLaunchKernelGGL((conv3x3_c64_kernel<true, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
     else if (g_v6_xm == 1) hipLaunchKernelGGL((conv3x3_c64_kernel<true, false, 1>), dim3((unsigned)grid), dim3(512), 0, st, p);
@@ -471,6 +722,10 @@ int gemm_fwd_v6_tune(int key, int value) {
   }
   if (key == VU_TUNE_V6) {
     g_v6 = value < 0 ? 0 : value;
+    return 0;
+  }
+  if (key == VU_TUNE_V6_STAG) {
+    g_v6_stag = value != 0;
     return 0;
   }
   return -1;
