@@ -321,6 +321,11 @@ typedef struct VuConvFp8 {
   /* split-K over the input channels for grids under one block per CU:
    * vu_conv3x3_fp8_workspace_bytes() of fp32 slab space (NULL when 0) */
   float* workspace;
+  /* optional (round 6): per statistics row tile and channel, the min / max of
+   * the stored (bf16-rounded) output, laid out as stat_sum; only where
+   * vu_conv3x3_fp8_minmax_ok() (else the launch is refused).  NULL: none. */
+  float* stat_min;
+  float* stat_max;
 } VuConvFp8;
 /* statistics row tile (128, or 64 on the 64 -> 64 resident-weight kernel)
  * when the kernel serves this problem, else 0 */
@@ -328,6 +333,16 @@ int64_t vu_conv3x3_fp8_row_tile(const VuConvFp8* args);
 /* fp32 split-K slab bytes vu_conv3x3_fp8 needs in args->workspace (0 = none) */
 int64_t vu_conv3x3_fp8_workspace_bytes(const VuConvFp8* args);
 int vu_conv3x3_fp8(const VuConvFp8* args, void* stream);
+/* 1 when the kernel serving *args can emit stat_min / stat_max, else 0 */
+int vu_conv3x3_fp8_minmax_ok(const VuConvFp8* args);
+/* amax[0] = max over rows x C of |relu?(y * scale[c] + shift[c])| for y in
+ * {pmin, pmax} ([rows][C] per-tile min / max of a conv output): the
+ * just-in-time e4m3 scale of relu(BN(y)) without a pass over y (the affine is
+ * monotone per channel); the same two roundings as vu_bn_apply_fp8, so it
+ * equals that kernel's calibration max exactly.  scale NULL: identity.
+ * C % 4 == 0 and 16-byte aligned pmin / pmax / scale / shift. */
+int vu_fp8_relu_amax(const float* pmin, const float* pmax, int64_t rows, int C, const float* scale,
+                     const float* shift, int relu, float* amax, void* stream);
 
 /* ---- weights ----------------------------------------------------------- */
 /* out[i0][i1][i2][i3] (contiguous) = in[base + i0*s0 + i1*s1 + i2*s2 + i3*s3]

@@ -355,3 +355,76 @@ def test_double_conv_fp8_chained():
         got = q.float() * dq
         err = (got - ref.float()).abs()
         assert (err <= 2.0 ** -3 * ref.float().abs() + 1e-3 * ref.float().abs().max()).all(), step
+
+
+# (N, [cin per source], H, W, cout): the step-loop kernel (256 / 128 / 64
+# column tiles) and the two resident-weight 64-channel kernels (one and two
+# 64-channel chunks)
+MINMAX_CASES = [
+    (2, [64], 16, 64, 256),
+    (2, [128], 32, 32, 128),
+    (2, [64], 32, 64, 64),
+    (2, [64], 256, 512, 64),        # resident weights, one chunk (512 tiles)
+    (2, [64, 64], 256, 512, 64),    # resident weights, two chunks
+]
+
+
+@pytest.mark.parametrize("case", MINMAX_CASES)
+def test_conv3x3_fp8_minmax_partials(case):
+    """VuConvFp8.stat_min / stat_max (round 6): per statistics tile and
+    channel, the min / max of the stored bf16 output -- combined over the
+    tiles they equal the output's per-channel min / max exactly; and
+    vu_fp8_relu_amax on them equals, bit for bit, the max |relu(y*s + t)|
+    that vu_bn_apply_fp8's calibration pass measures over every element."""
+    from vaeunet_amd import fp8
+    N, cins, H, W, co = case
+    g = torch.Generator().manual_seed(19)
+    xs = [_act(torch.randn(N, c, H, W, generator=g).relu()) for c in cins]
+    w = torch.randn(co, sum(cins), 3, 3, generator=g) / (3 * sum(cins) ** 0.5)
+    am = fp8.amax(xs)
+    qs = []
+    for t in xs:
+        q, dq = fp8.quantize(t, am)
+        qs.append(q)
+    wq, ws = fp8.quantize_weight(w.to(DEV))
+    y, st = fp8.conv3x3(qs, dq, wq, ws, co, stats=True, minmax=True)
+    assert st.minmax is not None
+    pmin, pmax = st.minmax
+    yf = y.float()
+    torch.testing.assert_close(pmin.min(0).values, yf.amin((0, 2, 3)), rtol=0, atol=0)
+    torch.testing.assert_close(pmax.max(0).values, yf.amax((0, 2, 3)), rtol=0, atol=0)
+    assert bool((pmin <= pmax).all())
+    sc = (torch.rand(co, generator=g) * 2 - 0.5).to(DEV)    # some negative scales
+    sh = (torch.randn(co, generator=g) * 0.3).to(DEV)
+    for relu in (True, False):
+        ds = fp8.relu_amax_scale(st.minmax, (sc, sh), relu, DEV)
+        cal = fp8.DelayedScale(DEV)
+        fp8.calibrate(y, (sc, sh), relu, cal)
+        assert ds.ring[0].item() == cal.ring[0].item(), (relu, ds.ring[0].item(), cal.ring[0].item())
+        assert ds.ring[1].item() == 0.0 and ds.ring[2].item() == 0.0
+
+
+@pytest.mark.parametrize("up", [False, True])
+def test_double_conv_fp8_jit_minmax_matches_two_pass(up):
+    """Just-in-time DoubleConv (default, round 6: conv2's input scale from
+    conv1's min / max epilogue, BN1 + ReLU fused with the quantise) against
+    the round-5 form (BN1 apply to bf16, then amax + quantise passes): the
+    same scale up to the bf16 rounding of the activation, so the outputs
+    agree to the e4m3 quantisation step; and both stay close to bf16."""
+    from vaeunet_amd import DoubleConv, fp8
+    torch.manual_seed(6)
+    cins = [64, 64] if up else [64]
+    mod = DoubleConv(sum(cins), 64 if up else 128).to(DEV)
+    xs = [_act(torch.randn(2, c, 256, 512).relu()) for c in cins]
+    old = fp8.JIT_MINMAX
+    try:
+        fp8.JIT_MINMAX = True
+        yn = fp8.double_conv_forward(mod, xs).float()
+        fp8.JIT_MINMAX = False
+        yo = fp8.double_conv_forward(mod, xs).float()
+    finally:
+        fp8.JIT_MINMAX = old
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        yb = mod(torch.cat(xs, 1)).float()
+    assert ((yn - yo).abs().max() / yo.abs().max()).item() < 0.03
+    assert ((yn - yb).abs().max() / yb.abs().max()).item() < 0.15

@@ -108,10 +108,29 @@ LAYERS = [
 ]
 
 
+GRAPH = False  # --graph: time one captured HIP graph of `reps` calls (GPU time, no Python enqueue)
+
+
 def timeit(fn, reps):
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if GRAPH:
+        # the training step replays as one graph: time the blocks the same way
+        # (eagerly, the just-in-time path's extra launches are Python-bound at
+        # the 64^2-128^2 blocks; a delayed call's host slot counter freezes in
+        # the capture, which changes values, not the kernels timed)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        s.record()
+        g.replay()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
     s.record()
     for _ in range(reps):
         fn()
@@ -129,7 +148,15 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--double", action="store_true", help="time whole DoubleConv blocks (see above)")
     ap.add_argument("--tune", default="", help="KEY=VAL,... vu_gemm_set_tuning before the run (A/B)")
+    ap.add_argument("--jit-two-pass", action="store_true",
+                    help="just-in-time path as in round 5 (fp8.JIT_MINMAX = False: BN1 apply to bf16, amax + "
+                         "quantise passes) instead of the min/max-epilogue scale")
+    ap.add_argument("--graph", action="store_true", help="time graph replays (GPU time) instead of eager calls")
     args = ap.parse_args()
+    global GRAPH
+    GRAPH = args.graph
+    if args.jit_two_pass:
+        fp8.JIT_MINMAX = False
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
         _lib.call("vu_gemm_set_tuning", int(k), int(v))

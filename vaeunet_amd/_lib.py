@@ -53,7 +53,7 @@ class VuGemmWgrad(C.Structure):
 class VuConvFp8(C.Structure):
     _fields_ = [("a", VuGather), ("w", _p), ("ldw", _l), ("ncol", C.c_int32), ("out_coff", C.c_int32),
                 ("x_scale", _p), ("w_scale", _p), ("bias", _p), ("out", _p), ("out_stride", _l),
-                ("stat_sum", _p), ("stat_m2", _p), ("workspace", _p)]
+                ("stat_sum", _p), ("stat_m2", _p), ("workspace", _p), ("stat_min", _p), ("stat_max", _p)]
 
 
 class VuPermJob(C.Structure):
@@ -113,6 +113,8 @@ _SIGS = {
     "vu_conv3x3_fp8_row_tile": (_l, [C.POINTER(VuConvFp8)]),
     "vu_conv3x3_fp8": (_i, [C.POINTER(VuConvFp8), _p]),
     "vu_conv3x3_fp8_workspace_bytes": (_l, [C.POINTER(VuConvFp8)]),
+    "vu_conv3x3_fp8_minmax_ok": (_i, [C.POINTER(VuConvFp8)]),
+    "vu_fp8_relu_amax": (_i, [_p, _p, _l, _i, _p, _p, _i, _p, _p]),
     "vu_permute4_chunk": (_l, []),
     "vu_permute4_tile": (_l, []),
     "vu_permute4_batch": (_i, [_p, _i, _l, _p]),

@@ -120,9 +120,13 @@ def quantize_weight(w):
     return ent[1]
 
 
-def conv3x3(xqs, x_dq, wq, w_dq, ncol, out=None, out_coff=0, bias=None, stats=False):
+def conv3x3(xqs, x_dq, wq, w_dq, ncol, out=None, out_coff=0, bias=None, stats=False, minmax=False):
     """out[m][co] = x_dq * w_dq[co] * sum_k xq[m][k] wq[co][k] (+bias), bf16 NHWC.
-    xqs: 1-3 e4m3 NHWC sources (channel concat, 64-channel aligned)."""
+    xqs: 1-3 e4m3 NHWC sources (channel concat, 64-channel aligned).
+    minmax: also the per-tile per-channel min / max of the output where the
+    serving kernel emits them (vu_conv3x3_fp8_minmax_ok), returned as
+    ``(pmin, pmax)`` in ``Stats.minmax`` (``Stats.minmax`` None where it does
+    not; a Stats is then returned even without ``stats``)."""
     N, _, H, W = xqs[0].shape
     if out is None:
         out = K.empty_act(N, ncol, H, W, torch.bfloat16, xqs[0].device)
@@ -137,18 +141,27 @@ def conv3x3(xqs, x_dq, wq, w_dq, ncol, out=None, out_coff=0, bias=None, stats=Fa
     a.bias = bias.data_ptr() if bias is not None else None
     a.out = out.data_ptr()
     a.out_stride = K.pstride(out)
-    a.stat_sum = a.stat_m2 = None
+    a.stat_sum = a.stat_m2 = a.stat_min = a.stat_max = None
     rows = N * H * W
     bm = query("vu_conv3x3_fp8_row_tile", C.byref(a))
     if bm <= 0:
         raise ValueError(f"fp8 3x3 conv: shape not served (C={a.a.C}, ncol={ncol}, H={H}, W={W})")
     st = None
+    tiles = (rows + bm - 1) // bm
     if stats:
-        tiles = (rows + bm - 1) // bm
         psum = torch.empty((tiles, ncol), dtype=torch.float32, device=out.device)
         pm2 = torch.empty_like(psum)
         a.stat_sum, a.stat_m2 = psum.data_ptr(), pm2.data_ptr()
         st = K.Stats(psum, pm2, tiles, bm, rows)
+    if minmax:
+        if st is None:
+            st = K.Stats(None, None, tiles, bm, rows)
+        st.minmax = None
+        if query("vu_conv3x3_fp8_minmax_ok", C.byref(a)):
+            pmin = torch.empty((tiles, ncol), dtype=torch.float32, device=out.device)
+            pmax = torch.empty_like(pmin)
+            a.stat_min, a.stat_max = pmin.data_ptr(), pmax.data_ptr()
+            st.minmax = (pmin, pmax)
     a.workspace = None
     nb = query("vu_conv3x3_fp8_workspace_bytes", C.byref(a))
     ws = None
@@ -160,7 +173,7 @@ def conv3x3(xqs, x_dq, wq, w_dq, ncol, out=None, out_coff=0, bias=None, stats=Fa
     return out, st
 
 
-def conv3x3_q(srcs, weight, bias=None, stats=False):
+def conv3x3_q(srcs, weight, bias=None, stats=False, minmax=False):
     """Quantise the (bf16) sources with one shared scale and the weights, then
     run the fp8 conv.  Returns (bf16 output, Stats or None)."""
     am = amax(srcs)
@@ -169,7 +182,26 @@ def conv3x3_q(srcs, weight, bias=None, stats=False):
         q, dq = quantize(t, am)
         qs.append(q)
     wq, ws = quantize_weight(weight)
-    return conv3x3(qs, dq, wq, ws, weight.shape[0], bias=bias, stats=stats)
+    return conv3x3(qs, dq, wq, ws, weight.shape[0], bias=bias, stats=stats, minmax=minmax)
+
+
+def relu_amax_scale(minmax, coef, relu, device):
+    """A fresh single-use DelayedScale whose slot 0 holds the just-in-time
+    amax of relu?(y * coef[0] + coef[1]) (vu_fp8_relu_amax, from the producing
+    conv's per-tile min / max: no pass over y)."""
+    pmin, pmax = minmax
+    ds = DelayedScale(device)
+    call("vu_fp8_relu_amax", C.c_void_p(pmin.data_ptr()), C.c_void_p(pmax.data_ptr()), pmin.shape[0],
+         pmin.shape[1], C.c_void_p(coef[0].data_ptr()) if coef is not None else None,
+         C.c_void_p(coef[1].data_ptr()) if coef is not None else None, 1 if relu else 0,
+         C.c_void_p(ds.ring.data_ptr()), stream())
+    return ds
+
+
+# just-in-time fp8 DoubleConv: conv2's input scale from conv1's min / max
+# epilogue and BN1 + ReLU applied with the e4m3 quantise in one pass (round 6),
+# instead of BN1 apply (bf16) + an amax pass + a quantise pass (A/B switch)
+JIT_MINMAX = True
 
 
 def _site_scales(mod, device):
@@ -198,8 +230,12 @@ def double_conv_forward(mod, x, delayed=False, x_q=None, out_fp8=False):
     x: a bf16 NHWC tensor, or the list of channel-concat sources of an Up
     block's DoubleConv (they share one scale, as in conv3x3_q).
 
-    delayed=False (default): just-in-time scaling (amax pass + quantise pass
-    of the input and of the bf16 BN1 output): every call is self-contained.
+    delayed=False (default): just-in-time scaling, every call self-contained:
+    an amax pass + a quantise pass of the input; conv2's input scale is the
+    exact max of relu(BN1(y1)) formed from conv1's per-tile per-channel
+    min / max (its epilogue, vu_fp8_relu_amax), and BN1 + ReLU is applied and
+    quantised in one pass (vu_bn_apply_fp8) -- round 6; before, BN1 was
+    applied to a bf16 tensor that was then read twice more (amax, quantise).
     delayed=True (opt-in, for step loops over same-range data): both
     activation quantisations use the amax the previous call recorded
     (DelayedScale, one per site, kept on the module; ``reset_scales`` drops
@@ -219,14 +255,36 @@ def double_conv_forward(mod, x, delayed=False, x_q=None, out_fp8=False):
     if (x_q is not None or out_fp8) and not delayed:
         raise ValueError("fp8.double_conv_forward: x_q / out_fp8 (chained fp8 blocks) need delayed=True")
     if not delayed:
-        a = srcs
-        for conv, bn in ((conv1, bn1), (conv2, bn2)):
-            y, st = conv3x3_q(a, conv.weight, stats=bn.training)
-            coef = E.bn_coef(bn, st, conv.out_channels)
-            out = torch.empty_like(y)
-            K.bn_apply(y, out, coef, True, _lib.BF16)
-            a = [out]
-        return a[0]
+        if JIT_MINMAX:
+            # the input: exact amax by the calibration pass (max-accumulated over
+            # the sources), one quantising pass per source with that scale
+            ds_x = DelayedScale(srcs[0].device)
+            for t in srcs:
+                calibrate(t, None, False, ds_x)
+            qs = []
+            for t in srcs:
+                q, xdq = bn_apply_quant(t, None, False, ds_x)
+                qs.append(q)
+            w1, s1 = quantize_weight(conv1.weight)
+            y1, st1 = conv3x3(qs, xdq, w1, s1, conv1.out_channels, stats=bn1.training, minmax=True)
+        else:
+            y1, st1 = conv3x3_q(srcs, conv1.weight, stats=bn1.training)
+        coef1 = E.bn_coef(bn1, st1 if bn1.training else None, conv1.out_channels)
+        w2, s2 = quantize_weight(conv2.weight)
+        if JIT_MINMAX and st1 is not None and st1.minmax is not None:
+            # exact just-in-time scale of relu(BN1(y1)) from the min / max
+            # partials, then BN1 + ReLU + e4m3 in one pass (no bf16 a1)
+            ds = relu_amax_scale(st1.minmax, coef1, True, y1.device)
+            aq, adq = bn_apply_quant(y1, coef1, True, ds)
+            y2, st2 = conv3x3([aq], adq, w2, s2, conv2.out_channels, stats=bn2.training)
+        else:
+            a1 = torch.empty_like(y1)
+            K.bn_apply(y1, a1, coef1, True, _lib.BF16)
+            y2, st2 = conv3x3_q([a1], conv2.weight, stats=bn2.training)
+        coef2 = E.bn_coef(bn2, st2, conv2.out_channels)
+        out = torch.empty_like(y2)
+        K.bn_apply(y2, out, coef2, True, _lib.BF16)
+        return out
     if x_q is not None:
         qs, xdq = list(x_q[0]), x_q[1]
         dev = qs[0].device

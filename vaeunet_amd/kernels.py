@@ -156,6 +156,7 @@ class Stats:
 
     def __init__(self, psum, pm2, tiles, tile_rows, rows):
         self.psum, self.pm2, self.tiles, self.tile_rows, self.rows = psum, pm2, tiles, tile_rows, rows
+        self.minmax = None  # (pmin, pmax) where an fp8 conv epilogue emitted them
 
 
 class BnbPart:
