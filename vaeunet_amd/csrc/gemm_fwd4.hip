@@ -899,8 +899,18 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
     else if (p.zbias)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64, true>), dim3((unsigned)tiles),
                          dim3(512), 0, st, q);
-    else if (p.bnb_part)
-      hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+    else if (p.bnb_part) {
+      // (the 64-column tiles spill with the FULL step's extra fragments)
+      if constexpr (BN != 64) {
+        if (g_pp_full)
+          hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true, false, true>), dim3((unsigned)tiles), dim3(512), 0, st,
+                             q);
+        else
+          hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+      } else {
+        hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
+      }
+    }
     else if (p.relu)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, true>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     else if (BN != 64 && g_pp_full && (g_pp_persist >= 2 || (g_pp_persist == 1 && tiles > cu_count4()))) {

@@ -40,13 +40,15 @@ OVERLAP_WGRAD = False
 # The first stage of a BatchNorm backward reduction (sum dz, sum dz * xhat)
 # emitted by the epilogue of the input-gradient GEMM that produces dz's
 # source (DoubleConv conv2 -> BN1; the ping-pong kernel and its split-K
-# finish), instead of a separate pass over dy and x.  Measured neutral
-# (same-box A/B, profiles/r3_ab_bn_bwd_fusion.log: UNet +0.35 %, VAE -0.4 %;
-# per kernel, profiles/r3_prof_bnb_fusion.txt: the 22 -> 16 reduction passes
-# save 172 us/step, the epilogues that replace them cost 124 us/step and the
-# partial folds 18): the epilogue's BN-input loads and sums run serialised
-# at one block per CU.  Off by default; module-level switch for A/B runs.
-FUSE_BN_BWD_REDUCE = False
+# finish), instead of a separate pass over dy and x.  Round 3 measured it
+# neutral (profiles/r3_ab_bn_bwd_fusion.log: UNet +0.35 %, VAE -0.4 %): the
+# epilogue variant ran the two-halves step loop, not the one-read-segment
+# FULL loop of the plain input gradient (+56 us/step of the 172 the fused
+# reduction saves, profiles/r6l_*).  Round 6: the epilogue variant on the
+# FULL loop (243-246 VGPRs, no spill): UNet +0.38 / +0.40 %, VAE +0.04 /
+# -0.02 % in a same-box A/B (profiles/r6m_ab_bn_bwd_fusion.txt).  On by
+# default; module-level switch for A/B runs.
+FUSE_BN_BWD_REDUCE = True
 
 
 class SideStream:
