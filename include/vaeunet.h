@@ -551,6 +551,25 @@ int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int64_t dys,
                      int64_t P, int C, int J, const float* w, void* dx,
                      int64_t dxs, float* dw, float* db, int accumulate,
                      float* workspace, int dtype, void* stream);
+/* The same 1x1 conv over the producing BatchNorm + ReLU applied on the fly
+ * (round 6: the UNet's last BN never materialised): x is the PRE-BN tensor
+ * and the operand a = relu(x * bn_scale[c] + bn_shift[c]) rounded to the
+ * storage dtype (the bytes vu_bn_apply would store).  C <= 512. */
+int vu_pointwise_bn_fwd(const void* x, int64_t xs, int64_t P, int C, int J,
+                        const float* bn_scale, const float* bn_shift, const float* w,
+                        const float* b, float* y, int64_t ys, int dtype, void* stream);
+/* Backward of vu_pointwise_bn_fwd: dx = gradient w.r.t. a (as
+ * vu_pointwise_bwd), dw / db over the re-formed a, and bnb[blk][2][C] = the
+ * first stage of the BatchNorm's backward reduction over block blk's pixels
+ * (sum dz, sum dz * (x - mean) * invstd, dz = the stored dx masked by the
+ * ReLU) -- VuGemmFwd.bnb_part's layout, finished by vu_bn_bwd_finish with
+ * nblk = vu_pointwise_bn_bwd_blocks(P).  bn_coef: rows scale, shift, mean,
+ * invstd at coef_stride floats apart.  workspace: vu_pointwise_bwd's. */
+int64_t vu_pointwise_bn_bwd_blocks(int64_t P);
+int vu_pointwise_bn_bwd(const void* x, int64_t xs, const float* bn_coef, int64_t coef_stride,
+                        const float* dy, int64_t dys, int64_t P, int C, int J, const float* w,
+                        void* dx, int64_t dxs, float* dw, float* db, int accumulate,
+                        float* workspace, float* bnb, int dtype, void* stream);
 
 /* ---- loss (utils/loss.py) ---------------------------------------------- */
 int64_t vu_loss_workspace_bytes(void);

@@ -158,6 +158,9 @@ _SIGS = {
                              _p]),
     "vu_pointwise_fwd": (_i, [_p, _l, _l, _i, _i, _p, _p, _p, _l, _i, _p]),
     "vu_pointwise_bwd_workspace_bytes": (_l, [_l, _i, _i]),
+    "vu_pointwise_bn_fwd": (_i, [_p, _l, _l, _i, _i, _p, _p, _p, _p, _p, _l, _i, _p]),
+    "vu_pointwise_bn_bwd_blocks": (_l, [_l]),
+    "vu_pointwise_bn_bwd": (_i, [_p, _l, _p, _l, _p, _l, _l, _i, _i, _p, _p, _l, _p, _p, _i, _p, _p, _i, _p]),
     "vu_pointwise_bwd": (_i, [_p, _l, _p, _l, _l, _i, _i, _p, _p, _l, _p, _p, _i, _p, _i, _p]),
     "vu_loss_workspace_bytes": (_l, []),
     "vu_bce_dice_fwd2": (_i, [_p, _p, _l, _p, _f, _f, _f, _p, _p, _p, _p]),

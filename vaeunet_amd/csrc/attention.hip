@@ -469,9 +469,14 @@ __global__ void part_final(const float* part, int nblk, int width, float* out, i
 }
 
 // ---- tiny-output pointwise conv ----
-template <typename T>
+// BNA (round 6): x is the PRE-BatchNorm tensor of the producing DoubleConv and
+// the operand is a = relu(x * bn_scale + bn_shift) rounded to the storage
+// type -- exactly the bytes vu_bn_apply would have stored -- formed in
+// registers, so the UNet's last BatchNorm + ReLU is never materialised
+// (unet_parts.py:44-45 feeding OutConv :100).
+template <typename T, bool BNA = false>
 __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, const float* w, const float* b,
-                              float* y, int64_t ys) {
+                              float* y, int64_t ys, const float* bn_scale = nullptr, const float* bn_shift = nullptr) {
   const int lpp = C >> 3 > 64 ? 64 : C >> 3;
   const int ppw = 64 / lpp;
   const int lane = threadIdx.x & 63;
@@ -485,13 +490,16 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
     // (cold-cache 512^2 x 64 -> 2: 135 -> 107 us with the DPP group sums)
     constexpr int PU = 4;   // (8 rows in flight: 144 VGPRs, 3 waves per SIMD, measured 71 -> 91 us)
     const int c = sub * 8;
-    float wr[4][8], bj[4];
+    float wr[4][8], bj[4], bsc[8], bsh[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       bj[j] = (j < J && b) ? b[j] : 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) wr[j][k] = j < J ? w[j * C + c + k] : 0.f;
     }
+    if constexpr (BNA)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { bsc[k] = bn_scale[c + k]; bsh[k] = bn_shift[c + k]; }
     for (int64_t pb = wave * ppw * PU; pb < P; pb += nwaves * ppw * PU) {
       // the PU loads from clamped pixel addresses, unconditionally: a guarded
       // load per pixel sat in its own basic block with a vmcnt(0) wait after
@@ -503,6 +511,11 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
         const int64_t p = pb + u * ppw + slot;
         load8<T>(x + (p < P ? p : P - 1) * xs + c, f[u]);
       }
+      if constexpr (BNA)
+#pragma unroll
+        for (int u = 0; u < PU; ++u)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[u][k] = rnd<T>(fmaxf(fmaf(f[u][k], bsc[k], bsh[k]), 0.f));
 #pragma unroll
       for (int u = 0; u < PU; ++u)
         if (pb + u * ppw + slot >= P)
@@ -525,6 +538,7 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
     }
     return;
   }
+  if constexpr (BNA) return;  // (host: C <= 512 only)
   for (int64_t pb = wave * ppw; pb < P; pb += nwaves * ppw) {
     int64_t p = pb + slot;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -547,9 +561,18 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
 }
 
 // dx = dy w ; per-block partials of dw[j][c] = sum dy[p,j] x[p,c] and db[j]
-template <typename T>
-__global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t dys, int64_t P, int C, int J,
-                              const float* w, T* dx, int64_t dxs, float* part) {
+// BNA (round 6): x is the pre-BatchNorm tensor (the operand a = relu(x * sc +
+// sh) rounded to T is re-formed in registers, as pw_fwd_kernel<BNA>), and the
+// block also emits the first stage of that BatchNorm's backward reduction over
+// its pixels -- sum dz, sum dz * (x - mean) * invstd with dz = the stored
+// (rounded) dx masked by the ReLU, vu_bn_bwd_reduce's arithmetic -- as
+// bnb[blk][2][C] (VuGemmFwd.bnb_part's layout), so the separate reduction
+// pass over dx and x is not run.
+template <typename T, bool BNA = false>
+__global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t dys, int64_t P, int C, int J,
+                              const float* w, T* dx, int64_t dxs, float* part, const float* bn_scale = nullptr,
+                              const float* bn_shift = nullptr, const float* bn_mean = nullptr,
+                              const float* bn_invstd = nullptr, float* bnb = nullptr) {
   __shared__ float sh[256 * 8];
   const int lpp = C >> 3;   // <= 32 enforced on host (C <= 256)
   const int ppw = 64 / lpp;
@@ -564,6 +587,13 @@ __global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t d
 #pragma unroll
     for (int k = 0; k < 8; ++k) { dw[j][k] = 0.f; wr[j][k] = j < J ? w[j * C + c + k] : 0.f; }
   }
+  float bsc[8], bsh[8], bmu[8], bis[8], z0[8], z1[8];
+  if constexpr (BNA)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bsc[k] = bn_scale[c + k]; bsh[k] = bn_shift[c + k]; bmu[k] = bn_mean[c + k]; bis[k] = bn_invstd[c + k];
+      z0[k] = 0.f; z1[k] = 0.f;
+    }
   for (int64_t p0 = (int64_t)blockIdx.x * TILE; p0 < P; p0 += (int64_t)gridDim.x * TILE) {
     for (int i = wv * ppw + slot; i < TILE; i += 4 * ppw) {
       int64_t p = p0 + i;
@@ -571,8 +601,14 @@ __global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t d
       float g[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) g[j] = j < J ? dy[p * dys + j] : 0.f;
-      float f[8];
+      float f[8], xr[8];
       load8<T>(x + p * xs + c, f);
+      if constexpr (BNA)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          xr[k] = f[k];
+          f[k] = rnd<T>(fmaxf(fmaf(xr[k], bsc[k], bsh[k]), 0.f));
+        }
       Vec8<T> o;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -580,6 +616,12 @@ __global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t d
 #pragma unroll
         for (int j = 0; j < 4; ++j) { dw[j][k] += g[j] * f[k]; s += g[j] * wr[j][k]; }
         o.set(k, s);
+        if constexpr (BNA) {
+          float dz = o.get(k);  // the stored (rounded) value, as the reduction pass would read it
+          if (!(xr[k] * bsc[k] + bsh[k] > 0.f)) dz = 0.f;
+          z0[k] += dz;
+          z1[k] += dz * ((xr[k] - bmu[k]) * bis[k]);
+        }
       }
       o.store(dx + p * dxs + c);
       if (sub == 0)
@@ -605,6 +647,21 @@ __global__ void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t d
       float s = 0.f;
       for (int t = 0; t < 256; ++t) s += sh[t];
       part[(int64_t)blockIdx.x * width + J * C + j] = s;
+    }
+  }
+  if constexpr (BNA) {
+    // threads with equal `sub` hold the same channels: fixed-order sums
+    for (int q = 0; q < 2; ++q) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = q ? z1[k] : z0[k];
+      __syncthreads();
+      for (int cc = threadIdx.x; cc < C; cc += 256) {
+        int sb_ = cc >> 3, k = cc & 7;
+        float s = 0.f;
+        for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
+        bnb[((int64_t)blockIdx.x * 2 + q) * C + cc] = s;
+      }
     }
   }
 }
@@ -713,6 +770,45 @@ extern "C" int vu_pointwise_fwd(const void* x, int64_t xs, int64_t P, int C, int
     hipLaunchKernelGGL((pw_fwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w, b, y,
                        ys);
   })
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_pointwise_bn_fwd(const void* x, int64_t xs, int64_t P, int C, int J, const float* bn_scale,
+                                   const float* bn_shift, const float* w, const float* b, float* y, int64_t ys,
+                                   int dtype, void* stream) {
+  if (C % 8 != 0 || xs % 8 != 0 || J < 1 || J > 4 || C > 512 || !pow2(C / 8) || !bn_scale || !bn_shift)
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (P == 0) return 0;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((pw_fwd_kernel<T, true>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w,
+                       b, y, ys, bn_scale, bn_shift);
+  })
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t vu_pointwise_bn_bwd_blocks(int64_t P) {
+  const int64_t nb = (P + TILE - 1) / TILE;
+  return nb < MAXB ? nb : MAXB;
+}
+
+extern "C" int vu_pointwise_bn_bwd(const void* x, int64_t xs, const float* bn_coef, int64_t coef_stride,
+                                   const float* dy, int64_t dys, int64_t P, int C, int J, const float* w, void* dx,
+                                   int64_t dxs, float* dw, float* db, int accumulate, float* workspace, float* bnb,
+                                   int dtype, void* stream) {
+  if (C % 8 != 0 || xs % 8 || dxs % 8 || J < 1 || J > 4 || !pow2(C / 8) || C / 8 > 32 || !bn_coef || !bnb ||
+      coef_stride < C)
+    return (int)hipErrorInvalidValue;
+  int nblk = (int)vu_pointwise_bn_bwd_blocks(P);
+  if (nblk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((pw_bwd_kernel<T, true>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w,
+                       (T*)dx, dxs, workspace, bn_coef, bn_coef + coef_stride, bn_coef + 2 * coef_stride,
+                       bn_coef + 3 * coef_stride, bnb);
+  })
+  hipLaunchKernelGGL(part_final, dim3((J * C + J + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, J * C + J, dw,
+                     J * C, db, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -535,9 +535,11 @@ def fold_bn_eval(M, conv, bn, cin_pad=None, cin_use=None):
 
 def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False, zbias=None, cin_use=None):
     """defer: leave BN + ReLU unapplied (returns a = None) when the consumer
-    is a MaxPool2d that applies it in the same pass (down_fwd).  zbias /
-    cin_use: the latent shortcut of a DecoderBlock conv1 (the conv contracts
-    over the first cin_use input channels; VuGemmFwd.zbias adds the rest)."""
+    is a MaxPool2d that applies it in the same pass (down_fwd); defer="any":
+    for any consumer that applies it itself (the OutConv kernel, outconv_fwd).
+    zbias / cin_use: the latent shortcut of a DecoderBlock conv1 (the conv
+    contracts over the first cin_use input channels; VuGemmFwd.zbias adds the
+    rest)."""
     N, _, H, W = srcs[0].shape
     co = conv.out_channels
     if can_fold(M, bn) and not defer:
@@ -548,7 +550,7 @@ def conv_bn_relu_fwd(M, srcs, conv, bn, cin_pad=None, defer=False, zbias=None, c
     y = M.act(N, co, H, W)
     st = K.gemm_fwd(K.gather3x3(srcs), w3x3_fwd(conv.weight, M.d, cin_pad, cin_use), co, y, M.d,
                     stats=bn.training, zbias=zbias)
-    if defer and K.pool_fusable(y):
+    if defer == "any" or (defer and K.pool_fusable(y)):
         return None, (y, bn_coef(bn, st, co))
     a = M.act(N, co, H, W)
     coef = bn_fwd_apply(bn, st, y, a, True, M)
@@ -607,11 +609,13 @@ def double_conv_fwd(M, seq, srcs, cin_pad=None, defer=False):
     return a2, (srcs, a1, s1, s2)
 
 
-def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None):
+def double_conv_bwd(M, seq, saved, da2, need_dsrc, cvalid=None, da2_part=None):
+    """da2_part: BN2's first backward reduction stage, emitted by the kernel
+    that produced da2 (outconv_bwd with a deferred BN2)."""
     conv1, bn1, _, conv2, bn2, _ = seq
     srcs, a1, s1, s2 = saved
     # conv2's input gradient also emits BN1's first backward reduction stage
-    da1, part = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True, feeds=(s1, bn1))
+    da1, part = conv_bn_relu_bwd(M, [a1], conv2, bn2, s2, da2, True, feeds=(s1, bn1), da_part=da2_part)
     return conv_bn_relu_bwd(M, srcs, conv1, bn1, s1, da1, need_dsrc, cvalid, da_part=part)
 
 
@@ -741,7 +745,9 @@ def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
 # ----------------------------------------------------------------------------
 # Up (unet_parts.py:65-95): up(x1) -> F.pad -> attention(x1, x2) -> cat([x2, x1]) -> DoubleConv
 # ----------------------------------------------------------------------------
-def up_fwd(M, mod, x1, x2):
+def up_fwd(M, mod, x1, x2, defer_out=False):
+    """defer_out: leave the DoubleConv's BN2 + ReLU unapplied (out None; its
+    (y2, coef2) is saved[5][3]) for a consumer that applies it itself."""
     N, _, H, W = x2.shape
     h, w = x1.shape[2], x1.shape[3]
     bilinear = isinstance(mod.up, torch.nn.Upsample)
@@ -770,15 +776,15 @@ def up_fwd(M, mod, x1, x2):
             K.gemm_fwd(K.gather1x1([x1]), wT_fwd(mod.up.weight, M.d), 4 * cu, u, M.d,
                        bias=mod.up.bias, convT=(H, W, py, px, cu))
     x2a, satt = attention_fwd(M, mod.attention, u, x2)
-    out, sdc = double_conv_fwd(M, mod.conv.double_conv, [x2a, u])
+    out, sdc = double_conv_fwd(M, mod.conv.double_conv, [x2a, u], defer="any" if defer_out else False)
     return out, (x1, x2, u, (py, px, uh, uw), satt, sdc)
 
 
-def up_bwd(M, mod, saved, dout):
+def up_bwd(M, mod, saved, dout, dout_part=None):
     x1, x2, u, (py, px, uh, uw), satt, sdc = saved
     N, cs, H, W = x2.shape
     cu = u.shape[1]
-    dcat = double_conv_bwd(M, mod.conv.double_conv, sdc, dout, True)
+    dcat = double_conv_bwd(M, mod.conv.double_conv, sdc, dout, True, da2_part=dout_part)
     dx2a = dcat[:, :cs]
     du = dcat[:, cs:]
     dx2 = attention_bwd(M, mod.attention, satt, dx2a, (dcat, cs), True)
@@ -810,17 +816,42 @@ def up_bwd(M, mod, saved, dout):
 # ----------------------------------------------------------------------------
 # OutConv (unet_parts.py:97-103): 1x1 conv + bias, fp32 logits
 # ----------------------------------------------------------------------------
-def outconv_fwd(M, conv, x):
-    N, Cc, H, W = x.shape
+# OutConv over the UNet's last BatchNorm + ReLU applied in its operand path
+# (round 6): up4's DoubleConv leaves BN2 unapplied (defer "any"), the 1x1
+# kernel forms a = relu(y2 * scale + shift) in registers (bit-identical to the
+# applied bytes), and its backward re-forms a for the weight gradient and
+# emits BN2's first backward reduction stage over the gradient it writes --
+# the BN2 apply pass and the BN2 reduction pass are not run.  A/B switch.
+FUSE_OUTCONV_BN = True
+
+
+def outconv_fusable(x_channels, n_classes):
+    return FUSE_OUTCONV_BN and x_channels % 8 == 0 and x_channels <= 256 and \
+        (x_channels // 8) & (x_channels // 8 - 1) == 0 and 1 <= n_classes <= 4
+
+
+def outconv_fwd(M, conv, x, pend=None):
+    """pend = (y, coef): x is None and the operand is relu(BN(y)) (the
+    producing DoubleConv's deferred BN2)."""
+    src = x if pend is None else pend[0]
+    N, Cc, H, W = src.shape
     J = conv.out_channels
-    y = torch.empty((N, J, H, W), dtype=torch.float32, device=x.device, memory_format=K.CL)
-    K.call("vu_pointwise_fwd", K.ptr(x), K.pstride(x), N * H * W, Cc, J, K.ptr(conv.weight),
-           K.ptr(conv.bias), K.ptr(y), J, M.d, K.stream())
-    return y, (x,)
+    y = torch.empty((N, J, H, W), dtype=torch.float32, device=src.device, memory_format=K.CL)
+    if pend is None:
+        K.call("vu_pointwise_fwd", K.ptr(x), K.pstride(x), N * H * W, Cc, J, K.ptr(conv.weight),
+               K.ptr(conv.bias), K.ptr(y), J, M.d, K.stream())
+        return y, (x,)
+    yb, coef = pend
+    K.call("vu_pointwise_bn_fwd", K.ptr(yb), K.pstride(yb), N * H * W, Cc, J, K.ptr(coef[0]), K.ptr(coef[1]),
+           K.ptr(conv.weight), K.ptr(conv.bias), K.ptr(y), J, M.d, K.stream())
+    return y, (yb, coef)
 
 
 def outconv_bwd(M, conv, saved, dy):
-    (x,) = saved
+    """Returns the gradient of OutConv's input, or (da2, BnbPart) for a
+    deferred BN2 (saved = (y2, coef2)): da2 is the gradient w.r.t. the
+    never-stored relu(BN2(y2)) and the part BN2's first reduction stage."""
+    x = saved[0]
     N, Cc, H, W = x.shape
     J = conv.out_channels
     dy = dy.float().contiguous(memory_format=K.CL)
@@ -828,11 +859,20 @@ def outconv_bwd(M, conv, saved, dy):
     gb, _ = grad_sink(conv.bias)
     dx = torch.empty_like(x)
     ws = K.workspace_f32(K.query("vu_pointwise_bwd_workspace_bytes", N * H * W, Cc, J), x.device)
-    K.call("vu_pointwise_bwd", K.ptr(x), K.pstride(x), K.ptr(dy), J, N * H * W, Cc, J,
-           K.ptr(conv.weight), K.ptr(dx), K.pstride(dx), K.ptr(gw), K.ptr(gb), 1 if acc else 0,
-           K.ptr(ws), M.d, K.stream())
+    if len(saved) == 1:
+        K.call("vu_pointwise_bwd", K.ptr(x), K.pstride(x), K.ptr(dy), J, N * H * W, Cc, J,
+               K.ptr(conv.weight), K.ptr(dx), K.pstride(dx), K.ptr(gw), K.ptr(gb), 1 if acc else 0,
+               K.ptr(ws), M.d, K.stream())
+        M.notify([conv.weight, conv.bias])
+        return dx
+    coef = saved[1]
+    nblk = K.query("vu_pointwise_bn_bwd_blocks", N * H * W)
+    bnb = torch.empty((nblk, 2, Cc), dtype=torch.float32, device=x.device)
+    K.call("vu_pointwise_bn_bwd", K.ptr(x), K.pstride(x), K.ptr(coef), coef.stride(0), K.ptr(dy), J, N * H * W,
+           Cc, J, K.ptr(conv.weight), K.ptr(dx), K.pstride(dx), K.ptr(gw), K.ptr(gb), 1 if acc else 0,
+           K.ptr(ws), K.ptr(bnb), M.d, K.stream())
     M.notify([conv.weight, conv.bias])
-    return dx
+    return dx, K.BnbPart(bnb, nblk, x)
 
 
 # ----------------------------------------------------------------------------

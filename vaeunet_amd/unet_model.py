@@ -48,14 +48,20 @@ class UNet(nn.Module):
         y, u1 = E.up_fwd(M, self.up1, x5, x4)
         y, u2 = E.up_fwd(M, self.up2, y, x3)
         y, u3 = E.up_fwd(M, self.up3, y, x2)
-        y, u4 = E.up_fwd(M, self.up4, y, x1)
-        logits, so = E.outconv_fwd(M, self.outc.conv, y)
+        # up4's BN2 + ReLU is applied inside OutConv's kernels (engine.outconv_fwd)
+        fuse = E.outconv_fusable(self.up4.conv.double_conv[3].out_channels, self.n_classes)
+        y, u4 = E.up_fwd(M, self.up4, y, x1, defer_out=fuse)
+        pend = u4[5][3] if y is None else None
+        logits, so = E.outconv_fwd(M, self.outc.conv, y, pend=pend)
         return logits, (s0, s1, s2, s3, s4, u1, u2, u3, u4, so)
 
     def _bwd(self, M, state, dlogits, need_dx):
         s0, s1, s2, s3, s4, u1, u2, u3, u4, so = state
         dy = E.outconv_bwd(M, self.outc.conv, so, dlogits)
-        dy, dx1 = E.up_bwd(M, self.up4, u4, dy)
+        part = None
+        if isinstance(dy, tuple):
+            dy, part = dy
+        dy, dx1 = E.up_bwd(M, self.up4, u4, dy, dout_part=part)
         dy, dx2 = E.up_bwd(M, self.up3, u3, dy)
         dy, dx3 = E.up_bwd(M, self.up2, u2, dy)
         dx5, dx4 = E.up_bwd(M, self.up1, u1, dy)
