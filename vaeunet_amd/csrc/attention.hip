@@ -474,7 +474,7 @@ __global__ void part_final(const float* part, int nblk, int width, float* out, i
 // type -- exactly the bytes vu_bn_apply would have stored -- formed in
 // registers, so the UNet's last BatchNorm + ReLU is never materialised
 // (unet_parts.py:44-45 feeding OutConv :100).
-template <typename T, bool BNA = false>
+template <typename T, bool BNA = false, int JM = 4>
 __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, const float* w, const float* b,
                               float* y, int64_t ys, const float* bn_scale = nullptr, const float* bn_shift = nullptr) {
   const int lpp = C >> 3 > 64 ? 64 : C >> 3;
@@ -490,9 +490,11 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
     // (cold-cache 512^2 x 64 -> 2: 135 -> 107 us with the DPP group sums)
     constexpr int PU = 4;   // (8 rows in flight: 144 VGPRs, 3 waves per SIMD, measured 71 -> 91 us)
     const int c = sub * 8;
-    float wr[4][8], bj[4], bsc[8], bsh[8];
+    // JM: the largest J this instantiation serves (outputs j >= J carry zero
+    // weights); JM = 2 halves the FMAs and group sums of the UNet's 2-class head
+    float wr[JM][8], bj[JM], bsc[8], bsh[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < JM; ++j) {
       bj[j] = (j < J && b) ? b[j] : 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k) wr[j][k] = j < J ? w[j * C + c + k] : 0.f;
@@ -524,9 +526,9 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
         const int64_t p = pb + u * ppw + slot;
-        float acc[4];
+        float acc[JM];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < JM; ++j) {
           acc[j] = 0.f;
 #pragma unroll
           for (int k = 0; k < 8; ++k) acc[j] += f[u][k] * wr[j][k];
@@ -568,7 +570,7 @@ __global__ void pw_fwd_kernel(const T* x, int64_t xs, int64_t P, int C, int J, c
 // (rounded) dx masked by the ReLU, vu_bn_bwd_reduce's arithmetic -- as
 // bnb[blk][2][C] (VuGemmFwd.bnb_part's layout), so the separate reduction
 // pass over dx and x is not run.
-template <typename T, bool BNA = false>
+template <typename T, bool BNA = false, int JM = 4>
 __global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, const float* dy, int64_t dys, int64_t P, int C, int J,
                               const float* w, T* dx, int64_t dxs, float* part, const float* bn_scale = nullptr,
                               const float* bn_shift = nullptr, const float* bn_mean = nullptr,
@@ -580,9 +582,10 @@ __global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, con
   const int sub = lane % lpp, slot = lane / lpp;
   const int c = sub * 8;
   const int width = J * C + J;
-  float dw[4][8], db[4], wr[4][8];
+  // JM as in pw_fwd_kernel: dy columns j >= J are read as zero
+  float dw[JM][8], db[JM], wr[JM][8];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < JM; ++j) {
     db[j] = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) { dw[j][k] = 0.f; wr[j][k] = j < J ? w[j * C + c + k] : 0.f; }
@@ -594,39 +597,58 @@ __global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, con
       bsc[k] = bn_scale[c + k]; bsh[k] = bn_shift[c + k]; bmu[k] = bn_mean[c + k]; bis[k] = bn_invstd[c + k];
       z0[k] = 0.f; z1[k] = 0.f;
     }
+  // PU pixel rows per lane are loaded (from clamped addresses, unconditionally)
+  // before any is used: a guarded load per pixel serialised the round trips
+  // (as pw_fwd_kernel); rows past the tile or P get a zero dy, so they add
+  // nothing to dw, db or the BatchNorm sums, and are not stored.
+  constexpr int PU = 2;
+  const int step = 4 * ppw;
   for (int64_t p0 = (int64_t)blockIdx.x * TILE; p0 < P; p0 += (int64_t)gridDim.x * TILE) {
-    for (int i = wv * ppw + slot; i < TILE; i += 4 * ppw) {
-      int64_t p = p0 + i;
-      if (p >= P) continue;
-      float g[4];
+    for (int i0 = wv * ppw + slot; i0 < TILE; i0 += step * PU) {
+      float g[PU][JM], f[PU][8], xr[PU][8];
+      bool ok[PU];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] = j < J ? dy[p * dys + j] : 0.f;
-      float f[8], xr[8];
-      load8<T>(x + p * xs + c, f);
-      if constexpr (BNA)
+      for (int u = 0; u < PU; ++u) {
+        const int64_t p = p0 + i0 + u * step;
+        ok[u] = i0 + u * step < TILE && p < P;
+        const int64_t pc = p < P ? p : P - 1;
+#pragma unroll
+        for (int j = 0; j < JM; ++j) g[u][j] = j < J ? dy[pc * dys + j] : 0.f;
+        load8<T>(x + pc * xs + c, f[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        if (!ok[u])
+#pragma unroll
+          for (int j = 0; j < JM; ++j) g[u][j] = 0.f;
+        if constexpr (BNA)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            xr[u][k] = f[u][k];
+            f[u][k] = rnd<T>(fmaxf(fmaf(xr[u][k], bsc[k], bsh[k]), 0.f));
+          }
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        Vec8<T> o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xr[k] = f[k];
-          f[k] = rnd<T>(fmaxf(fmaf(xr[k], bsc[k], bsh[k]), 0.f));
-        }
-      Vec8<T> o;
+          float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { dw[j][k] += g[j] * f[k]; s += g[j] * wr[j][k]; }
-        o.set(k, s);
-        if constexpr (BNA) {
-          float dz = o.get(k);  // the stored (rounded) value, as the reduction pass would read it
-          if (!(xr[k] * bsc[k] + bsh[k] > 0.f)) dz = 0.f;
-          z0[k] += dz;
-          z1[k] += dz * ((xr[k] - bmu[k]) * bis[k]);
+          for (int j = 0; j < JM; ++j) { dw[j][k] += g[u][j] * f[u][k]; s += g[u][j] * wr[j][k]; }
+          o.set(k, s);
+          if constexpr (BNA) {
+            float dz = o.get(k);  // the stored (rounded) value, as the reduction pass would read it
+            if (!(xr[u][k] * bsc[k] + bsh[k] > 0.f)) dz = 0.f;
+            z0[k] += dz;
+            z1[k] += dz * ((xr[u][k] - bmu[k]) * bis[k]);
+          }
         }
+        if (ok[u]) o.store(dx + (p0 + i0 + u * step) * dxs + c);
+        if (sub == 0)
+#pragma unroll
+          for (int j = 0; j < JM; ++j) db[j] += g[u][j];
       }
-      o.store(dx + p * dxs + c);
-      if (sub == 0)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) db[j] += g[j];
     }
   }
   for (int j = 0; j < J; ++j) {
@@ -767,8 +789,12 @@ extern "C" int vu_pointwise_fwd(const void* x, int64_t xs, int64_t P, int C, int
   hipStream_t st = (hipStream_t)stream;
   if (P == 0) return 0;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((pw_fwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w, b, y,
-                       ys);
+    if (J <= 2 && C <= 512)
+      hipLaunchKernelGGL((pw_fwd_kernel<T, false, 2>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J,
+                         w, b, y, ys);
+    else
+      hipLaunchKernelGGL((pw_fwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w, b, y,
+                         ys);
   })
   return (int)hipGetLastError();
 }
@@ -781,8 +807,12 @@ extern "C" int vu_pointwise_bn_fwd(const void* x, int64_t xs, int64_t P, int C, 
   hipStream_t st = (hipStream_t)stream;
   if (P == 0) return 0;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((pw_fwd_kernel<T, true>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w,
-                       b, y, ys, bn_scale, bn_shift);
+    if (J <= 2)
+      hipLaunchKernelGGL((pw_fwd_kernel<T, true, 2>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J,
+                         w, b, y, ys, bn_scale, bn_shift);
+    else
+      hipLaunchKernelGGL((pw_fwd_kernel<T, true>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)x, xs, P, C, J, w,
+                         b, y, ys, bn_scale, bn_shift);
   })
   return (int)hipGetLastError();
 }
@@ -803,9 +833,14 @@ extern "C" int vu_pointwise_bn_bwd(const void* x, int64_t xs, const float* bn_co
   if (nblk == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((pw_bwd_kernel<T, true>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w,
-                       (T*)dx, dxs, workspace, bn_coef, bn_coef + coef_stride, bn_coef + 2 * coef_stride,
-                       bn_coef + 3 * coef_stride, bnb);
+    if (J <= 2)
+      hipLaunchKernelGGL((pw_bwd_kernel<T, true, 2>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J,
+                         w, (T*)dx, dxs, workspace, bn_coef, bn_coef + coef_stride, bn_coef + 2 * coef_stride,
+                         bn_coef + 3 * coef_stride, bnb);
+    else
+      hipLaunchKernelGGL((pw_bwd_kernel<T, true>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w,
+                         (T*)dx, dxs, workspace, bn_coef, bn_coef + coef_stride, bn_coef + 2 * coef_stride,
+                         bn_coef + 3 * coef_stride, bnb);
   })
   hipLaunchKernelGGL(part_final, dim3((J * C + J + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, J * C + J, dw,
                      J * C, db, accumulate);
@@ -827,8 +862,12 @@ extern "C" int vu_pointwise_bwd(const void* x, int64_t xs, const float* dy, int6
   if (nblk > MAXB) nblk = MAXB;
   hipStream_t st = (hipStream_t)stream;
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((pw_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w, (T*)dx,
-                       dxs, workspace);
+    if (J <= 2)
+      hipLaunchKernelGGL((pw_bwd_kernel<T, false, 2>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J,
+                         w, (T*)dx, dxs, workspace);
+    else
+      hipLaunchKernelGGL((pw_bwd_kernel<T>), dim3(nblk), dim3(256), 0, st, (const T*)x, xs, dy, dys, P, C, J, w,
+                         (T*)dx, dxs, workspace);
   })
   hipLaunchKernelGGL(part_final, dim3((J * C + J + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, J * C + J, dw, J * C,
                      db, accumulate);
