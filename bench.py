@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--model", choices=("unet", "vae"), default="unet",
                     help="unet = BASELINE configs[1] (the metric); vae = configs[2], UNetResNet + KL")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--layer-table", action="store_true",
+                    help="print the roofline leg's per-launch GEMM table (shape, kernel, time) to stderr")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the config-3 (VAE) secondary line that a default N=1 UNet run appends "
@@ -517,9 +519,15 @@ def main():
     if not args.no_roofline:
         # live per-launch HIP-event timing of the 3x3 implicit-GEMM kernels over
         # 2 further steps (events on the launch stream, one pair per launch)
-        K.TIMER = K.LaunchTimer()
+        K.TIMER = K.LaunchTimer(detail=args.layer_table)
         for _ in range(2):
             eager_step()   # the same kernels, launched one by one so each can be bracketed
+        if args.layer_table and rank == 0:
+            # per-launch table of the second step (stderr): kind, shape, kernel, us, TFLOP/s
+            recs = K.TIMER.per_launch()
+            for tag, shape, kn, ms, fl in recs[len(recs) // 2:]:
+                print(f"LAYER {tag:22s} {shape:40s} {kn:40s} {ms * 1e3:8.1f} us {fl / ms / 1e9:7.0f} TF",
+                      file=sys.stderr)
         summ = K.TIMER.summary()
         K.TIMER = None
         fam = {k: v for k, v in summ.items() if k.startswith("conv3x3_") and "image" not in k}

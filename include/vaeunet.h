@@ -816,7 +816,7 @@ typedef struct VuZbJob {
   float* part;                 /* the consumer's VuLatentJob.part ([N][32][L]) */
   float* dw;                   /* conv1.weight.grad (strides of w): z columns written, or added when grad_acc */
   int32_t grad_acc;
-  int32_t pad_;
+  int32_t rs_ready;            /* 1: rs's region partials already written (vu_bn_bwd_apply_zrs): no region pass */
   int64_t block0;
 } VuZbJob;
 /* 1 when the shortcut serves N samples, L latent channels and co conv1 outputs */
@@ -824,10 +824,22 @@ int vu_zbias_supported(int N, int L, int co);
 int64_t vu_zbias_rs_floats(int N, int co, int H, int W);
 /* the [N][9][co] tables of every job (one launch) */
 int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream);
-/* region sums of every job's dy (partials per ~64 KB pixel chunk, then their
- * sums), then dW's z columns and the dc partials (three launches); dtype:
- * dy's storage (VU_BF16 / VU_F32) */
+/* region sums of every job's dy (partials per ~64 KB pixel chunk -- skipped
+ * for jobs with rs_ready -- then their sums), then dW's z columns and the dc
+ * partials (three launches, two when every job has rs_ready); dtype: dy's
+ * storage (VU_BF16 / VU_F32) */
 int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, void* stream);
+/* BatchNorm(+ReLU) backward apply (vu_bn_bwd_apply's arithmetic, coef from
+ * vu_bn_bwd_reduce / vu_bn_bwd_finish) of a shortcut conv1's BatchNorm over
+ * N x H x W x C, also writing the region partials of the dy it stores into rs
+ * (the first N * nchunks * 5 * C floats of a vu_zbias_rs_floats buffer; the
+ * job then passes rs_ready = 1): dy and rs bit-identical to vu_bn_bwd_apply
+ * followed by vu_zbias_bwd's region pass.  Replaces the backward re-read of
+ * dy for unet_resnet.py:92-99's z channels. */
+int vu_bn_bwd_apply_zrs_ok(int H, int W, int C, int64_t dzs, int64_t xs, int64_t dys);
+int vu_bn_bwd_apply_zrs(const void* dz, int64_t dzs, const void* x, int64_t xs, int N, int H, int W, int C,
+                        const float* scale, const float* shift, const float* mean, const float* coef, int relu,
+                        void* dy, int64_t dys, float* rs, int dtype, void* stream);
 /* 0 when a consumer of this geometry is served (co = 8 * 2^k <= 2048, cpad % 8,
  * stride % 8), else hipErrorInvalidValue */
 int vu_latent_check_job(int co, int cpad, int64_t out_stride, int dtype);

@@ -88,9 +88,9 @@ def _oracle64(model, x, t, eps, inj):
             R.PROBE = None
         return {k: v.grad for k, v in p.items() if v.grad is not None}, terms
     g64, t64 = run(torch.float64)
-    _, t32 = run(torch.float32)
+    g32, t32 = run(torch.float32)
     sigma = {k: float((t32[k] - t64[k]).norm()) for k in t64 if k in t32}
-    return g64, sigma
+    return g64, sigma, g32
 
 
 @pytest.mark.parametrize("inj", ["all", "first", "bottleneck", "none", "inject_no_bottleneck"])
@@ -108,7 +108,7 @@ def test_latent_vector_path_matches_map_path(inj, bf16, sc):
     eps = torch.randn(B, 32, device=DEV)
     a = _model(inj)
     b = copy.deepcopy(a)
-    g64, sigma = _oracle64(a, x, t, eps, inj)
+    g64, sigma, g32 = _oracle64(a, x, t, eps, inj)
     ra = _run(a, x, t, eps, True, bf16, steps=1, shortcut=sc)
     rb = _run(b, x, t, eps, False, bf16, steps=1)
     tol = 3e-2 if bf16 else 1e-4
@@ -124,7 +124,13 @@ def test_latent_vector_path_matches_map_path(inj, bf16, sc):
         ga, gb = pa[k].grad, pb[k].grad
         da = float((ga.double().cpu() - ref).norm())
         db = float((gb.double().cpu() - ref).norm())
-        base = fac * db + floor * gmax
+        # the reference error is the map path's or, when larger, the fp32
+        # oracle's own (CPU, same inputs): downstream of the psi BatchNorm(1)
+        # sums (cancellation ~1e3) two independent fp32 noise draws differ by
+        # 2x at random, and the vector path is held to the oracle as every
+        # other fp32 parity test is (round 6)
+        d32 = float((g32[k].double().cpu() - ref).norm()) if (not bf16 and k in g32) else 0.0
+        base = fac * max(db, d32) + floor * gmax
         # the BatchNorm term spread may widen the bound, but never past half
         # the gradient's norm (an uncapped sigma passed ~1.2 |g|)
         bound[k] = max(base, min(base + fac * sigma.get(k, 0.0), 0.5 * float(ref.norm())))

@@ -164,3 +164,105 @@ def test_zbias_backward_matches_map_gradient(mode, shape, acc, cl):
     got_dc = part.view(N, 32, L).double().cpu().sum(1)
     assert bool(((got_dc - dc).abs() <= 1e-5 * dmapa.sum((2, 3)) + 1e-12).all())
     assert not bool(torch.isnan(part).any())   # every split written (unused ones zero)
+
+
+@pytest.mark.parametrize("mode", ["bf16", "f32"])
+@pytest.mark.parametrize("shape", [(8, 32, 16, 16, 64), (2, 32, 7, 12, 512), (3, 16, 2, 5, 96), (2, 16, 48, 72, 64),
+                                   (2, 16, 9, 40, 1024), (2, 16, 64, 64, 128)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_fused_region_partials_bit_identical(mode, shape, relu):
+    """Round 6: conv1's BatchNorm backward apply with the shortcut's region
+    partials (vu_bn_bwd_apply_zrs) against vu_bn_bwd_apply followed by
+    vu_zbias_bwd's own region pass -- dy, every rs float and the outputs of
+    the remaining launches (z columns of dW, dc partials) bit-identical."""
+    from vaeunet_amd import kernels as K
+    N, L, H, W, co = shape
+    lead = 64
+    dt = torch.bfloat16 if mode == "bf16" else torch.float32
+    dcode = 1 if mode == "bf16" else 0
+    g = torch.Generator().manual_seed(31)
+    w = (torch.randn(co, lead + L, 3, 3, generator=g) / 10).to(DEV).contiguous(memory_format=CL)
+    act = torch.rand(N, L, generator=g).to(DEV)
+    da = torch.randn(N, co, H, W, generator=g).to(dt).to(DEV).contiguous(memory_format=CL)
+    x = torch.randn(N, co, H, W, generator=g).to(dt).to(DEV).contiguous(memory_format=CL)
+    scale = (torch.rand(co, generator=g) + 0.5).to(DEV)
+    shift = (torch.randn(co, generator=g) * 0.3).to(DEV)
+    mean = (torch.randn(co, generator=g) * 0.2).to(DEV)
+    k = torch.randn(3, co, generator=g).to(DEV).contiguous()
+    out = []
+    for fused in (False, True):
+        dy = torch.full_like(da, float("nan"))
+        rs = torch.full((K.query("vu_zbias_rs_floats", N, co, H, W),), float("nan"), dtype=torch.float32, device=DEV)
+        part = torch.full((N * 32 * L,), float("nan"), dtype=torch.float32, device=DEV)
+        dw = torch.zeros(co, lead + L, 3, 3, device=DEV).contiguous(memory_format=CL)
+        if fused:
+            assert K.query("vu_bn_bwd_apply_zrs_ok", H, W, co, K.pstride(da), K.pstride(x), K.pstride(dy))
+            K.call("vu_bn_bwd_apply_zrs", da.data_ptr(), K.pstride(da), x.data_ptr(), K.pstride(x), N, H, W, co,
+                   scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), k.data_ptr(), 1 if relu else 0,
+                   dy.data_ptr(), K.pstride(dy), rs.data_ptr(), dcode, K.stream())
+        else:
+            K.call("vu_bn_bwd_apply", da.data_ptr(), K.pstride(da), x.data_ptr(), K.pstride(x), N * H * W, co,
+                   scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), k.data_ptr(), 1 if relu else 0,
+                   dy.data_ptr(), K.pstride(dy), dcode, K.stream())
+        arr = (type(_job(w, lead, L, H, W, act)) * 1)()
+        j = _job(w, lead, L, H, W, act)
+        j.dy, j.dy_stride = dy.data_ptr(), K.pstride(dy)
+        j.rs, j.part, j.dw, j.grad_acc = rs.data_ptr(), part.data_ptr(), dw.data_ptr(), 0
+        j.rs_ready = 1 if fused else 0
+        arr[0] = j
+        K.call("vu_zbias_bwd", arr, 1, N, dcode, K.stream())
+        torch.cuda.synchronize()
+        out.append((dy.clone(), rs.clone(), part.clone(), dw.clone()))
+    (dy0, rs0, p0, w0), (dy1, rs1, p1, w1) = out
+    assert not bool(torch.isnan(dy1.float()).any()) and not bool(torch.isnan(rs1).any())
+    assert torch.equal(dy0, dy1)
+    assert torch.equal(rs0, rs1)
+    assert torch.equal(p0, p1)
+    assert torch.equal(w0, w1)
+
+
+def test_region_pass_skips_only_ready_jobs():
+    """Two shortcut jobs in one vu_zbias_bwd, only the first with its
+    partials from the fused apply (rs_ready): both jobs' outputs equal the
+    all-unfused run bit for bit (the second job's region pass still runs)."""
+    from vaeunet_amd import kernels as K
+    N, L, dcode = 2, 16, 1
+    g = torch.Generator().manual_seed(5)
+    shapes = [(16, 20, 64), (8, 12, 128)]
+    jobs = []
+    for H, W, co in shapes:
+        w = (torch.randn(co, 64 + L, 3, 3, generator=g) / 10).to(DEV).contiguous(memory_format=CL)
+        act = torch.rand(N, L, generator=g).to(DEV)
+        da = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=CL)
+        x = torch.randn(N, co, H, W, generator=g).to(torch.bfloat16).to(DEV).contiguous(memory_format=CL)
+        bn = [(torch.rand(co, generator=g) + 0.5).to(DEV), (torch.randn(co, generator=g) * 0.3).to(DEV),
+              (torch.randn(co, generator=g) * 0.2).to(DEV), torch.randn(3, co, generator=g).to(DEV).contiguous()]
+        jobs.append((H, W, co, w, act, da, x, bn))
+    res = []
+    for fuse_first in (False, True):
+        arr = (type(_job(jobs[0][3], 64, L, 4, 4, jobs[0][4])) * 2)()
+        outs = []
+        for i, (H, W, co, w, act, da, x, bn) in enumerate(jobs):
+            dy = torch.empty_like(da)
+            rs = torch.full((K.query("vu_zbias_rs_floats", N, co, H, W),), float("nan"), device=DEV)
+            part = torch.full((N * 32 * L,), float("nan"), device=DEV)
+            dw = torch.zeros(co, 64 + L, 3, 3, device=DEV).contiguous(memory_format=CL)
+            args = (bn[0].data_ptr(), bn[1].data_ptr(), bn[2].data_ptr(), bn[3].data_ptr(), 1)
+            if fuse_first and i == 0:
+                K.call("vu_bn_bwd_apply_zrs", da.data_ptr(), K.pstride(da), x.data_ptr(), K.pstride(x), N, H, W, co,
+                       *args, dy.data_ptr(), K.pstride(dy), rs.data_ptr(), dcode, K.stream())
+            else:
+                K.call("vu_bn_bwd_apply", da.data_ptr(), K.pstride(da), x.data_ptr(), K.pstride(x), N * H * W, co,
+                       *args, dy.data_ptr(), K.pstride(dy), dcode, K.stream())
+            j = _job(w, 64, L, H, W, act)
+            j.dy, j.dy_stride = dy.data_ptr(), K.pstride(dy)
+            j.rs, j.part, j.dw, j.grad_acc = rs.data_ptr(), part.data_ptr(), dw.data_ptr(), 0
+            j.rs_ready = 1 if (fuse_first and i == 0) else 0
+            arr[i] = j
+            outs.append((dy, rs, part, dw))
+        K.call("vu_zbias_bwd", arr, 2, N, dcode, K.stream())
+        torch.cuda.synchronize()
+        res.append([tuple(t.clone() for t in o) for o in outs])
+    for a, b in zip(res[0], res[1]):
+        for ta, tb in zip(a, b):
+            assert torch.equal(ta, tb)

@@ -82,7 +82,7 @@ class VuZbJob(C.Structure):
     _fields_ = [("w", _p), ("ws_co", _l), ("ws_ci", _l), ("ws_ky", _l), ("ws_kx", _l), ("cz0", C.c_int32),
                 ("L", C.c_int32), ("co", C.c_int32), ("H", C.c_int32), ("W", C.c_int32), ("act", _p),
                 ("row_scale", _p), ("table", _p), ("dy", _p), ("dy_stride", _l), ("rs", _p), ("part", _p),
-                ("dw", _p), ("grad_acc", C.c_int32), ("pad_", C.c_int32), ("block0", _l)]
+                ("dw", _p), ("grad_acc", C.c_int32), ("rs_ready", C.c_int32), ("block0", _l)]
 
 
 class VuLatentHeads(C.Structure):
@@ -198,6 +198,8 @@ _SIGS = {
     "vu_zbias_rs_floats": (_l, [_i, _i, _i, _i]),
     "vu_zbias_fwd": (_i, [_p, _i, _i, _p]),
     "vu_zbias_bwd": (_i, [_p, _i, _i, _i, _p]),
+    "vu_bn_bwd_apply_zrs_ok": (_i, [_i, _i, _i, _l, _l, _l]),
+    "vu_bn_bwd_apply_zrs": (_i, [_p, _l, _p, _l, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _l, _p, _i, _p]),
     "vu_mean_groups": (_i, [_p, _i, _l, _p, _p]),
     "vu_sigmoid": (_i, [_p, _l, _p, _p]),
     "vu_patch_blend": (_i, [_p, _l, _i, _i, _i, _p, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p]),

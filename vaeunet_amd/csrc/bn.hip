@@ -294,7 +294,7 @@ __global__ void chan_partial_kernel(RedArgs r) {
         for (int i = 0; i < 8; ++i) {
           float xv = vb[u].get(i);
           float dz = va[u].get(i);
-          if (r.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+          if (r.relu && !(fmaf(xv, sc[i], sf[i]) > 0.f)) dz = 0.f;
           s0[i] += dz;
           s1[i] += dz * ((xv - mu[i]) * is[i]);
         }
@@ -426,8 +426,8 @@ __global__ void bn_bwd_apply_kernel(const T* dy, int64_t dys, const T* x, int64_
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         float xv = vx[u].get(i), dz = vd[u].get(i);
-        if (relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
-        vo.set(i, k1[i] * dz + k2[i] * (xv - mu[i]) + k3[i]);
+        if (relu && !(fmaf(xv, sc[i], sf[i]) > 0.f)) dz = 0.f;
+        vo.set(i, fmaf(k1[i], dz, k2[i] * (xv - mu[i])) + k3[i]);
       }
       vo.store(dx + p * dxs + c);
     }
@@ -444,8 +444,8 @@ __global__ void bn_bwd_apply_scalar(const T* dy, int64_t dys, const T* x, int64_
     int64_t p = e / C;
     int c = (int)(e - p * C);
     float xv = ld1<T>(x + p * xs + c), dz = ld1<T>(dy + p * dys + c);
-    if (relu && !(xv * scale[c] + shift[c] > 0.f)) dz = 0.f;
-    st1<T>(dx + p * dxs + c, coef[c] * dz + coef[C + c] * (xv - mean[c]) + coef[2 * C + c]);
+    if (relu && !(fmaf(xv, scale[c], shift[c]) > 0.f)) dz = 0.f;
+    st1<T>(dx + p * dxs + c, fmaf(coef[c], dz, coef[C + c] * (xv - mean[c])) + coef[2 * C + c]);
   }
 }
 
@@ -897,8 +897,8 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_apply_kernel(BnBwdFusedArgs 
       for (int i = 0; i < 8; ++i) {
         const float xv = vx[u].get(i);
         float dz = vd[u].get(i);
-        if (a.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
-        vo.set(i, k1[i] * dz + k2[i] * (xv - mu[i]) + k3[i]);
+        if (a.relu && !(fmaf(xv, sc[i], sf[i]) > 0.f)) dz = 0.f;
+        vo.set(i, fmaf(k1[i], dz, k2[i] * (xv - mu[i])) + k3[i]);
       }
       vo.store(dx + p * a.dxs + c);
     }
@@ -1336,7 +1336,7 @@ __global__ __launch_bounds__(ONEPASS_T) void bn_bwd_onepass_kernel(BnBwdFusedArg
       for (int i = 0; i < 8; ++i) {
         const float xv = vx[k].get(i);
         float dz = vd[k].get(i);
-        if (a.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
+        if (a.relu && !(fmaf(xv, sc[i], sf[i]) > 0.f)) dz = 0.f;
         s0[i] += dz;
         s1[i] += dz * ((xv - mu[i]) * is[i]);
       }
@@ -1393,8 +1393,8 @@ __global__ __launch_bounds__(ONEPASS_T) void bn_bwd_onepass_kernel(BnBwdFusedArg
       for (int i = 0; i < 8; ++i) {
         const float xv = vx[k].get(i);
         float dz = vd[k].get(i);
-        if (a.relu && !(xv * sc[i] + sf[i] > 0.f)) dz = 0.f;
-        vo.set(i, k1[i] * dz + k2[i] * (xv - mu[i]) + k3[i]);
+        if (a.relu && !(fmaf(xv, sc[i], sf[i]) > 0.f)) dz = 0.f;
+        vo.set(i, fmaf(k1[i], dz, k2[i] * (xv - mu[i])) + k3[i]);
       }
       vo.store(dxc + p * dxs);
     }

@@ -919,9 +919,10 @@ int launch(const VuGemmFwd& p, int ks, hipStream_t st) {
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64, false, BN != 64>),
                          dim3((unsigned)grid), dim3(512), 0, st, q);
     }
-    else if (BN != 64 && g_pp_full)  // (BN = 64 spills with the extra fragments)
+    else if (BN != 64 && g_pp_full)  // (BN = 64 FULL spills 11 VGPRs: up4.1 fwd 341 -> 389 us, profiles/r6z_ab_pp64_full.txt)
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false, false, BN != 64>), dim3((unsigned)tiles), dim3(512), 0,
                          st, q);
+
     else
       hipLaunchKernelGGL((conv3x3_pp_kernel<BN, false, false>), dim3((unsigned)tiles), dim3(512), 0, st, q);
     return (int)hipGetLastError();

@@ -236,6 +236,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int njobs, int N) {
   __shared__ __attribute__((aligned(16))) float sh[ZB_NS * 2048];
   const VuZbJob& J = jobs.j[find_job(jobs, njobs)];
+  if (J.rs_ready) return;   // partials already written by vu_bn_bwd_apply_zrs (block-uniform)
   const int H = J.H, W = J.W, C = J.co;
   const int HW = H * W, pch = pix_chunk(C), nch = (HW + pch - 1) / pch;
   const int lb = (int)((int64_t)blockIdx.x - J.block0);
@@ -293,6 +294,95 @@ __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int nj
     float t = 0.f;
     for (int r = 0; r < slots; ++r) t += sh[(k * slots + r) * C + c];
     J.rs[(((int64_t)n * nch + chunk) * ZB_NS + k) * C + c] = t;
+  }
+}
+
+// ---- backward 1, fused (round 6): the BatchNorm(+ReLU) backward apply of
+// conv1's BatchNorm -- the pass that WRITES dy -- taking the region partials
+// of the values it stores.  Same blocks (sample, pixel chunk), the same lane
+// -> (pixel, 8 channels) map and summation order as zbias_rs_kernel, and the
+// per-element arithmetic of vu_bn_bwd_apply (bn.hip bn_bwd_apply_kernel):
+// dy and rs come out bit-identical to the two separate passes, without the
+// re-read of dy.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_zrs_kernel(const T* dz_in, int64_t dzs, const T* x, int64_t xs,
+                                                               int H, int W, int C, const float* scale,
+                                                               const float* shift, const float* mean,
+                                                               const float* coef, int relu, T* dy, int64_t dys,
+                                                               float* rs) {
+  __shared__ __attribute__((aligned(16))) float sh[ZB_NS * 2048];
+  const int HW = H * W, pch = pix_chunk(C), nch = (HW + pch - 1) / pch;
+  const int n = (int)blockIdx.x / nch, chunk = (int)blockIdx.x - n * nch;
+  const int V = C >> 3, slots = 256 / V;
+  const int tid = threadIdx.x, cv = tid % V, slot = tid / V;
+  const int p0 = chunk * pch, p1 = min(HW, p0 + pch);
+  constexpr int U = 8;
+  float s[ZB_NS][8];
+#pragma unroll
+  for (int k = 0; k < ZB_NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[k][e] = 0.f;
+  if (slot < slots) {
+    const int c = cv * 8;
+    float sc[8], sf[8], mu[8], k1[8], k2[8], k3[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = scale[c + i]; sf[i] = shift[c + i]; mu[i] = mean[c + i];
+      k1[i] = coef[c + i]; k2[i] = coef[C + c + i]; k3[i] = coef[2 * C + c + i];
+    }
+    const int64_t nb = (int64_t)n * HW;
+    const FastDiv dw((uint32_t)W);
+    for (int p = p0 + slot; p < p1; p += U * slots) {
+      Vec8<T> vd[U], vx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // clamped loads, used only when inside
+        const int q = p + u * slots;
+        const int64_t qc = nb + (q < p1 ? q : p1 - 1);
+        vd[u].load(dz_in + qc * dzs + c);
+        vx[u].load(x + qc * xs + c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = p + u * slots;
+        if (q >= p1) break;
+        Vec8<T> vo;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float xv = vx[u].get(i), d = vd[u].get(i);
+          if (relu && !(fmaf(xv, sc[i], sf[i]) > 0.f)) d = 0.f;
+          vo.set(i, fmaf(k1[i], d, k2[i] * (xv - mu[i])) + k3[i]);
+        }
+        vo.store(dy + (nb + q) * dys + c);
+        const int y = (int)dw.div((uint32_t)q), xq = q - y * W;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[0][e] += vo.get(e);
+        if (xq == 0 || xq == W - 1 || y == 0 || y == H - 1) {
+          const float m1 = xq == 0 ? 1.f : 0.f, m2 = xq == W - 1 ? 1.f : 0.f;
+          const float m3 = y == 0 ? 1.f : 0.f, m4 = y == H - 1 ? 1.f : 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = vo.get(e);
+            s[1][e] = fmaf(m1, d, s[1][e]);
+            s[2][e] = fmaf(m2, d, s[2][e]);
+            s[3][e] = fmaf(m3, d, s[3][e]);
+            s[4][e] = fmaf(m4, d, s[4][e]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < ZB_NS; ++k) {
+      f32x4* d = reinterpret_cast<f32x4*>(sh + (k * slots + slot) * C + cv * 8);
+      d[0] = f32x4{s[k][0], s[k][1], s[k][2], s[k][3]};
+      d[1] = f32x4{s[k][4], s[k][5], s[k][6], s[k][7]};
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < ZB_NS * C; q += 256) {
+    const int k = q / C, c = q - (q / C) * C;
+    float t = 0.f;
+    for (int r = 0; r < slots; ++r) t += sh[(k * slots + r) * C + c];
+    rs[(((int64_t)n * nch + chunk) * ZB_NS + k) * C + c] = t;
   }
 }
 
@@ -468,6 +558,23 @@ extern "C" int vu_zbias_fwd(const VuZbJob* jobs, int njobs, int N, void* stream)
   return (int)hipGetLastError();
 }
 
+extern "C" int vu_bn_bwd_apply_zrs_ok(int H, int W, int C, int64_t dzs, int64_t xs, int64_t dys) {
+  return H >= 2 && W >= 2 && C >= 8 && C % 8 == 0 && C / 8 <= 256 && dzs % 8 == 0 && xs % 8 == 0 &&
+         dys % 8 == 0 && (int64_t)H * W <= (1 << 30) / C;
+}
+
+extern "C" int vu_bn_bwd_apply_zrs(const void* dz, int64_t dzs, const void* x, int64_t xs, int N, int H, int W, int C,
+                                   const float* scale, const float* shift, const float* mean, const float* coef,
+                                   int relu, void* dy, int64_t dys, float* rs, int dtype, void* stream) {
+  if (!vu_bn_bwd_apply_zrs_ok(H, W, C, dzs, xs, dys) || N < 1 || !rs) return (int)hipErrorInvalidValue;
+  const int64_t blocks = (int64_t)N * n_chunks(C, H, W);
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((bn_bwd_apply_zrs_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const T*)dz, dzs, (const T*)x, xs, H, W, C, scale, shift, mean, coef, relu, (T*)dy, dys, rs);
+  })
+  return (int)hipGetLastError();
+}
+
 extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, void* stream) {
   ZbJobs J;
   if (int rc = pack(jobs, njobs, J)) return rc;
@@ -484,9 +591,12 @@ extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, vo
     maxL = q.L > maxL ? q.L : maxL;
   }
   hipStream_t st = (hipStream_t)stream;
-  DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((zbias_rs_kernel<T>), dim3((unsigned)rblocks), dim3(256), 0, st, J, njobs, N);
-  })
+  bool all_ready = true;
+  for (int j = 0; j < njobs; ++j) all_ready = all_ready && J.j[j].rs_ready;
+  if (!all_ready)
+    DISPATCH_T(dtype, {
+      hipLaunchKernelGGL((zbias_rs_kernel<T>), dim3((unsigned)rblocks), dim3(256), 0, st, J, njobs, N);
+    })
   int64_t sblocks = 0;
   for (int j = 0; j < njobs; ++j) {
     J.j[j].block0 = sblocks;

@@ -473,12 +473,13 @@ class PoolGrad:
 POOL_BN_BWD = False
 
 
-def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None):
+def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None, zrs=None):
     """BatchNorm2d(+ReLU) backward.  Train mode differentiates through the
     batch statistics; eval mode (running statistics, constants) gives
     dx = gamma*invstd*dz and the same dgamma/dbeta sums.  part: the first
     reduction stage, already emitted by the GEMM that produced dy.  dy may be
-    a PoolGrad (the activation fed a 2x2 max-pool)."""
+    a PoolGrad (the activation fed a 2x2 max-pool).  zrs: a latent shortcut's
+    K.ZbiasRegions, filled by the apply pass when it serves."""
     gw, gb, acc = bn_grad_sinks(bn)
     if dx is None:
         dx = torch.empty_like(x)
@@ -493,10 +494,10 @@ def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None):
         dy = dy.materialize(M)
     if part is not None and part.x is x:
         K.bn_backward_part(part, dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
-                           train=bn.training)
+                           train=bn.training, zrs=zrs)
     else:
         K.bn_backward(dy, x, coef, bn.weight, relu, gw, gb, acc, dx, K.dcode(x.dtype),
-                      train=bn.training, fused=FUSED_BN_BWD)
+                      train=bn.training, fused=FUSED_BN_BWD, zrs=zrs)
     return dx
 
 
@@ -573,7 +574,8 @@ def conv_bn_relu_bwd(M, srcs, conv, bn, saved, da, need_dsrc, cvalid=None, dsrc=
     GEMM's epilogue, returned as (dsrc, part) -- part None when the kernel
     cannot."""
     y, coef = saved
-    dy = bn_bwd(da, y, coef, bn, True, M, part=da_part)
+    zrs = shortcut.regions(y) if shortcut is not None else None
+    dy = bn_bwd(da, y, coef, bn, True, M, part=da_part, zrs=zrs)
     if shortcut is not None:
         shortcut.dy = dy
 

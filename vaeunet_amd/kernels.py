@@ -92,8 +92,15 @@ class LaunchTimer:
     roofline leg).  Events are recorded on the current stream — the stream
     the kernels are launched on — so they bracket exactly one launch."""
 
-    def __init__(self):
+    def __init__(self, detail=False):
         self.recs = []
+        self.detail = detail   # keep each launch's problem shape (tools: per-layer tables)
+        self.shapes = []
+
+    def per_launch(self):
+        """[(tag, shape, kernel, ms, flops)] in launch order (detail=True)."""
+        torch.cuda.synchronize()
+        return [(r[0], sh, r[4], r[2].elapsed_time(r[3]), r[1]) for r, sh in zip(self.recs, self.shapes)]
 
     def summary(self):
         """tag -> [flops, ms, launches, {kernel names}]"""
@@ -129,7 +136,7 @@ FWD_KERNELS = {1: "gemm_fwd_kernel", 2: "gemm_fwd_v2_kernel", 3: "conv3x3_halo_k
 WGRAD_KERNELS = {1: "gemm_wgrad_kernel", 2: "gemm_wgrad_v2_kernel", 3: "wgrad3x3_halo_kernel"}
 
 
-def _timed(tag, flops, fn, kname=None):
+def _timed(tag, flops, fn, kname=None, shape=None):
     if TIMER is None:
         return fn()
     s = torch.cuda.Event(enable_timing=True)
@@ -138,6 +145,8 @@ def _timed(tag, flops, fn, kname=None):
     r = fn()
     e.record()
     TIMER.recs.append((tag, flops, s, e, kname() if callable(kname) else kname))
+    if TIMER.detail:
+        TIMER.shapes.append(shape() if callable(shape) else shape)
     return r
 
 
@@ -248,7 +257,9 @@ def gemm_fwd(g, wmat, ncol, out, dtype, out_coff=0, bias=None, stats=False, accu
         def kname():
             k = FWD_KERNELS.get(query("vu_gemm_fwd_kernel", C.byref(a), dtype), "?")
             return k + "+splitk_finish_kernel" if ws is not None else k
-        _timed(_gemm_tag(g, kind), 2 * M * ncol * g.R * g.S * g.C if flops is None else flops, launch, kname)
+        _timed(_gemm_tag(g, kind), 2 * M * ncol * g.R * g.S * g.C if flops is None else flops, launch, kname,
+               lambda: f"{g.N}x{g.H}x{g.W} C{g.C}->{ncol}" + (" stats" if st is not None else "")
+               + (" bnb" if bnb is not None else ""))
     if bnb is not None:
         return part
     return st
@@ -336,7 +347,8 @@ def gemm_wgrad(gp, gq, ni, nj, grad, layout, dtype, accumulate, cvalid=None):
         AUDIT.gemm_wgrad(w, dtype, kind, gp, gq, ni, nj, grad, layout, accumulate, cv, launch)
         return slab
     _timed(_gemm_tag(gq, "wgrad"), 2 * M * ni * nj,
-           lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()), WGRAD_KERNELS.get(kind, "?"))
+           lambda: call("vu_gemm_wgrad", C.byref(w), dtype, stream()), WGRAD_KERNELS.get(kind, "?"),
+           lambda: f"{gq.N}x{gq.H}x{gq.W} {ni}x{nj} splits {splits}")
     reduce()
     return slab
 
@@ -510,15 +522,43 @@ def bn_apply(x, y, coef, relu, dtype):
     return y
 
 
-def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True, fused=True):
+class ZbiasRegions:
+    """A latent-shortcut conv1's region-partial buffer (vu_zbias_rs_floats
+    floats); ``ready`` once the BatchNorm backward apply that wrote conv1's dy
+    also wrote the partials (vu_bn_bwd_apply_zrs)."""
+
+    def __init__(self, rs):
+        self.rs, self.ready = rs, False
+
+
+def _apply(dy, x, coef, k, relu, dx, dtype, zrs):
+    """The BN backward apply pass; with zrs (a ZbiasRegions) the fused variant
+    that also takes the shortcut's region partials of dx, when it serves."""
+    N, Cc, H, W = x.shape
+    if zrs is not None and query("vu_bn_bwd_apply_zrs_ok", H, W, Cc, pstride(dy), pstride(x), pstride(dx)):
+        call("vu_bn_bwd_apply_zrs", ptr(dy), pstride(dy), ptr(x), pstride(x), N, H, W, Cc, ptr(coef[0]),
+             ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), ptr(zrs.rs), dtype,
+             stream())
+        zrs.ready = True
+        return
+    call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), N * H * W, Cc, ptr(coef[0]),
+         ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
+         stream())
+
+
+def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True, fused=True, zrs=None):
     """dx = BN(+ReLU) backward; writes/accumulates dgamma, dbeta.  train=False:
     the statistics are constants (eval mode).  fused: small tensors take the
-    two-launch path (vu_bn_bwd_fused) instead of reduce + finish + apply."""
+    two-launch path (vu_bn_bwd_fused) instead of reduce + finish + apply.
+    zrs: a ZbiasRegions to fill from the apply pass (the reduce + apply path
+    only)."""
     N, Cc, H, W = x.shape
     P = N * H * W
     dev = x.device
     ws = torch.empty(query("vu_reduce_workspace_bytes", P, Cc) // 4 + 1, dtype=torch.float32,
                      device=dev)
+    # (the small-tensor two-launch path keeps its own, more accurate fp64
+    # reduction: a zrs is then left unfilled and the region pass runs)
     if fused and query("vu_bn_bwd_fused_supported", P, Cc, pstride(dy), pstride(x), pstride(dx)):
         call("vu_bn_bwd_fused", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]), ptr(coef[1]),
              ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0, 1 if train else 0, ptr(dgamma), ptr(dbeta),
@@ -529,9 +569,7 @@ def bn_backward(dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=T
          ptr(coef[1]), ptr(coef[2]), ptr(coef[3]), ptr(gamma), 1 if relu else 0,
          1 if train else 0, ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), dtype,
          stream())
-    call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
-         ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
-         stream())
+    _apply(dy, x, coef, k, relu, dx, dtype, zrs)
     return dx
 
 
@@ -550,9 +588,10 @@ def bn_backward_pool(dp, add, y, coef, gamma, relu, dgamma, dbeta, acc, dx, dtyp
     return dx
 
 
-def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True):
+def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dtype, train=True, zrs=None):
     """bn_backward with the first reduction stage done by the producing GEMM's
-    epilogue (a BnbPart): the fp64 finish, then the apply pass."""
+    epilogue (a BnbPart): the fp64 finish, then the apply pass (zrs: as
+    bn_backward)."""
     N, Cc, H, W = x.shape
     P = N * H * W
     k = torch.empty((3, Cc), dtype=torch.float32, device=x.device)
@@ -560,9 +599,7 @@ def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dty
     ws = workspace_f32(nb, x.device) if nb > 0 else None
     call("vu_bn_bwd_finish", ptr(part.part), part.nblk, P, Cc, ptr(gamma), ptr(coef[3]), 1 if train else 0,
          ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), stream())
-    call("vu_bn_bwd_apply", ptr(dy), pstride(dy), ptr(x), pstride(x), P, Cc, ptr(coef[0]),
-         ptr(coef[1]), ptr(coef[2]), ptr(k), 1 if relu else 0, ptr(dx), pstride(dx), dtype,
-         stream())
+    _apply(dy, x, coef, k, relu, dx, dtype, zrs)
     return dx
 
 

@@ -557,6 +557,10 @@ def latent_consumers(M, model, feats, N, skip_always=False):
 # over [x, skip] only; the z part is a per-sample, per-border-class bias of
 # its GEMM epilogue, its backward per-sample region sums of conv1's dy.
 LATENT_SHORTCUT = True   # A/B switch: False = the round-4 map (64-channel padded z_proj source)
+# Round 6: conv1's BatchNorm backward apply -- the pass
+# that writes dy -- also writes the shortcut's region partials
+# (vu_bn_bwd_apply_zrs), so vu_zbias_bwd skips its re-read of dy.  A/B switch.
+FUSE_ZBIAS_REGIONS = True
 
 
 def shortcut_ok(M, blk, N, size):
@@ -582,6 +586,17 @@ class ZShortcut:
         self.row_scale = None    # eval-mode BN folded into conv1 (inference)
         self.dy = None           # backward: conv1's pre-BN gradient (engine.conv_bn_relu_bwd)
         self.sink = None         # backward: (conv1.weight.grad, accumulate)
+        self.zrs = None          # backward: K.ZbiasRegions (region partials from the BN apply pass)
+
+    def regions(self, y):
+        """The region-partial buffer conv1's BatchNorm backward apply fills
+        (FUSE_ZBIAS_REGIONS; None = the separate region pass)."""
+        self.zrs = None
+        if FUSE_ZBIAS_REGIONS:
+            N, co = y.shape[0], self.blk.conv1[0].out_channels
+            self.zrs = K.ZbiasRegions(torch.empty(K.query("vu_zbias_rs_floats", N, co, self.H, self.W),
+                                                  dtype=torch.float32, device=y.device))
+        return self.zrs
 
     def job(self):
         conv1 = self.blk.conv1[0]
@@ -629,12 +644,15 @@ def zbias_backward(M, zscs, parts):
             tmp = torch.empty_like(conv1.weight)
             fix.append((g, acc, tmp, z.lead, z.lead + z.cons.conv.out_channels))
             g, acc = tmp, False
-        rs = torch.empty(K.query("vu_zbias_rs_floats", N, conv1.out_channels, z.H, z.W), dtype=torch.float32,
-                         device=z.table.device)
+        # the region pass skips a job whose BatchNorm apply pass wrote its partials
+        ready = z.zrs is not None and z.zrs.ready
+        rs = z.zrs.rs if ready else torch.empty(K.query("vu_zbias_rs_floats", N, conv1.out_channels, z.H, z.W),
+                                                dtype=torch.float32, device=z.table.device)
         keep.append(rs)
         arr[i].dy, arr[i].dy_stride = z.dy.data_ptr(), K.pstride(z.dy)
         arr[i].rs, arr[i].part = rs.data_ptr(), parts[i].data_ptr()
         arr[i].dw, arr[i].grad_acc = K.ptr(g), 1 if acc else 0
+        arr[i].rs_ready = 1 if ready else 0
     K.call("vu_zbias_bwd", arr, len(zscs), N, K.dcode(zscs[0].dy.dtype), K.stream())
     for g, acc, tmp, a, b in fix:
         if acc:
@@ -646,6 +664,7 @@ def zbias_backward(M, zscs, parts):
     for z in zscs:
         z.dy = None
         z.sink = None
+        z.zrs = None
     return keep
 
 
