@@ -593,10 +593,11 @@ extern "C" int vu_zbias_bwd(const VuZbJob* jobs, int njobs, int N, int dtype, vo
   hipStream_t st = (hipStream_t)stream;
   bool all_ready = true;
   for (int j = 0; j < njobs; ++j) all_ready = all_ready && J.j[j].rs_ready;
-  if (!all_ready)
+  if (!all_ready) {
     DISPATCH_T(dtype, {
       hipLaunchKernelGGL((zbias_rs_kernel<T>), dim3((unsigned)rblocks), dim3(256), 0, st, J, njobs, N);
     })
+  }
   int64_t sblocks = 0;
   for (int j = 0; j < njobs; ++j) {
     J.j[j].block0 = sblocks;
