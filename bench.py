@@ -51,7 +51,12 @@ def pmc_traffic(model):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    # 300 timed steps (~4.5 s of graph replay for the UNet, ~2.5 s for the
+    # VAE child): long enough for an external GPU-busy sampler polling every
+    # few seconds to see the card busy (50 steps were
+    # 0.75 s of a ~150 s run), short enough for the default run to stay
+    # within minutes
+    ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=512)
