@@ -64,6 +64,11 @@ def parse():
     ap.add_argument("--model", choices=("unet", "vae"), default="unet",
                     help="unet = BASELINE configs[1] (the metric); vae = configs[2], UNetResNet + KL")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # 20 rounds ~ 68 us: covers the host enqueue of start event + launch + end
+    # event (same box: the 3x3 family read 0.442-0.445 without it, 0.453-0.454
+    # with it -- host time had leaked into the brackets; profiles/r6td_timer_delay.txt)
+    ap.add_argument("--timer-delay", type=int, default=20,
+                    help="roofline leg: GPU sleep rounds (~3.4 us each) queued before every timed launch")
     ap.add_argument("--layer-table", action="store_true",
                     help="print the roofline leg's per-launch GEMM table (shape, kernel, time) to stderr")
     ap.add_argument("--no-roofline", action="store_true")
@@ -524,7 +529,7 @@ def main():
     if not args.no_roofline:
         # live per-launch HIP-event timing of the 3x3 implicit-GEMM kernels over
         # 2 further steps (events on the launch stream, one pair per launch)
-        K.TIMER = K.LaunchTimer(detail=args.layer_table)
+        K.TIMER = K.LaunchTimer(detail=args.layer_table, delay=args.timer_delay)
         for _ in range(2):
             eager_step()   # the same kernels, launched one by one so each can be bracketed
         if args.layer_table and rank == 0:

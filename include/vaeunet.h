@@ -461,6 +461,10 @@ int64_t vu_reduce_workspace_bytes(int64_t P, int C);
 int64_t vu_bn_finalize_workspace_bytes(int tiles, int C);
 /* y[p][0..C) = 0 for P pixels at pixel stride ys (channel-slice zero fill) */
 int vu_zero(void* y, int64_t ys, int64_t P, int C, int dtype, void* stream);
+/* one wave sleeping ~rounds x 3.4 us on the stream (0 <= rounds <= 1000):
+ * bench.py's per-launch timing puts it in front of each timed launch so the
+ * event pair brackets GPU time only (no memory access) */
+int vu_gpu_delay(int rounds, void* stream);
 /* zero insertion for a stride-2 conv's input gradient: up (N,H,W,C) holds
  * dy (N,h,w,C) at the even pixels, zeros elsewhere (C, strides % 8 == 0) */
 int vu_zero_insert2(const void* dy, int64_t dys, int N, int h, int w, int C,

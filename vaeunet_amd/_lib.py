@@ -141,6 +141,7 @@ _SIGS = {
     "vu_chan_sum": (_i, [_p, _l, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
     "vu_copy": (_i, [_p, _l, _i, _p, _l, _i, _l, _i, _i, _p]),
     "vu_zero": (_i, [_p, _l, _l, _i, _i, _p]),
+    "vu_gpu_delay": (_i, [_i, _p]),
     "vu_zero_insert2": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _i, _i, _p]),
     "vu_input_pack": (_i, [_p, _l, _l, _l, _l, _i, _i, _i, _i, _i, _p, _i, _p]),
     "vu_maxpool2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _i, _p]),

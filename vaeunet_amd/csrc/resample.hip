@@ -703,6 +703,23 @@ __global__ void zero_kernel(char* y, int64_t ys_bytes, int64_t P, int row_bytes)
 
 // y[p][0..C) = 0 for P pixels at pixel stride ys (a channel slice of an NHWC
 // tensor: the zero channels a 64-aligned concat source is padded with)
+// one wave sleeping ~rounds x 3.4 us (s_sleep 127 = 127 x 64 clocks): put
+// in front of a timed launch (bench.py's roofline leg), it keeps the queue
+// busy while the host enqueues the start event, the launch and the end
+// event, so the event pair brackets the kernel and not the host's enqueue
+// time.  No memory access.
+namespace {
+__global__ void delay_kernel(int rounds) {
+  for (int i = 0; i < rounds; ++i) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
+
+extern "C" int vu_gpu_delay(int rounds, void* stream) {
+  if (rounds < 0 || rounds > 1000) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, rounds);
+  return (int)hipGetLastError();
+}
+
 extern "C" int vu_zero(void* y, int64_t ys, int64_t P, int C, int dtype, void* stream) {
   const int eb = dtype == VU_BF16 ? 2 : 4;
   if ((C * eb) % 4 != 0) return (int)hipErrorInvalidValue;

@@ -92,8 +92,12 @@ class LaunchTimer:
     roofline leg).  Events are recorded on the current stream — the stream
     the kernels are launched on — so they bracket exactly one launch."""
 
-    def __init__(self, detail=False):
+    def __init__(self, detail=False, delay=0):
         self.recs = []
+        # delay > 0: a GPU sleep of ~delay x 3.4 us before each bracketed
+        # launch (vu_gpu_delay), so host enqueue time between the start event
+        # and the launch is not counted
+        self.delay = delay
         self.detail = detail   # keep each launch's problem shape (tools: per-layer tables)
         self.shapes = []
 
@@ -141,6 +145,8 @@ def _timed(tag, flops, fn, kname=None, shape=None):
         return fn()
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
+    if TIMER.delay:
+        call("vu_gpu_delay", TIMER.delay, stream())
     s.record()
     r = fn()
     e.record()
