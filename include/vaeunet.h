@@ -656,6 +656,14 @@ int vu_mt_adamw(const VuMtEntry* table, int ntensors, int64_t nchunks,
 int vu_mt_adamw_dev(const VuMtEntry* table, int ntensors, int64_t nchunks,
                     double lr, double weight_decay, double beta1, double beta2,
                     double eps, float* step, int zero_grad, void* stream);
+/* the same, each gradient multiplied by *grad_scale (the clip coefficient of
+ * vu_mt_grad_norm) as it is read -- the bits of vu_mt_scale_grads followed by
+ * vu_mt_adamw_dev, one pass over the gradients fewer; only with zero_grad
+ * (the scaled gradient is never stored).  grad_scale NULL = 1. */
+int vu_mt_adamw_dev_scaled(const VuMtEntry* table, int ntensors, int64_t nchunks,
+                           double lr, double weight_decay, double beta1, double beta2,
+                           double eps, float* step, int zero_grad, const float* grad_scale,
+                           void* stream);
 
 /* ---- VAE-U-Net (unet/unet_resnet.py) ----------------------------------- */
 /* ResNet34 stem max-pool 3x3/s2/p1 (timm resnet34, unet_resnet.py:131):

@@ -175,6 +175,8 @@ _SIGS = {
     "vu_mt_adamw": (_i, [_p, _i, _l, _f, _f, _f, _f, _f, _p, _p]),
     "vu_mt_adamw_dev": (_i, [_p, _i, _l, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, _p, _i,
                              _p]),
+    "vu_mt_adamw_dev_scaled": (_i, [_p, _i, _l, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double, _p,
+                                    _i, _p, _p]),
     "vu_maxpool3s2_fwd": (_i, [_p, _l, _i, _i, _i, _i, _p, _l, _p, _i, _p]),
     "vu_maxpool3s2_bwd": (_i, [_p, _l, _p, _i, _i, _i, _i, _p, _l, _i, _i, _p]),
     "vu_bn_add_relu": (_i, [_p, _l, _p, _p, _p, _l, _p, _p, _l, _i, _p, _l, _i, _p]),

@@ -147,7 +147,7 @@ __global__ void mt_step_incr_kernel(float* step) { *step += 1.f; }
 
 __global__ void mt_adamw_dev_kernel(const VuMtEntry* t, int n, float decay, float w1, float beta2, float w2,
                                     float eps, double lr, double beta1d, double beta2d, const float* step,
-                                    int zero_grad) {
+                                    int zero_grad, const float* gscale) {
   const int64_t chunk = blockIdx.x;
   const int k = find_tensor(t, n, chunk);
   const int64_t off = (chunk - t[k].chunk0) * MT_CHUNK;
@@ -159,7 +159,11 @@ __global__ void mt_adamw_dev_kernel(const VuMtEntry* t, int n, float decay, floa
   const double sc = (double)*step;
   const float step_size = (float)(lr / (1.0 - pow(beta1d, sc)));
   const float bc2s = (float)sqrt(1.0 - pow(beta2d, sc));
+  // gscale (the clip coefficient): g * c rounded once, as vu_mt_scale_grads
+  // stores it -- the same bits as scaling first
+  const float gc = gscale ? *gscale : 1.f;
   auto upd = [&](float gi, float& pi, float& mi, float& vi) {
+    if (gscale) gi = gi * gc;
     adamw_elem(gi, pi, mi, vi, decay, w1, beta2, w2, eps, step_size, bc2s);
   };
   // 16-byte accesses (4 elements per thread and iteration, the four streams'
@@ -201,16 +205,24 @@ __global__ void mt_adamw_dev_kernel(const VuMtEntry* t, int n, float decay, floa
 
 }  // namespace
 
-extern "C" int vu_mt_adamw_dev(const VuMtEntry* table, int ntensors, int64_t nchunks, double lr,
-                               double weight_decay, double beta1, double beta2, double eps, float* step,
-                               int zero_grad, void* stream) {
+extern "C" int vu_mt_adamw_dev_scaled(const VuMtEntry* table, int ntensors, int64_t nchunks, double lr,
+                                      double weight_decay, double beta1, double beta2, double eps, float* step,
+                                      int zero_grad, const float* grad_scale, void* stream) {
   if (ntensors <= 0 || nchunks <= 0) return 0;
+  if (grad_scale && !zero_grad) return (int)hipErrorInvalidValue;  // the scaled gradient is never stored
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(mt_step_incr_kernel, dim3(1), dim3(1), 0, st, step);
   hipLaunchKernelGGL(mt_adamw_dev_kernel, dim3((unsigned)nchunks), dim3(MT_THREADS), 0, st, table, ntensors,
                      (float)(1.0 - lr * weight_decay), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2),
-                     (float)eps, lr, beta1, beta2, step, zero_grad);
+                     (float)eps, lr, beta1, beta2, step, zero_grad, grad_scale);
   return (int)hipGetLastError();
+}
+
+extern "C" int vu_mt_adamw_dev(const VuMtEntry* table, int ntensors, int64_t nchunks, double lr,
+                               double weight_decay, double beta1, double beta2, double eps, float* step,
+                               int zero_grad, void* stream) {
+  return vu_mt_adamw_dev_scaled(table, ntensors, nchunks, lr, weight_decay, beta1, beta2, eps, step, zero_grad,
+                                nullptr, stream);
 }
 
 extern "C" int64_t vu_mt_chunk_elems() { return MT_CHUNK; }

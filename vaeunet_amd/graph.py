@@ -134,15 +134,21 @@ class GraphedTrainStep:
 
     def _tail(self):
         s = _lib.stream()
+        coef = None
         if self.max_norm is not None:
             t = self.clip_tab
             _lib.call("vu_mt_grad_norm", t.ptr(), t.n, t.nchunks, float(self.max_norm), _lib.ptr(self.norm[0:1]),
                       _lib.ptr(self.norm[1:2]), _lib.ptr(self.ws), s)
-            _lib.call("vu_mt_scale_grads", t.ptr(), t.n, t.nchunks, _lib.ptr(self.norm[1:2]), s)
+            # the clip coefficient is applied as AdamW reads each gradient
+            # (the gradients are cleared after use, so nothing else sees them
+            # scaled): the same bits as clip_grad_norm_'s in-place scaling, one
+            # pass over the gradients fewer (round 6)
+            coef = _lib.ptr(self.norm[1:2])
         for group, t, step in self.groups:
             b1, b2 = group["betas"]
-            _lib.call("vu_mt_adamw_dev", t.ptr(), t.n, t.nchunks, float(group["lr"]), float(group["weight_decay"]),
-                      float(b1), float(b2), float(group["eps"]), _lib.ptr(step), 1, s)
+            _lib.call("vu_mt_adamw_dev_scaled", t.ptr(), t.n, t.nchunks, float(group["lr"]),
+                      float(group["weight_decay"]), float(b1), float(b2), float(group["eps"]), _lib.ptr(step), 1,
+                      coef, s)
 
     def step(self):
         """Replay one training step; returns the (static) loss tensor.
