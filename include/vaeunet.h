@@ -542,6 +542,21 @@ int vu_attn_psi_bwd(const void* ug, const void* ux, int64_t P, int F,
                     const float* tx, const float* wpsi, const float* dq,
                     void* ds, float* dwpsi, float* dbpsi, int accumulate,
                     float* workspace, int dtype, void* stream);
+/* the same (batched kernels, VU_TUNE_ATTN 1) also emitting the first stage of
+ * the backward reduction of the two BatchNorms ds flows into (W_g's over ug,
+ * W_x's over ux, unet_parts.py:11-20; no ReLU between): per block b,
+ *   bnb_?[(2b + 0) * F + c] = sum ds,  bnb_?[(2b + 1) * F + c] = sum ds * (u - mean) * invstd
+ * over the stored ds -- VuGemmFwd.bnb_part's layout, finished by
+ * vu_bn_bwd_finish with nblk = vu_attn_psi_bwd_blocks(P). */
+int64_t vu_attn_psi_bwd_blocks(int64_t P);
+int vu_attn_psi_bwd_bnb_ok(int F);   /* 1 when vu_attn_psi_bwd_bnb serves F */
+int vu_attn_psi_bwd_bnb(const void* ug, const void* ux, int64_t P, int F,
+                        const float* sg, const float* tg, const float* sx,
+                        const float* tx, const float* wpsi, const float* dq,
+                        void* ds, float* dwpsi, float* dbpsi, int accumulate,
+                        float* workspace, const float* mean_g, const float* invstd_g,
+                        const float* mean_x, const float* invstd_x, float* bnb_g,
+                        float* bnb_x, int dtype, void* stream);
 
 /* ---- 1x1 conv with a tiny output (OutConv unet_parts.py:97-103,
  *      final_conv unet_resnet.py:189) -------------------------------------- */

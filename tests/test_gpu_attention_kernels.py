@@ -109,3 +109,61 @@ def test_attention_forward_vs_torch(case):
         blk = q[t * tile:(t + 1) * tile].double()
         assert abs(float(o["psum"][t]) - float(blk.sum())) < 1e-3
         assert abs(float(o["pm2"][t]) - float(((blk - blk.mean()) ** 2).sum())) < 1e-3 * (1 + float(o["pm2"][t]))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("case", CASES[:5])
+def test_psi_bwd_emits_both_batchnorm_partials(dt, case):
+    """Round 6: vu_attn_psi_bwd_bnb writes the same ds bits as vu_attn_psi_bwd
+    (dwpsi / dbpsi to fp32 rounding), and its per-block (sum ds, sum ds*xhat) partials for the
+    W_g and W_x BatchNorms, finished by vu_bn_bwd_finish, equal the fp64 sums
+    over the stored ds (what the separate vu_bn_bwd_reduce passes computed)."""
+    K = _k()
+    from vaeunet_amd import _lib
+    P, F, _ = case
+    d = _lib.BF16 if dt == torch.bfloat16 else _lib.F32
+    g = torch.Generator().manual_seed(41)
+    ug = torch.randn(P, F, generator=g).to(dt).to(DEV)
+    ux = torch.randn(P, F, generator=g).to(dt).to(DEV)
+    co = [(torch.rand(F, generator=g) + 0.5).to(DEV), (torch.randn(F, generator=g) * 0.3).to(DEV),
+          (torch.rand(F, generator=g) + 0.5).to(DEV), (torch.randn(F, generator=g) * 0.3).to(DEV)]
+    mg, ig = (torch.randn(F, generator=g) * 0.2).to(DEV), (torch.rand(F, generator=g) + 0.5).to(DEV)
+    mx, ix = (torch.randn(F, generator=g) * 0.2).to(DEV), (torch.rand(F, generator=g) + 0.5).to(DEV)
+    wpsi = (torch.randn(F, generator=g) / F ** 0.5).to(DEV)
+    dq = torch.randn(P, generator=g).to(DEV)
+    assert K.query("vu_attn_psi_bwd_bnb_ok", F)
+    res = {}
+    for fused in (False, True):
+        ds = torch.empty_like(ug)
+        dw, db = torch.zeros(F, device=DEV), torch.zeros(1, device=DEV)
+        ws = K.workspace_f32(K.query("vu_attn_psi_bwd_workspace_bytes", P, F), DEV)
+        args = [K.ptr(ug), K.ptr(ux), P, F, K.ptr(co[0]), K.ptr(co[1]), K.ptr(co[2]), K.ptr(co[3]), K.ptr(wpsi),
+                K.ptr(dq), K.ptr(ds), K.ptr(dw), K.ptr(db), 0, K.ptr(ws)]
+        if fused:
+            nb = K.query("vu_attn_psi_bwd_blocks", P)
+            bg = torch.full((nb, 2, F), float("nan"), device=DEV)
+            bx = torch.full((nb, 2, F), float("nan"), device=DEV)
+            K.call("vu_attn_psi_bwd_bnb", *args, K.ptr(mg), K.ptr(ig), K.ptr(mx), K.ptr(ix), K.ptr(bg), K.ptr(bx),
+                   d, K.stream())
+        else:
+            K.call("vu_attn_psi_bwd", *args, d, K.stream())
+        torch.cuda.synchronize()
+        res[fused] = (ds.clone(), dw.clone(), db.clone())
+    # ds bit-identical; the psi weight / bias gradients equal up to the
+    # compiler's fma contraction in the two instantiations
+    assert torch.equal(res[False][0], res[True][0])
+    for a, b in zip(res[False][1:], res[True][1:]):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6 * float(a.abs().max()))
+    ds = res[True][0].double().cpu()
+    for part, u, m, i in ((bg, ug, mg, ig), (bx, ux, mx, ix)):
+        assert not bool(torch.isnan(part).any())
+        gamma = torch.ones(F, device=DEV)
+        dgamma, dbeta, k = torch.empty(F, device=DEV), torch.empty(F, device=DEV), torch.empty(3, F, device=DEV)
+        wsf = torch.empty(max(1, _lib.query("vu_bn_bwd_finish_workspace_bytes", nb, F) // 4), device=DEV)
+        _lib.call("vu_bn_bwd_finish", K.ptr(part), nb, P, F, K.ptr(gamma), K.ptr(i), 1, K.ptr(dgamma), K.ptr(dbeta),
+                  0, K.ptr(k), K.ptr(wsf), K.stream())
+        xhat = (u.double().cpu() - m.double().cpu()) * i.double().cpu()
+        s0, s1 = ds.sum(0), (ds * xhat).sum(0)
+        torch.testing.assert_close(dbeta.double().cpu(), s0, rtol=0, atol=2e-6 * float(ds.abs().sum(0).max()))
+        torch.testing.assert_close(dgamma.double().cpu(), s1, rtol=0,
+                                   atol=2e-6 * float((ds * xhat).abs().sum(0).max()))

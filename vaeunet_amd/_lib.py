@@ -155,6 +155,10 @@ _SIGS = {
     "vu_attn_gate_fwd": (_i, [_p, _p, _p, _l, _l, _i, _p, _p, _l, _i, _p]),
     "vu_attn_gate_bwd": (_i, [_p, _l, _p, _l, _p, _l, _i, _p, _l, _p, _i, _p]),
     "vu_attn_psi_bwd_workspace_bytes": (_l, [_l, _i]),
+    "vu_attn_psi_bwd_blocks": (_l, [_l]),
+    "vu_attn_psi_bwd_bnb_ok": (_i, [_i]),
+    "vu_attn_psi_bwd_bnb": (_i, [_p, _p, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p,
+                                 _i, _p]),
     "vu_attn_psi_bwd": (_i, [_p, _p, _l, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _i,
                              _p]),
     "vu_pointwise_fwd": (_i, [_p, _l, _l, _i, _i, _p, _p, _p, _l, _i, _p]),

@@ -327,10 +327,21 @@ __global__ __launch_bounds__(256) void gate_bwd_u_kernel(const T* dout, int64_t 
 // (grid-stride over 256-pixel tiles, so at most MAXB partial rows)
 constexpr int MAXB = 1024;
 
-template <typename T, int U>
+// BNB (round 6): the kernel also emits the first stage of the backward
+// reduction of BOTH BatchNorms in front of the sum (W_g's over ug, W_x's over
+// ux; unet_parts.py:11-20), whose output gradient is ds itself (no ReLU
+// between: the ReLU is after the sum): sum dz and sum dz (u - mean) invstd
+// with dz = the stored ds -- vu_bn_bwd_reduce's arithmetic -- as bnb_g / bnb_x
+// [block][2][F] (VuGemmFwd.bnb_part's layout), from the ug, ux and ds values
+// already in registers: the two separate reduction passes over ds, ug and
+// ds, ux are not run.
+template <typename T, int U, bool BNB = false>
 __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux, int64_t P, int F, const float* sg,
                                                         const float* tg, const float* sx, const float* tx,
-                                                        const float* wpsi, const float* dq, T* ds, float* part) {
+                                                        const float* wpsi, const float* dq, T* ds, float* part,
+                                                        const float* mg = nullptr, const float* ig = nullptr,
+                                                        const float* mx = nullptr, const float* ix = nullptr,
+                                                        float* bnb_g = nullptr, float* bnb_x = nullptr) {
   __shared__ float sh[256 * 8];
   __shared__ float sb[256];
   const int lpp = F >> 3, ppw = 64 / lpp;
@@ -343,6 +354,13 @@ __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux
     wsg[k] = sg[c + k]; wtg[k] = tg[c + k]; wsx[k] = sx[c + k]; wtx[k] = tx[c + k]; wp[k] = wpsi[c + k];
     dw[k] = 0.f;
   }
+  float bmg[8], big[8], bmx[8], bix[8], z0[8], zg[8], zx[8];
+  if constexpr (BNB)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bmg[k] = mg[c + k]; big[k] = ig[c + k]; bmx[k] = mx[c + k]; bix[k] = ix[c + k];
+      z0[k] = 0.f; zg[k] = 0.f; zx[k] = 0.f;
+    }
   float db = 0.f;
   const int niter = lpp;  // TILE / (4 * ppw)
   for (int64_t p0 = (int64_t)blockIdx.x * TILE; p0 < P; p0 += (int64_t)gridDim.x * TILE) {
@@ -375,6 +393,14 @@ __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux
           bool on = s > 0.f;
           if (okp[u]) dw[k] += on ? g[u] * s : 0.f;
           o[u].set(k, on ? g[u] * wp[k] : 0.f);
+          if constexpr (BNB) {
+            if (okp[u]) {
+              const float dz = o[u].get(k);  // the stored (rounded) ds
+              z0[k] += dz;
+              zg[k] += dz * ((va[u].get(k) - bmg[k]) * big[k]);
+              zx[k] += dz * ((vb[u].get(k) - bmx[k]) * bix[k]);
+            }
+          }
         }
         vec8_tie(o[u]);
       }
@@ -397,6 +423,27 @@ __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux
     float s = 0.f;
     for (int t = 0; t < 256; ++t) s += sb[t];
     part[(int64_t)blockIdx.x * (F + 1) + F] = s;
+  }
+  if constexpr (BNB) {
+    // threads with equal `sub` hold the same channels: fixed-order sums, as
+    // the dwpsi partials above; sum dz goes to both BatchNorms' rows
+    for (int q = 0; q < 3; ++q) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sh[threadIdx.x * 8 + k] = q == 0 ? z0[k] : (q == 1 ? zg[k] : zx[k]);
+      __syncthreads();
+      for (int cc = threadIdx.x; cc < F; cc += 256) {
+        int sb_ = cc >> 3, k = cc & 7;
+        float v = 0.f;
+        for (int t = sb_; t < 256; t += lpp) v += sh[t * 8 + k];
+        if (q == 0) {
+          bnb_g[((int64_t)blockIdx.x * 2 + 0) * F + cc] = v;
+          bnb_x[((int64_t)blockIdx.x * 2 + 0) * F + cc] = v;
+        } else {
+          (q == 1 ? bnb_g : bnb_x)[((int64_t)blockIdx.x * 2 + 1) * F + cc] = v;
+        }
+      }
+    }
   }
 }
 
@@ -753,6 +800,36 @@ extern "C" int vu_attn_gate_bwd(const void* dout, int64_t dos, const void* x, in
       hipLaunchKernelGGL((gate_bwd_kernel<T>), dim3(ew_grid(P * 8)), dim3(256), 0, st, (const T*)dout, dos,
                          (const T*)x, xs, pmap, P, C, (T*)dx, dxs, dqpre);
   })
+  return (int)hipGetLastError();
+}
+
+extern "C" int64_t vu_attn_psi_bwd_blocks(int64_t P) {
+  const int64_t nb = (P + TILE - 1) / TILE;
+  return nb < MAXB ? nb : MAXB;
+}
+
+extern "C" int vu_attn_psi_bwd_bnb_ok(int F) {
+  return F % 8 == 0 && pow2(F / 8) && F / 8 <= 64 && F <= 2048 && g_attn ? 1 : 0;
+}
+
+extern "C" int vu_attn_psi_bwd_bnb(const void* ug, const void* ux, int64_t P, int F, const float* sg, const float* tg,
+                                   const float* sx, const float* tx, const float* wpsi, const float* dq, void* ds,
+                                   float* dwpsi, float* dbpsi, int accumulate, float* workspace,
+                                   const float* mean_g, const float* invstd_g, const float* mean_x,
+                                   const float* invstd_x, float* bnb_g, float* bnb_x, int dtype, void* stream) {
+  if (F % 8 != 0 || !pow2(F / 8) || F / 8 > 64 || F > 2048 || !g_attn || !mean_g || !invstd_g || !mean_x ||
+      !invstd_x || !bnb_g || !bnb_x)
+    return (int)hipErrorInvalidValue;
+  const int nblk = (int)vu_attn_psi_bwd_blocks(P);
+  if (nblk == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_T(dtype, {
+    hipLaunchKernelGGL((psi_bwd_u_kernel<T, 4, true>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P,
+                       F, sg, tg, sx, tx, wpsi, dq, (T*)ds, workspace, mean_g, invstd_g, mean_x, invstd_x, bnb_g,
+                       bnb_x);
+  })
+  hipLaunchKernelGGL(part_final, dim3((F + 1 + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, F + 1, dwpsi,
+                     F, dbpsi, accumulate);
   return (int)hipGetLastError();
 }
 

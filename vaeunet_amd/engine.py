@@ -659,6 +659,11 @@ def down_bwd(M, mod, saved, dout, add=None):
 # ----------------------------------------------------------------------------
 # AttentionGate (unet_parts.py:7-30): x * sigmoid(BN(psi(relu(BN(W_g g) + BN(W_x x)))))
 # ----------------------------------------------------------------------------
+# Round 6: the attention psi backward emits the first backward-reduction
+# stage of the W_g and W_x BatchNorms (vu_attn_psi_bwd_bnb).  A/B switch.
+FUSE_ATTN_BN_REDUCE = True
+
+
 def attention_fwd(M, att, g, x):
     N, _, H, W = x.shape
     P = N * H * W
@@ -721,11 +726,24 @@ def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
     gwp, accp = grad_sink(wp.weight)
     gbp, _ = grad_sink(wp.bias)
     ws = K.workspace_f32(K.query("vu_attn_psi_bwd_workspace_bytes", P, F), x.device)
-    K.call("vu_attn_psi_bwd", K.ptr(ug), K.ptr(ux), P, F, K.ptr(cg[0]), K.ptr(cg[1]),
-           K.ptr(cx[0]), K.ptr(cx[1]), K.ptr(wp.weight), K.ptr(dq), K.ptr(ds), K.ptr(gwp),
-           K.ptr(gbp), 1 if accp else 0, K.ptr(ws), M.d, K.stream())
-    dug = bn_bwd(ds, ug, cg, bng, False, M)
-    dux = bn_bwd(ds, ux, cx, bnx, False, M)
+    pg = px = None
+    if FUSE_ATTN_BN_REDUCE and K.query("vu_attn_psi_bwd_bnb_ok", F):
+        # the psi backward also emits both BatchNorms' first reduction stage
+        # (round 6): no separate reduction passes over (ds, ug) and (ds, ux)
+        nb = K.query("vu_attn_psi_bwd_blocks", P)
+        bg = torch.empty((nb, 2, F), dtype=torch.float32, device=x.device)
+        bx = torch.empty_like(bg)
+        K.call("vu_attn_psi_bwd_bnb", K.ptr(ug), K.ptr(ux), P, F, K.ptr(cg[0]), K.ptr(cg[1]),
+               K.ptr(cx[0]), K.ptr(cx[1]), K.ptr(wp.weight), K.ptr(dq), K.ptr(ds), K.ptr(gwp),
+               K.ptr(gbp), 1 if accp else 0, K.ptr(ws), K.ptr(cg[2]), K.ptr(cg[3]), K.ptr(cx[2]),
+               K.ptr(cx[3]), K.ptr(bg), K.ptr(bx), M.d, K.stream())
+        pg, px = K.BnbPart(bg, nb, ug), K.BnbPart(bx, nb, ux)
+    else:
+        K.call("vu_attn_psi_bwd", K.ptr(ug), K.ptr(ux), P, F, K.ptr(cg[0]), K.ptr(cg[1]),
+               K.ptr(cx[0]), K.ptr(cx[1]), K.ptr(wp.weight), K.ptr(dq), K.ptr(ds), K.ptr(gwp),
+               K.ptr(gbp), 1 if accp else 0, K.ptr(ws), M.d, K.stream())
+    dug = bn_bwd(ds, ug, cg, bng, False, M, part=pg)
+    dux = bn_bwd(ds, ux, cx, bnx, False, M, part=px)
 
     def wgs():
         wgrad1x1(dug, [g], wg.weight, M)
