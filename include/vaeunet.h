@@ -450,6 +450,16 @@ int vu_bn_bwd_apply(const void* dy, int64_t dy_stride, const void* x,
                     const float* shift, const float* mean, const float* coef,
                     int relu, void* dx, int64_t dx_stride, int dtype,
                     void* stream);
+/* the backward apply (no ReLU) of TWO BatchNorms fed by the same output
+ * gradient dy (the attention gate's W_g / W_x BatchNorms, whose gradient is
+ * the psi backward's ds): dx1 from (x1, mean1, coef1 = that BN's
+ * vu_bn_bwd_finish coefficients), dx2 likewise, dy read once; per element
+ * vu_bn_bwd_apply's arithmetic (round 6) */
+int vu_bn_bwd_apply2_ok(int C, int64_t dys, int64_t x1s, int64_t x2s, int64_t dx1s, int64_t dx2s);
+int vu_bn_bwd_apply2(const void* dy, int64_t dys, const void* x1, int64_t x1s, const void* x2, int64_t x2s,
+                     int64_t P, int C, const float* mean1, const float* coef1, const float* mean2,
+                     const float* coef2, void* dx1, int64_t dx1s, void* dx2, int64_t dx2s, int dtype,
+                     void* stream);
 
 /* ---- per-channel reductions / elementwise ------------------------------ */
 /* out[c] (=|+=) sum over the pixels of the (Hr, Wr) window at (y0, x0) of

@@ -167,3 +167,30 @@ def test_psi_bwd_emits_both_batchnorm_partials(dt, case):
         torch.testing.assert_close(dbeta.double().cpu(), s0, rtol=0, atol=2e-6 * float(ds.abs().sum(0).max()))
         torch.testing.assert_close(dgamma.double().cpu(), s1, rtol=0,
                                    atol=2e-6 * float((ds * xhat).abs().sum(0).max()))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("P,F", [(4096, 32), (2048 + 77, 64), (777, 256), (300, 512)])
+def test_paired_bn_backward_apply_bit_identical(dt, P, F):
+    """Round 6: vu_bn_bwd_apply2 (the attention gate's two BatchNorms from one
+    read of ds) writes the bits of two vu_bn_bwd_apply calls (no ReLU)."""
+    K = _k()
+    from vaeunet_amd import _lib
+    d = _lib.BF16 if dt == torch.bfloat16 else _lib.F32
+    g = torch.Generator().manual_seed(43)
+    ds, x1, x2 = (torch.randn(P, F, generator=g).to(dt).to(DEV) for _ in range(3))
+    c1 = [(torch.rand(F, generator=g) + 0.5).to(DEV) for _ in range(4)]
+    c2 = [(torch.rand(F, generator=g) + 0.5).to(DEV) for _ in range(4)]
+    k1, k2 = torch.randn(3, F, generator=g).to(DEV), torch.randn(3, F, generator=g).to(DEV)
+    ref = []
+    for x, c, k in ((x1, c1, k1), (x2, c2, k2)):
+        o = torch.empty_like(x)
+        K.call("vu_bn_bwd_apply", K.ptr(ds), F, K.ptr(x), F, P, F, K.ptr(c[0]), K.ptr(c[1]), K.ptr(c[2]), K.ptr(k), 0,
+               K.ptr(o), F, d, K.stream())
+        ref.append(o)
+    o1, o2 = torch.full_like(x1, float("nan")), torch.full_like(x2, float("nan"))
+    assert K.query("vu_bn_bwd_apply2_ok", F, F, F, F, F, F)
+    K.call("vu_bn_bwd_apply2", K.ptr(ds), F, K.ptr(x1), F, K.ptr(x2), F, P, F, K.ptr(c1[2]), K.ptr(k1), K.ptr(c2[2]),
+           K.ptr(k2), K.ptr(o1), F, K.ptr(o2), F, d, K.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(o1, ref[0]) and torch.equal(o2, ref[1])

@@ -217,10 +217,22 @@ class _DzRecorder:
                 self.dz[pre] = d.to(self.dtype).cpu()
             return orig(dy, xx, coef, bn, relu, M, *a, **kw)
         E.bn_bwd = bn_bwd
+        # the attention gates' W_g / W_x BatchNorms (round 6: one paired
+        # backward, no ReLU: dz = ds for both)
+        self.orig_pair = orig_pair = E.bn_bwd_pair
+
+        def bn_bwd_pair(dy, a, b, M):
+            for _, _, bn, _ in (a, b):
+                pre = self.names.get(id(bn))
+                if pre is not None:
+                    self.dz[pre] = dy.detach().float().to(self.dtype).cpu()
+            return orig_pair(dy, a, b, M)
+        E.bn_bwd_pair = bn_bwd_pair
         return self
 
     def __exit__(self, *a):
         self.E.bn_bwd = self.orig
+        self.E.bn_bwd_pair = self.orig_pair
         self.K.bn_backward = self.orig_k
         return False
 

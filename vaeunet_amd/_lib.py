@@ -137,6 +137,8 @@ _SIGS = {
     "vu_bn_bwd_reduce": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _i, _i, _p, _p, _i,
                               _p, _p, _i, _p]),
     "vu_bn_bwd_apply": (_i, [_p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _i, _p, _l, _i, _p]),
+    "vu_bn_bwd_apply2_ok": (_i, [_i, _l, _l, _l, _l, _l]),
+    "vu_bn_bwd_apply2": (_i, [_p, _l, _p, _l, _p, _l, _l, _i, _p, _p, _p, _p, _p, _l, _p, _l, _i, _p]),
     "vu_reduce_workspace_bytes": (_l, [_l, _i]),
     "vu_chan_sum": (_i, [_p, _l, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p, _i, _p]),
     "vu_copy": (_i, [_p, _l, _i, _p, _l, _i, _l, _i, _i, _p]),

@@ -391,7 +391,7 @@ __global__ void bn_bwd_final(const float* part, int nblk, int C, int64_t P, cons
 }
 
 template <typename T, bool NT>
-__global__ void bn_bwd_apply_kernel(const T* dy, int64_t dys, const T* x, int64_t xs, int64_t P, int C,
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* dy, int64_t dys, const T* x, int64_t xs, int64_t P, int C,
                                     const float* scale, const float* shift, const float* mean,
                                     const float* coef, int relu, T* dx, int64_t dxs) {
   ChanMap cm(C);
@@ -430,6 +430,58 @@ __global__ void bn_bwd_apply_kernel(const T* dy, int64_t dys, const T* x, int64_
         vo.set(i, fmaf(k1[i], dz, k2[i] * (xv - mu[i])) + k3[i]);
       }
       vo.store(dx + p * dxs + c);
+    }
+  }
+}
+
+// Round 6: the backward apply of TWO BatchNorms (no ReLU) fed by the SAME
+// output gradient -- the attention gate's W_g and W_x BatchNorms, whose
+// output gradient is the psi backward's ds (unet_parts.py:11-20): dz read
+// once, both input gradients written; per element exactly
+// bn_bwd_apply_kernel's arithmetic.
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void bn_bwd_apply2_kernel(const T* dy, int64_t dys, const T* x1, int64_t x1s, const T* x2, int64_t x2s,
+                                     int64_t P, int C, const float* mean1, const float* coef1, const float* mean2,
+                                     const float* coef2, T* dx1, int64_t dx1s, T* dx2, int64_t dx2s) {
+  ChanMap cm(C);
+  const int c = cm.cv * 8;
+  float mu1[8], a1[8], b1[8], e1[8], mu2[8], a2[8], b2[8], e2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu1[i] = mean1[c + i]; a1[i] = coef1[c + i]; b1[i] = coef1[C + c + i]; e1[i] = coef1[2 * C + c + i];
+    mu2[i] = mean2[c + i]; a2[i] = coef2[c + i]; b2[i] = coef2[C + c + i]; e2[i] = coef2[2 * C + c + i];
+  }
+  const int64_t step = (int64_t)gridDim.x * cm.R * UNR;
+  for (int64_t p0 = (int64_t)blockIdx.x * cm.R * UNR + cm.row; p0 < P; p0 += step) {
+    Vec8<T> vd[UNR], v1[UNR], v2[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * cm.R;
+      if (p < P) {
+        if (NT) {
+          vd[u].load_nt(dy + p * dys + c);
+          v1[u].load_nt(x1 + p * x1s + c);
+          v2[u].load_nt(x2 + p * x2s + c);
+        } else {
+          vd[u].load(dy + p * dys + c);
+          v1[u].load(x1 + p * x1s + c);
+          v2[u].load(x2 + p * x2s + c);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = p0 + (int64_t)u * cm.R;
+      if (p >= P) continue;
+      Vec8<T> o1, o2;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float dz = vd[u].get(i);
+        o1.set(i, fmaf(a1[i], dz, b1[i] * (v1[u].get(i) - mu1[i])) + e1[i]);
+        o2.set(i, fmaf(a2[i], dz, b2[i] * (v2[u].get(i) - mu2[i])) + e2[i]);
+      }
+      o1.store(dx1 + p * dx1s + c);
+      o2.store(dx2 + p * dx2s + c);
     }
   }
 }
@@ -1168,6 +1220,35 @@ extern "C" int vu_bn_bwd_apply(const void* dy, int64_t dys, const void* x, int64
       hipLaunchKernelGGL(bn_bwd_apply_scalar<float>, dim3(ew_grid(P * C)), dim3(256), 0, st,
                          (const float*)dy, dys, (const float*)x, xs, P, C, scale, shift, mean, coef,
                          relu, (float*)dx, dxs);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int vu_bn_bwd_apply2_ok(int C, int64_t dys, int64_t x1s, int64_t x2s, int64_t dx1s, int64_t dx2s) {
+  return chanmap_ok(C, dys, x1s, x2s) && chanmap_ok(C, dx1s, dx2s, 8) ? 1 : 0;
+}
+
+extern "C" int vu_bn_bwd_apply2(const void* dy, int64_t dys, const void* x1, int64_t x1s, const void* x2,
+                                int64_t x2s, int64_t P, int C, const float* mean1, const float* coef1,
+                                const float* mean2, const float* coef2, void* dx1, int64_t dx1s, void* dx2,
+                                int64_t dx2s, int dtype, void* stream) {
+  if (!vu_bn_bwd_apply2_ok(C, dys, x1s, x2s, dx1s, dx2s)) return (int)hipErrorInvalidValue;
+  if (P * C == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned grid = chan_grid(P, C, 8192);
+  if (dtype == VU_BF16) {
+    if (bn_nt(P, C, 2))
+      hipLaunchKernelGGL((bn_bwd_apply2_kernel<bf16_t, true>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy, dys,
+                         (const bf16_t*)x1, x1s, (const bf16_t*)x2, x2s, P, C, mean1, coef1, mean2, coef2,
+                         (bf16_t*)dx1, dx1s, (bf16_t*)dx2, dx2s);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply2_kernel<bf16_t, false>), dim3(grid), dim3(256), 0, st, (const bf16_t*)dy,
+                         dys, (const bf16_t*)x1, x1s, (const bf16_t*)x2, x2s, P, C, mean1, coef1, mean2, coef2,
+                         (bf16_t*)dx1, dx1s, (bf16_t*)dx2, dx2s);
+  } else {
+    hipLaunchKernelGGL((bn_bwd_apply2_kernel<float, false>), dim3(grid), dim3(256), 0, st, (const float*)dy, dys,
+                       (const float*)x1, x1s, (const float*)x2, x2s, P, C, mean1, coef1, mean2, coef2, (float*)dx1,
+                       dx1s, (float*)dx2, dx2s);
   }
   return (int)hipGetLastError();
 }

@@ -501,6 +501,23 @@ def bn_bwd(dy, x, coef, bn, relu, M, dx=None, part=None, zrs=None):
     return dx
 
 
+def bn_bwd_pair(dy, a, b, M):
+    """Backward of two BatchNorms (no ReLU) fed by the same dy, each
+    a / b = (x, coef, bn, BnbPart): both fp64 finishes, then one apply pass
+    that reads dy once (vu_bn_bwd_apply2; the attention gate's W_g / W_x
+    BatchNorms, round 6).  Returns (dx_a, dx_b)."""
+    outs, ks = [], []
+    for x, coef, bn, part in (a, b):
+        gw, gb, acc = bn_grad_sinks(bn)
+        ks.append(K.bn_backward_finish(part, x, coef, bn.weight, gw, gb, acc, train=bn.training))
+        outs.append(torch.empty_like(x))
+    (xa, ca, _, _), (xb, cb, _, _) = a, b
+    if not K.bn_backward_apply2(dy, xa, ca, ks[0], outs[0], xb, cb, ks[1], outs[1], K.dcode(xa.dtype)):
+        K._apply(dy, xa, ca, ks[0], False, outs[0], K.dcode(xa.dtype), None)
+        K._apply(dy, xb, cb, ks[1], False, outs[1], K.dcode(xb.dtype), None)
+    return outs[0], outs[1]
+
+
 # ----------------------------------------------------------------------------
 # DoubleConv  (unet_parts.py:32-49; DecoderBlock conv1/conv2 unet_resnet.py:59-69)
 #   conv3x3(no bias) -> BN -> ReLU -> conv3x3(no bias) -> BN -> ReLU
@@ -742,8 +759,11 @@ def attention_bwd(M, att, saved, dout, dg_out, dg_acc):
         K.call("vu_attn_psi_bwd", K.ptr(ug), K.ptr(ux), P, F, K.ptr(cg[0]), K.ptr(cg[1]),
                K.ptr(cx[0]), K.ptr(cx[1]), K.ptr(wp.weight), K.ptr(dq), K.ptr(ds), K.ptr(gwp),
                K.ptr(gbp), 1 if accp else 0, K.ptr(ws), M.d, K.stream())
-    dug = bn_bwd(ds, ug, cg, bng, False, M, part=pg)
-    dux = bn_bwd(ds, ux, cx, bnx, False, M, part=px)
+    if pg is not None:
+        dug, dux = bn_bwd_pair(ds, (ug, cg, bng, pg), (ux, cx, bnx, px), M)
+    else:
+        dug = bn_bwd(ds, ug, cg, bng, False, M)
+        dux = bn_bwd(ds, ux, cx, bnx, False, M)
 
     def wgs():
         wgrad1x1(dug, [g], wg.weight, M)

@@ -609,6 +609,30 @@ def bn_backward_part(part, dy, x, coef, gamma, relu, dgamma, dbeta, acc, dx, dty
     return dx
 
 
+def bn_backward_finish(part, x, coef, gamma, dgamma, dbeta, acc, train=True):
+    """The fp64 finish of a BnbPart: dgamma / dbeta written (or added) and the
+    apply coefficients k (3 x C) returned -- bn_backward_part without its apply."""
+    N, Cc, H, W = x.shape
+    k = torch.empty((3, Cc), dtype=torch.float32, device=x.device)
+    nb = query("vu_bn_bwd_finish_workspace_bytes", part.nblk, Cc)
+    ws = workspace_f32(nb, x.device) if nb > 0 else None
+    call("vu_bn_bwd_finish", ptr(part.part), part.nblk, N * H * W, Cc, ptr(gamma), ptr(coef[3]), 1 if train else 0,
+         ptr(dgamma), ptr(dbeta), 1 if acc else 0, ptr(k), ptr(ws), stream())
+    return k
+
+
+def bn_backward_apply2(dy, x1, coef1, k1, dx1, x2, coef2, k2, dx2, dtype):
+    """Backward apply (no ReLU) of two BatchNorms fed by the same dy: dy read
+    once (vu_bn_bwd_apply2).  False when the layout is not served."""
+    N, Cc, H, W = x1.shape
+    if not query("vu_bn_bwd_apply2_ok", Cc, pstride(dy), pstride(x1), pstride(x2), pstride(dx1), pstride(dx2)):
+        return False
+    call("vu_bn_bwd_apply2", ptr(dy), pstride(dy), ptr(x1), pstride(x1), ptr(x2), pstride(x2), N * H * W, Cc,
+         ptr(coef1[2]), ptr(k1), ptr(coef2[2]), ptr(k2), ptr(dx1), pstride(dx1), ptr(dx2), pstride(dx2), dtype,
+         stream())
+    return True
+
+
 def chan_sum(x, out, acc, dtype, window=None):
     N, Cc, H, W = x.shape
     y0, x0, Hr, Wr = window if window is not None else (0, 0, H, W)
