@@ -262,6 +262,12 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     the two wave halves' epilogues staggered into the next tile's first
  *     group (bit-identical results), 0 = the round-5 lock-step kernel. */
 #define VU_TUNE_V6_STAG 34
+/*   VU_TUNE_BN_STATS1: 1 = vu_bn_finalize as one launch (the last block of
+ *     each channel group combines the group's partials; measured 4x slower
+ *     per launch: the per-block agent-scope release), 0 (default) = the
+ *     two-launch path (stage 1 + stage 2).  Same fp64 combine up to the
+ *     summation order. */
+#define VU_TUNE_BN_STATS1 35
 int vu_gemm_set_tuning(int key, int value);
 /* Bit mask of the experiment modes currently non-zero (bit 0 V6_XM, 1 V7_XM,
  * 2 FP8_XM): 0 in production.  bench.py refuses to report while it is not. */

@@ -949,12 +949,26 @@ def test_batchnorm_train(mode, relu, shape):
     torch.testing.assert_close(bn_dev.bias.grad.cpu(), bn.bias.grad, rtol=2e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("tiles,tile_rows,C", [(40000, 7, 64), (300, 128, 192), (5, 64, 8)])
-def test_bn_finalize_partials(tiles, tile_rows, C):
+@pytest.mark.parametrize("stats1", [1, 0])
+@pytest.mark.parametrize("tiles,tile_rows,C", [(40000, 7, 64), (300, 128, 192), (5, 64, 8), (16385, 4, 16),
+                                              (64, 128, 1024)])
+def test_bn_finalize_partials(tiles, tile_rows, C, stats1):
     """vu_bn_finalize on synthetic per-tile (sum, M2) partials: several rounds
     per block (tiles > 64 x 256), several blocks and channel groups, a ragged
-    last tile; mean / biased var / running stats vs an fp64 combination."""
+    last tile, an empty last block (16385 tiles); mean / biased var / running
+    stats vs an fp64 combination.  stats1: the one-launch finalize (the last
+    block of each channel group combines, VU_TUNE_BN_STATS1 = 1, opt-in) or
+    the two-launch path (default)."""
     K, _ = _k()
+    from vaeunet_amd import _lib as lib
+    lib.call("vu_gemm_set_tuning", 35, stats1)
+    try:
+        _bn_finalize_partials(K, tiles, tile_rows, C)
+    finally:
+        lib.call("vu_gemm_set_tuning", 35, 0)
+
+
+def _bn_finalize_partials(K, tiles, tile_rows, C):
     g = torch.Generator().manual_seed(41)
     rows = tiles * tile_rows - 3
     n = torch.full((tiles,), float(tile_rows), dtype=torch.float64)

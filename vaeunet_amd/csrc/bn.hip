@@ -172,6 +172,164 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
   }
 }
 
+// Round 6: the statistics finalize as ONE launch (VU_TUNE_BN_STATS1; measured
+// slower, OFF: 45 us per launch against ~12 us for the two launches, UNet
+// -5.6 %, VAE -4.5 %, profiles/r6s1_*; the agent-scope release every block
+// needs before it counts writes the XCD's L2 back, and the per-block fences
+// serialise).  Stage 1 as bn_stats_stage1 with 64 channels x 16 tile lanes per
+// 1024-thread block (64 tiles per round); each block publishes its (mean, M2)
+// per channel, and the last block of its channel group to arrive -- counted
+// on a per-group device counter, which that block resets for the next launch
+// -- combines the group's S <= 256 partials (<= 16 per lane, about the group
+// mean in fp64, as stage 2) and writes the coefficients.  Saves stage 2's
+// launch per BatchNorm, a latency-bound ~6 us kernel (rocprof,
+// profiles/r6a5_unet_kernel_stats_attn_pair.csv: 25 per UNet step) -- in
+// principle.
+// The counters assume the launches of one device do not overlap one another
+// (one stream, as every caller runs them).
+constexpr int FST_LANES = 16, FST_U = 4, FST_TPB = FST_LANES * FST_U, FST_MAXS = 256, FST_MAXG = 64;
+constexpr int FST_PL = FST_MAXS / FST_LANES;   // partials per lane in the last block
+__device__ unsigned int g_fst_count[FST_MAXG];
+
+VU_DEV double fst_block_rows(int s, int per, int tiles, int64_t tile_rows, int64_t rows) {
+  const int tb = s * per;
+  if (tb >= tiles) return 0.0;
+  const int te = min(tiles, tb + per);
+  return (double)(min(rows, (int64_t)te * tile_rows) - (int64_t)tb * tile_rows);
+}
+
+__global__ __launch_bounds__(1024) void bn_stats_fused_kernel(
+    const float* psum, const float* pm2, int tiles, int64_t tile_rows, int64_t rows, int C, int S, double* ws,
+    const float* gamma, const float* beta, float* rmean, float* rvar, float momentum, float eps, float* scale,
+    float* shift, float* smean, float* sinvstd, int64_t* nbt) {
+  __shared__ double sh[2][FST_LANES][64];
+  __shared__ int is_last;
+  const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  const int cc = ok ? c : 0;
+  const int per = (tiles + S - 1) / S;
+  const int tb0 = blockIdx.y * per, te0 = min(tiles, tb0 + per);
+  double N = 0, Mn = 0, Q = 0;
+  for (int tb = tb0; tb < te0; tb += FST_TPB) {
+    const int te = min(te0, tb + FST_TPB);
+    const int64_t n_r = min(rows, (int64_t)te * tile_rows) - (int64_t)tb * tile_rows;
+    float sv[FST_U], mv[FST_U];
+    double nv[FST_U];
+#pragma unroll
+    for (int u = 0; u < FST_U; ++u) {
+      const int t = min(tb + tl + FST_LANES * u, te - 1);
+      sv[u] = psum[(int64_t)t * C + cc];
+      mv[u] = pm2[(int64_t)t * C + cc];
+    }
+#pragma unroll
+    for (int u = 0; u < FST_U; ++u) {
+      const int t = tb + tl + FST_LANES * u;
+      const bool in = ok && t < te;
+      sv[u] = in ? sv[u] : 0.f;
+      mv[u] = in ? mv[u] : 0.f;
+      const int64_t nt = rows - (int64_t)t * tile_rows;
+      nv[u] = in ? (double)(nt > tile_rows ? tile_rows : nt) : 0.0;
+    }
+    double s = 0;
+#pragma unroll
+    for (int u = 0; u < FST_U; ++u) s += (double)sv[u];
+    sh[0][tl][cl] = s;
+    __syncthreads();
+    double st = 0;
+#pragma unroll
+    for (int l = 0; l < FST_LANES; ++l) st += sh[0][l][cl];
+    const double m = st / (double)n_r;
+    double q = 0;
+#pragma unroll
+    for (int u = 0; u < FST_U; ++u) {
+      if (nv[u] > 0) {
+        const double d = (double)sv[u] / nv[u] - m;
+        q += (double)mv[u] + nv[u] * d * d;
+      }
+    }
+    sh[1][tl][cl] = q;
+    __syncthreads();
+    double q_r = 0;
+#pragma unroll
+    for (int l = 0; l < FST_LANES; ++l) q_r += sh[1][l][cl];
+    __syncthreads();
+    const double nn = N + (double)n_r, d = m - Mn;
+    Q += q_r + d * d * N * (double)n_r / nn;
+    Mn += d * (double)n_r / nn;
+    N = nn;
+  }
+  if (tl == 0 && ok) {
+    double* o = ws + ((int64_t)blockIdx.y * C + c) * 2;
+    o[0] = Mn;
+    o[1] = Q;
+  }
+  // publish, count, and let the last block of the channel group go on
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(&g_fst_count[blockIdx.x], 1u);
+    is_last = prev == (unsigned)(S - 1);
+    if (is_last) atomicExch(&g_fst_count[blockIdx.x], 0u);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  const float g = gamma ? gamma[cc] : 1.f, b = beta ? beta[cc] : 0.f;
+  const bool upd = rmean && momentum != 0.f;
+  const float rm0 = upd ? rmean[cc] : 0.f, rv0 = upd ? rvar[cc] : 0.f;
+  const int64_t nb0 = nbt ? nbt[0] : 0;
+  double pm[FST_PL], pq[FST_PL], pn[FST_PL];
+#pragma unroll
+  for (int u = 0; u < FST_PL; ++u) {
+    const double* o = ws + ((int64_t)min(tl + FST_LANES * u, S - 1) * C + cc) * 2;
+    pm[u] = o[0];
+    pq[u] = o[1];
+  }
+#pragma unroll
+  for (int u = 0; u < FST_PL; ++u) {
+    const int s = tl + FST_LANES * u;
+    const bool in = ok && s < S;
+    pn[u] = in ? fst_block_rows(s, per, tiles, tile_rows, rows) : 0.0;
+    pm[u] = in ? pm[u] : 0.0;
+    pq[u] = in ? pq[u] : 0.0;
+  }
+  double n = 0, sm = 0;
+#pragma unroll
+  for (int u = 0; u < FST_PL; ++u) { n += pn[u]; sm += pn[u] * pm[u]; }
+  sh[0][tl][cl] = n;
+  sh[1][tl][cl] = sm;
+  __syncthreads();
+  n = 0;
+  sm = 0;
+#pragma unroll
+  for (int l = 0; l < FST_LANES; ++l) { n += sh[0][l][cl]; sm += sh[1][l][cl]; }
+  const double m = n > 0 ? sm / n : 0.0;
+  __syncthreads();
+  double M2 = 0;
+#pragma unroll
+  for (int u = 0; u < FST_PL; ++u) { const double d = pm[u] - m; M2 += pq[u] + pn[u] * d * d; }
+  sh[0][tl][cl] = M2;
+  __syncthreads();
+  if (tl != 0 || !ok) return;
+  M2 = 0;
+#pragma unroll
+  for (int l = 0; l < FST_LANES; ++l) M2 += sh[0][l][cl];
+  const double var = n > 0 ? M2 / n : 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float mean = (float)m;
+  scale[c] = g * invstd;
+  shift[c] = b - mean * g * invstd;
+  if (smean) smean[c] = mean;
+  if (sinvstd) sinvstd[c] = invstd;
+  if (nbt && c == 0) nbt[0] = nb0 + 1;
+  if (upd) {
+    const double unb = n > 1 ? M2 / (n - 1) : var;
+    rmean[c] = (1.f - momentum) * rm0 + momentum * mean;
+    rvar[c] = (1.f - momentum) * rv0 + momentum * (float)unb;
+  }
+}
+
 __global__ void bn_eval_kernel(const float* gamma, const float* beta, const float* rm, const float* rv,
                                float eps, int C, float* scale, float* shift, float* smean, float* sinvstd) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -988,6 +1146,7 @@ inline unsigned chan_grid16(int64_t P, int C, int maxblk) {
 // layer3 BN backward).  VU_TUNE_BN_MINBLK, 0 = the 16-row grid only.
 int g_bn_minblk = 256;
 int g_bn_onepass = 0;  // VU_TUNE_BN_ONEPASS (vu_bn_bwd_fused below; measured slower, off)
+int g_bn_stats1 = 0;   // VU_TUNE_BN_STATS1 (vu_bn_finalize as one launch; measured slower, off)
 inline unsigned chan_grid(int64_t P, int C, int maxblk) {
   int R = 256 / (C / 8);
   int64_t g = (P + (int64_t)R * 16 - 1) / ((int64_t)R * 16);
@@ -1052,6 +1211,10 @@ int bn_tune(int key, int value) {
     g_bn_onepass = value ? 1 : 0;
     return 0;
   }
+  if (key == VU_TUNE_BN_STATS1) {
+    g_bn_stats1 = value ? 1 : 0;
+    return 0;
+  }
   if (key == VU_TUNE_BN_MINBLK) {
     g_bn_minblk = value < 0 ? 0 : value;
     return 0;
@@ -1082,8 +1245,17 @@ extern "C" int vu_bn_finalize(const float* psum, const float* pm2, int tiles, in
                               float* scale, float* shift, float* save_mean, float* save_invstd,
                               int64_t* num_batches_tracked, float* workspace, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int S = stats_blocks(tiles);
   double* ws = reinterpret_cast<double*>(workspace);
+  if (g_bn_stats1 && C <= 64 * FST_MAXG && tiles >= 1) {
+    // (its S * C * 2 doubles fit in stats_blocks' S * C * 3: fewer blocks of more tiles)
+    int S2 = (tiles + FST_TPB - 1) / FST_TPB;
+    S2 = S2 > FST_MAXS ? FST_MAXS : S2;
+    hipLaunchKernelGGL(bn_stats_fused_kernel, dim3((C + 63) / 64, S2), dim3(1024), 0, st, psum, pm2, tiles,
+                       tile_rows, rows, C, S2, ws, gamma, beta, running_mean, running_var, momentum, eps, scale,
+                       shift, save_mean, save_invstd, num_batches_tracked);
+    return (int)hipGetLastError();
+  }
+  int S = stats_blocks(tiles);
   hipLaunchKernelGGL(bn_stats_stage1, dim3((C + 63) / 64, S), dim3(256), 0, st, psum, pm2, tiles,
                      tile_rows, rows, C, S, ws);
   hipLaunchKernelGGL(bn_stats_stage2, dim3((C + 31) / 32), dim3(1024), 0, st, ws, S, C, gamma, beta,
