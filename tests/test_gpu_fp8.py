@@ -316,7 +316,8 @@ def test_double_conv_fp8_default_is_self_contained():
     """the default forward scales just in time, so a second call on
     a 4x-larger input is not clipped by the first call's amax; a delayed call
     after reset_scales calibrates again (equal to just-in-time on its first
-    call); chained arguments without delayed=True are refused."""
+    call); chained arguments on the just-in-time path are refused only on the
+    round-5 two-pass form (JIT_MINMAX False)."""
     from vaeunet_amd import DoubleConv, fp8
     torch.manual_seed(8)
     mod = DoubleConv(64, 64).to(DEV)
@@ -332,8 +333,44 @@ def test_double_conv_fp8_default_is_self_contained():
     fp8.reset_scales(mod)
     y_cal = fp8.double_conv_forward(mod, x4, delayed=True).float()   # calibrates on x4
     assert ((y_cal - y_fresh).abs().max() / y_fresh.abs().max()).item() < 0.03
-    with pytest.raises(ValueError):
-        fp8.double_conv_forward(mod, None, x_q=([x], torch.ones(1, device=DEV)))
+    old = fp8.JIT_MINMAX
+    try:
+        fp8.JIT_MINMAX = False
+        with pytest.raises(ValueError):
+            fp8.double_conv_forward(mod, None, x_q=([x], torch.ones(1, device=DEV)))
+    finally:
+        fp8.JIT_MINMAX = old
+
+
+@pytest.mark.parametrize("up", [False, True])
+def test_double_conv_fp8_jit_chained(up):
+    """Chained just-in-time blocks (round 6): an e4m3 input quantised just in
+    time by the producer gives the bf16-input block's output bit for bit (the
+    same exact amax, the same quantiser); the e4m3 output's scale is the exact
+    max of relu(BN2(y2)) from conv2's min / max epilogue (the largest code is
+    448) and its dequantised values are the bf16-output block's up to one
+    e4m3 rounding."""
+    from vaeunet_amd import DoubleConv, fp8
+    torch.manual_seed(9)
+    cins = [64, 64] if up else [64]
+    mod = DoubleConv(sum(cins), 64 if up else 128).to(DEV)
+    xs = [_act(torch.randn(2, c, 64, 128).relu()) for c in cins]
+    ref = fp8.double_conv_forward(mod, xs)                   # bf16 in, bf16 out
+    ds = fp8.DelayedScale(DEV)
+    for t in xs:
+        fp8.calibrate(t, None, False, ds)
+    qs = []
+    for t in xs:
+        q, xdq = fp8.bn_apply_quant(t, None, False, ds)
+        qs.append(q)
+    y = fp8.double_conv_forward(mod, None, x_q=(qs, xdq))     # e4m3 in, bf16 out
+    assert torch.equal(y, ref)
+    q, dq = fp8.double_conv_forward(mod, None, x_q=(qs, xdq), out_fp8=True)
+    assert q.dtype == fp8.E4M3
+    assert q.float().abs().max().item() == 448.0
+    got, r = q.float() * dq, ref.float()
+    err = (got - r).abs()
+    assert (err <= 2.0 ** -3 * r.abs() + 1e-3 * r.abs().max()).all()
 
 
 def test_double_conv_fp8_chained():

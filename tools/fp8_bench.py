@@ -10,7 +10,9 @@ delayed-scaling fp8 path (fp8.double_conv_forward: one-pass input quantise,
 BN1 apply fused with the e4m3 quantise), the just-in-time fp8 path and the
 chained fp8 block (e4m3 in from the producing block, BN2 apply fused with
 the e4m3 quantise of the output: the steady state of consecutive fp8
-blocks) against the bf16 engine path (engine.double_conv_fwd) on the same
+blocks), the same chained block just in time (the input quantised by the
+producer with its exact amax, the output's exact amax from conv2's min / max
+epilogue: no history, no calibration pass) against the bf16 engine path (engine.double_conv_fwd) on the same
 module.
 
 usage: python tools/fp8_bench.py [--batch 2] [--reps 20] [--layers inc.2,...] [--double] [--json out.json]
@@ -43,7 +45,7 @@ def double_main(args):
     from vaeunet_amd import engine as E
     dev = torch.device("cuda")
     B = args.batch
-    rows, tot = [], {"bf16": 0.0, "fp8": 0.0, "fp8_jit": 0.0, "fp8_chain": 0.0, "fl": 0.0}
+    rows, tot = [], {"bf16": 0.0, "fp8": 0.0, "fp8_jit": 0.0, "fp8_chain": 0.0, "fp8_jit_chain": 0.0, "fl": 0.0}
     for name, cins, co, H in BLOCKS:
         if args.layers and name not in args.layers.split(","):
             continue
@@ -67,14 +69,25 @@ def double_main(args):
         qdq = fp8.bn_apply_quant(srcs[0], None, False, dsq)[1]
         del xq
         msc = timeit(lambda: fp8.double_conv_forward(mod, None, delayed=True, x_q=(qin, qdq), out_fp8=True), args.reps)
+        # chained just in time: the producer's e4m3 output (exact just-in-time
+        # scale) in, e4m3 out with the exact scale of relu(BN2(y2)) from conv2's
+        # min / max epilogue -- every call self-contained, no history
+        dsj = fp8.DelayedScale(dev)
+        for t in srcs:
+            fp8.calibrate(t, None, False, dsj)
+        qj = []
+        for t in srcs:
+            q_, jdq = fp8.bn_apply_quant(t, None, False, dsj)
+            qj.append(q_)
+        msjc = timeit(lambda: fp8.double_conv_forward(mod, None, x_q=(qj, jdq), out_fp8=True), args.reps)
         with torch.no_grad():
             yb = E.double_conv_fwd(M, mod.double_conv, srcs)[0].float()
             y8 = fp8.double_conv_forward(mod, srcs, delayed=True).float()
         row = {"block": name, "cin": ci, "cout": co, "hw": H, "bf16_us": round(msb * 1e3, 1),
                "fp8_us": round(ms8 * 1e3, 1), "fp8_jit_us": round(msj * 1e3, 1),
-               "fp8_chain_us": round(msc * 1e3, 1),
+               "fp8_chain_us": round(msc * 1e3, 1), "fp8_jit_chain_us": round(msjc * 1e3, 1),
                "speedup": round(msb / ms8, 3), "speedup_jit": round(msb / msj, 3),
-               "speedup_chain": round(msb / msc, 3),
+               "speedup_chain": round(msb / msc, 3), "speedup_jit_chain": round(msb / msjc, 3),
                "rel_err_vs_bf16": round(((y8 - yb).abs().max() / yb.abs().max()).item(), 4)}
         rows.append(row)
         print(json.dumps(row), flush=True)
@@ -82,6 +95,7 @@ def double_main(args):
         tot["fp8"] += ms8
         tot["fp8_jit"] += msj
         tot["fp8_chain"] += msc
+        tot["fp8_jit_chain"] += msjc
         tot["fl"] += fl
         del srcs, mod
         torch.cuda.empty_cache()
@@ -90,6 +104,8 @@ def double_main(args):
             "fp8_chain_ms": round(tot["fp8_chain"], 3),
             "speedup": round(tot["bf16"] / tot["fp8"], 3), "speedup_jit": round(tot["bf16"] / tot["fp8_jit"], 3),
             "speedup_chain": round(tot["bf16"] / tot["fp8_chain"], 3),
+            "fp8_jit_chain_ms": round(tot["fp8_jit_chain"], 3),
+            "speedup_jit_chain": round(tot["bf16"] / tot["fp8_jit_chain"], 3),
             "fp8_block_tflops": round(tot["fl"] / tot["fp8"] / 1e9, 1)}
     print("SUMMARY " + json.dumps(summ), flush=True)
     if args.json:

@@ -245,26 +245,33 @@ def double_conv_forward(mod, x, delayed=False, x_q=None, out_fp8=False):
     saturate at +-448.  The host-side slot counter advances per call: a
     captured graph would freeze it, so delayed calls are not graph-safe.
 
-    Chained fp8 blocks (delayed only): ``x_q = (e4m3 sources, dequant scale)``
-    is an input already quantised by the producing block, and
-    ``out_fp8=True`` applies BN2 + ReLU fused with the e4m3 quantisation of
-    the block's output (its own delayed scale) and returns ``(q, dq)`` --
-    the activations between fp8 blocks are then never stored in bf16."""
+    Chained fp8 blocks: ``x_q = (e4m3 sources, dequant scale)`` is an input
+    already quantised by the producing block, and ``out_fp8=True`` applies
+    BN2 + ReLU fused with the e4m3 quantisation of the block's output and
+    returns ``(q, dq)`` -- the activations between fp8 blocks are then never
+    stored in bf16.  Delayed: the output's own delayed scale.  Just in time
+    (round 6): the exact amax of relu(BN2(y2)) from conv2's min / max
+    epilogue, as conv2's input scale is formed from conv1's (a calibration
+    pass over y2 where the serving kernel emits no min / max)."""
     conv1, bn1, _, conv2, bn2, _ = mod.double_conv
     srcs = list(x) if isinstance(x, (list, tuple)) else ([x] if x is not None else [])
-    if (x_q is not None or out_fp8) and not delayed:
-        raise ValueError("fp8.double_conv_forward: x_q / out_fp8 (chained fp8 blocks) need delayed=True")
+    if (x_q is not None or out_fp8) and not delayed and not JIT_MINMAX:
+        raise ValueError("fp8.double_conv_forward: x_q / out_fp8 (chained fp8 blocks) need delayed=True "
+                         "or the min/max just-in-time path (JIT_MINMAX)")
     if not delayed:
         if JIT_MINMAX:
-            # the input: exact amax by the calibration pass (max-accumulated over
-            # the sources), one quantising pass per source with that scale
-            ds_x = DelayedScale(srcs[0].device)
-            for t in srcs:
-                calibrate(t, None, False, ds_x)
-            qs = []
-            for t in srcs:
-                q, xdq = bn_apply_quant(t, None, False, ds_x)
-                qs.append(q)
+            if x_q is not None:
+                qs, xdq = list(x_q[0]), x_q[1]
+            else:
+                # the input: exact amax by the calibration pass (max-accumulated
+                # over the sources), one quantising pass per source with that scale
+                ds_x = DelayedScale(srcs[0].device)
+                for t in srcs:
+                    calibrate(t, None, False, ds_x)
+                qs = []
+                for t in srcs:
+                    q, xdq = bn_apply_quant(t, None, False, ds_x)
+                    qs.append(q)
             w1, s1 = quantize_weight(conv1.weight)
             y1, st1 = conv3x3(qs, xdq, w1, s1, conv1.out_channels, stats=bn1.training, minmax=True)
         else:
@@ -276,12 +283,19 @@ def double_conv_forward(mod, x, delayed=False, x_q=None, out_fp8=False):
             # partials, then BN1 + ReLU + e4m3 in one pass (no bf16 a1)
             ds = relu_amax_scale(st1.minmax, coef1, True, y1.device)
             aq, adq = bn_apply_quant(y1, coef1, True, ds)
-            y2, st2 = conv3x3([aq], adq, w2, s2, conv2.out_channels, stats=bn2.training)
+            y2, st2 = conv3x3([aq], adq, w2, s2, conv2.out_channels, stats=bn2.training, minmax=out_fp8)
         else:
             a1 = torch.empty_like(y1)
             K.bn_apply(y1, a1, coef1, True, _lib.BF16)
-            y2, st2 = conv3x3_q([a1], conv2.weight, stats=bn2.training)
-        coef2 = E.bn_coef(bn2, st2, conv2.out_channels)
+            y2, st2 = conv3x3_q([a1], conv2.weight, stats=bn2.training, minmax=out_fp8)
+        coef2 = E.bn_coef(bn2, st2 if bn2.training else None, conv2.out_channels)
+        if out_fp8:
+            if st2 is not None and st2.minmax is not None:
+                ds = relu_amax_scale(st2.minmax, coef2, True, y2.device)
+            else:
+                ds = DelayedScale(y2.device)
+                calibrate(y2, coef2, True, ds)
+            return bn_apply_quant(y2, coef2, True, ds)
         out = torch.empty_like(y2)
         K.bn_apply(y2, out, coef2, True, _lib.BF16)
         return out
