@@ -263,8 +263,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     group (bit-identical results), 0 = the round-5 lock-step kernel. */
 #define VU_TUNE_V6_STAG 34
 /*   VU_TUNE_BN_STATS1: 1 = vu_bn_finalize as one launch (the last block of
- *     each channel group combines the group's partials; measured 4x slower
- *     per launch: the per-block agent-scope release), 0 (default) = the
+ *     each channel group combines the group's partials, handed off through
+ *     write-through stores and one agent-scope atomic per block; measured
+ *     0.6-1.1 % slower per step than the two launches), 0 (default) = the
  *     two-launch path (stage 1 + stage 2).  Same fp64 combine up to the
  *     summation order. */
 #define VU_TUNE_BN_STATS1 35

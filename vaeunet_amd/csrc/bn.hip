@@ -172,11 +172,14 @@ __global__ void bn_stats_stage2(const double* ws, int S, int C, const float* gam
   }
 }
 
-// Round 6: the statistics finalize as ONE launch (VU_TUNE_BN_STATS1; measured
-// slower, OFF: 45 us per launch against ~12 us for the two launches, UNet
-// -5.6 %, VAE -4.5 %, profiles/r6s1_*; the agent-scope release every block
-// needs before it counts writes the XCD's L2 back, and the per-block fences
-// serialise).  Stage 1 as bn_stats_stage1 with 64 channels x 16 tile lanes per
+// Round 6: the statistics finalize as ONE launch (VU_TUNE_BN_STATS1).  First
+// built with __threadfence() release / acquire in every block: 45 us per
+// launch against ~12 us for the two launches (UNet -5.6 %, VAE -4.5 %,
+// profiles/r6s1_*: each fence writes the XCD's L2 back and invalidates).  Now
+// fence-free, on the guide's measured sc1 hand-off (below): still UNet
+// -0.6/-0.7 %, VAE -0.9/-1.1 % (profiles/r6s2_*): the last block's serial
+// tail (atomic round trip, write-through loads) costs more than the second
+// launch it saves inside a graph replay.  Kept opt-in.  Stage 1 as bn_stats_stage1 with 64 channels x 16 tile lanes per
 // 1024-thread block (64 tiles per round); each block publishes its (mean, M2)
 // per channel, and the last block of its channel group to arrive -- counted
 // on a per-group device counter, which that block resets for the next launch
@@ -259,22 +262,27 @@ __global__ __launch_bounds__(1024) void bn_stats_fused_kernel(
     Mn += d * (double)n_r / nn;
     N = nn;
   }
-  if (tl == 0 && ok) {
-    double* o = ws + ((int64_t)blockIdx.y * C + c) * 2;
-    o[0] = Mn;
-    o[1] = Q;
-  }
-  // publish, count, and let the last block of the channel group go on
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(&g_fst_count[blockIdx.x], 1u);
-    is_last = prev == (unsigned)(S - 1);
-    if (is_last) atomicExch(&g_fst_count[blockIdx.x], 0u);
+  // publish and count without fences (MI355X_MICROARCH.md, hand-off table,
+  // first row: write-through sc1 stores by the storing wave, its vmcnt(0)
+  // wait, ONE agent-scope atomic add per workgroup; the workgroup whose add
+  // returned S - 1 reads every handed-off byte with sc1 loads behind a
+  // workgroup barrier).  Wave 0 (tl == 0) is the only storing wave.
+  if (tl == 0) {
+    if (ok) {
+      double* o = ws + ((int64_t)blockIdx.y * C + c) * 2;
+      __hip_atomic_store(o, Mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o + 1, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      const unsigned prev =
+          __hip_atomic_fetch_add(&g_fst_count[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = prev == (unsigned)(S - 1);
+      if (is_last) __hip_atomic_store(&g_fst_count[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   if (!is_last) return;
-  __threadfence();
   const float g = gamma ? gamma[cc] : 1.f, b = beta ? beta[cc] : 0.f;
   const bool upd = rmean && momentum != 0.f;
   const float rm0 = upd ? rmean[cc] : 0.f, rv0 = upd ? rvar[cc] : 0.f;
@@ -282,9 +290,9 @@ __global__ __launch_bounds__(1024) void bn_stats_fused_kernel(
   double pm[FST_PL], pq[FST_PL], pn[FST_PL];
 #pragma unroll
   for (int u = 0; u < FST_PL; ++u) {
-    const double* o = ws + ((int64_t)min(tl + FST_LANES * u, S - 1) * C + cc) * 2;
-    pm[u] = o[0];
-    pq[u] = o[1];
+    double* o = ws + ((int64_t)min(tl + FST_LANES * u, S - 1) * C + cc) * 2;
+    pm[u] = __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pq[u] = __hip_atomic_load(o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #pragma unroll
   for (int u = 0; u < FST_PL; ++u) {
