@@ -416,12 +416,12 @@ __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux
   for (int cc = threadIdx.x; cc < F; cc += 256) {
     int sb_ = cc >> 3, k = cc & 7;
     float s = 0.f;
-    for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
+    s = lds_sum(sh + sb_ * 8 + k, (256 - sb_ + lpp - 1) / lpp, lpp * 8);
     part[(int64_t)blockIdx.x * (F + 1) + cc] = s;
   }
   if (threadIdx.x == 0) {
     float s = 0.f;
-    for (int t = 0; t < 256; ++t) s += sb[t];
+    s = lds_sum(sb, 256, 1);
     part[(int64_t)blockIdx.x * (F + 1) + F] = s;
   }
   if constexpr (BNB) {
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void psi_bwd_u_kernel(const T* ug, const T* ux
       for (int cc = threadIdx.x; cc < F; cc += 256) {
         int sb_ = cc >> 3, k = cc & 7;
         float v = 0.f;
-        for (int t = sb_; t < 256; t += lpp) v += sh[t * 8 + k];
+        v = lds_sum(sh + sb_ * 8 + k, (256 - sb_ + lpp - 1) / lpp, lpp * 8);
         if (q == 0) {
           bnb_g[((int64_t)blockIdx.x * 2 + 0) * F + cc] = v;
           bnb_x[((int64_t)blockIdx.x * 2 + 0) * F + cc] = v;
@@ -492,12 +492,12 @@ __global__ void psi_bwd_kernel(const T* ug, const T* ux, int64_t P, int F, const
   for (int cc = threadIdx.x; cc < F; cc += 256) {
     int sb_ = cc >> 3, k = cc & 7;
     float s = 0.f;
-    for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
+    s = lds_sum(sh + sb_ * 8 + k, (256 - sb_ + lpp - 1) / lpp, lpp * 8);
     part[(int64_t)blockIdx.x * (F + 1) + cc] = s;
   }
   if (threadIdx.x == 0) {
     float s = 0.f;
-    for (int t = 0; t < 256; ++t) s += sb[t];
+    s = lds_sum(sb, 256, 1);
     part[(int64_t)blockIdx.x * (F + 1) + F] = s;
   }
 }
@@ -706,7 +706,7 @@ __global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, con
     for (int cc = threadIdx.x; cc < C; cc += 256) {
       int sb_ = cc >> 3, k = cc & 7;
       float s = 0.f;
-      for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
+      s = lds_sum(sh + sb_ * 8 + k, (256 - sb_ + lpp - 1) / lpp, lpp * 8);
       part[(int64_t)blockIdx.x * width + j * C + cc] = s;
     }
     __syncthreads();
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, con
     __syncthreads();
     if (threadIdx.x == 0) {
       float s = 0.f;
-      for (int t = 0; t < 256; ++t) s += sh[t];
+      s = lds_sum(sh, 256, 1);
       part[(int64_t)blockIdx.x * width + J * C + j] = s;
     }
   }
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(256) void pw_bwd_kernel(const T* x, int64_t xs, con
       for (int cc = threadIdx.x; cc < C; cc += 256) {
         int sb_ = cc >> 3, k = cc & 7;
         float s = 0.f;
-        for (int t = sb_; t < 256; t += lpp) s += sh[t * 8 + k];
+        s = lds_sum(sh + sb_ * 8 + k, (256 - sb_ + lpp - 1) / lpp, lpp * 8);
         bnb[((int64_t)blockIdx.x * 2 + q) * C + cc] = s;
       }
     }

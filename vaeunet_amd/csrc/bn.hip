@@ -472,7 +472,8 @@ __global__ void chan_partial_kernel(RedArgs r) {
   __syncthreads();
   for (int cc = threadIdx.x; cc < r.C; cc += 256) {
     float a0 = 0.f, a1 = 0.f;
-    for (int q = 0; q < cm.R; ++q) { a0 += sh[0][q * r.C + cc]; a1 += sh[1][q * r.C + cc]; }
+    a0 = lds_sum(&sh[0][cc], cm.R, r.C);
+    a1 = lds_sum(&sh[1][cc], cm.R, r.C);
     r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + cc] = a0;
     if (MODE == 1) r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + cc] = a1;
   }
@@ -518,7 +519,8 @@ __global__ void chan_partial_scalar(RedArgs r) {
   __syncthreads();
   if (t < r.C) {
     float a0 = 0.f, a1 = 0.f;
-    for (int q = 0; q < R; ++q) { a0 += sh[0][q * r.C + t]; a1 += sh[1][q * r.C + t]; }
+    a0 = lds_sum(&sh[0][t], R, r.C);
+    a1 = lds_sum(&sh[1][t], R, r.C);
     r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + t] = a0;
     r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + t] = a1;
   }
@@ -822,7 +824,8 @@ __global__ void pool_bn_partial_kernel(PoolBnArgs r) {
   __syncthreads();
   for (int cc = threadIdx.x; cc < r.C; cc += 256) {
     float a0 = 0.f, a1 = 0.f;
-    for (int q = 0; q < cm.R; ++q) { a0 += sh[0][q * r.C + cc]; a1 += sh[1][q * r.C + cc]; }
+    a0 = lds_sum(&sh[0][cc], cm.R, r.C);
+    a1 = lds_sum(&sh[1][cc], cm.R, r.C);
     r.part[((int64_t)blockIdx.x * 2 + 0) * r.C + cc] = a0;
     r.part[((int64_t)blockIdx.x * 2 + 1) * r.C + cc] = a1;
   }

@@ -186,4 +186,22 @@ VU_DEV void colsum32(const float* part, int rows, int64_t row_stride, int64_t q_
   for (int k = 0; k < NQ; ++k) out[k] = sh[k][0][cl];
 }
 
+// sum_{q < n} p[q * stride] accumulated from 0.f in the order q = 0, 1, ...
+// (bit-identical to the plain loop) with 8 LDS reads in flight: the block-
+// reduction tails of the streaming kernels read one term per LDS round trip
+// as a loop-carried chain (round 6: up to 256 serial reads by one thread).
+VU_DEV float lds_sum(const float* p, int n, int stride) {
+  float s = 0.f;
+  int q = 0;
+  for (; q + 8 <= n; q += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(q + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; q < n; ++q) s += p[q * stride];
+  return s;
+}
+
 #define VU_CHECK_LAUNCH() return (int)hipGetLastError()

@@ -226,10 +226,21 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
     float* red = reinterpret_cast<float*>(smem + LDS_BYTES - RED);
     constexpr int PARTS = NT / BN;
     constexpr int RPP = BM / PARTS;
+    static_assert(RPP % 16 == 0, "statistics rows per thread: whole batches of 16");
     const int col = tid % BN, part = tid / BN;
-    const int r0 = part * RPP, r1 = min((part + 1) * RPP, rows_valid);
+    const int r0 = part * RPP, nv = rows_valid - r0;   // rows of this part that are valid (may be <= 0)
+    // Round 6: 16 LDS reads in flight per batch (a loop-carried read per row
+    // was one LDS round trip per row, twice: ~3 us of a 12 us short-K launch);
+    // same sums in the same order
     float s = 0.f;
-    for (int r = r0; r < r1; ++r) s += bf2f(E[r * ES + col]);
+    for (int rb = 0; rb < RPP; rb += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = bf2f(E[(r0 + rb + u) * ES + col]);
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (rb + u < nv) s += v[u];
+    }
     red[part * BN + col] = s;
     __syncthreads();
     float tot = 0.f;
@@ -237,7 +248,14 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
     for (int q = 0; q < PARTS; ++q) tot += red[q * BN + col];
     const float mean = tot / (float)rows_valid;
     float m2 = 0.f;
-    for (int r = r0; r < r1; ++r) { float d = bf2f(E[r * ES + col]) - mean; m2 += d * d; }
+    for (int rb = 0; rb < RPP; rb += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = bf2f(E[(r0 + rb + u) * ES + col]);
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (rb + u < nv) { float d = v[u] - mean; m2 += d * d; }
+    }
     __syncthreads();
     red[part * BN + col] = m2;
     __syncthreads();
@@ -252,8 +270,17 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
 
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
   constexpr int CPR = BN / 8;
-  for (int e = tid; e < BM * CPR; e += NT) {
+  constexpr int NIT = BM * CPR / NT;
+  static_assert(BM * CPR % NT == 0, "whole store iterations");
+  // Round 6: the destinations (and, accumulating, the old values) of every
+  // iteration first, then the adds and stores: a load -> store per iteration
+  // was one memory round trip each
+  bf16_t* dsts[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = it * NT + tid;
     int row = e / CPR, cc = (e - row * CPR) * 8;
+    dsts[it] = nullptr;
     if (row >= rows_valid) continue;
     int gj = n0 + cc;
     if (gj >= p.ncol) continue;
@@ -275,16 +302,27 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void gemm_fwd_v2_kernel(VuGemmFw
         dst = out + (((int64_t)n * p.oH + oy) * p.oW + ox) * p.out_stride + p.out_coff + co;
       }
     }
+    dsts[it] = dst;
+  }
+  Vec8<bf16_t> old[NIT];
+  if (p.accumulate) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it)
+      if (dsts[it]) old[it].load(dsts[it]);
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    if (!dsts[it]) continue;
+    const int e = it * NT + tid;
+    const int row = e / CPR, cc = (e - row * CPR) * 8;
     Vec8<bf16_t> v;
     v.v = *reinterpret_cast<const u32x4*>(E + row * ES + cc);
     if (p.accumulate) {
-      Vec8<bf16_t> o;
-      o.load(dst);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) o.set(q, o.get(q) + v.get(q));
-      o.store(dst);
+      for (int q = 0; q < 8; ++q) old[it].set(q, old[it].get(q) + v.get(q));
+      old[it].store(dsts[it]);
     } else {
-      v.store(dst);
+      v.store(dsts[it]);
     }
   }
 }

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void latent_sums_kernel(const LatentJobs jobs,
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
     float t = 0.f;
-    for (int q = 0; q < rows; ++q) t += sh[q * C + c];
+    t = lds_sum(sh + c, rows, C);
     J.part[((int64_t)n * LAT_SPLITS + sp) * C + c] = t;
   }
 }

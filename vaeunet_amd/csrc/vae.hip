@@ -176,7 +176,7 @@ __global__ void sample_sum_partial(const T* x, int64_t xs, int HW, int C, int pe
   __syncthreads();
   for (int cc = threadIdx.x; cc < C; cc += 256) {
     float t = 0.f;
-    for (int q = 0; q < R; ++q) t += sh[q * C + cc];
+    t = lds_sum(sh + cc, R, C);
     part[((int64_t)n * gridDim.y + sidx) * C + cc] = t;
   }
 }

@@ -292,7 +292,7 @@ __global__ __launch_bounds__(256) void zbias_rs_kernel(const ZbJobs jobs, int nj
   for (int q = tid; q < ZB_NS * C; q += 256) {
     const int k = q / C, c = q - (q / C) * C;
     float t = 0.f;
-    for (int r = 0; r < slots; ++r) t += sh[(k * slots + r) * C + c];
+    t = lds_sum(sh + (k * slots) * C + c, slots, C);
     J.rs[(((int64_t)n * nch + chunk) * ZB_NS + k) * C + c] = t;
   }
 }
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_zrs_kernel(const T* dz_in, i
   for (int q = tid; q < ZB_NS * C; q += 256) {
     const int k = q / C, c = q - (q / C) * C;
     float t = 0.f;
-    for (int r = 0; r < slots; ++r) t += sh[(k * slots + r) * C + c];
+    t = lds_sum(sh + (k * slots) * C + c, slots, C);
     rs[(((int64_t)n * nch + chunk) * ZB_NS + k) * C + c] = t;
   }
 }
