@@ -269,6 +269,12 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     two-launch path (stage 1 + stage 2).  Same fp64 combine up to the
  *     summation order. */
 #define VU_TUNE_BN_STATS1 35
+/*   VU_TUNE_V5_GRP: 1 = the persistent short-K 1x1 / ConvT GEMM walks its
+ *     tiles in 4 x 8 blocks per 32 consecutive tiles (one XCD's share of a
+ *     round) when the tile grid divides that way, 0 (default) = row-major
+ *     (the grouping measured 5-8 % slower on the up1 / up2 ConvT GEMMs:
+ *     per XCD, sharing A across 16 column tiles beats the smaller set). */
+#define VU_TUNE_V5_GRP 36
 int vu_gemm_set_tuning(int key, int value);
 /* Bit mask of the experiment modes currently non-zero (bit 0 V6_XM, 1 V7_XM,
  * 2 FP8_XM): 0 in production.  bench.py refuses to report while it is not. */

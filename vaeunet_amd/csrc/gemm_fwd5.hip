@@ -53,8 +53,25 @@ VU_DEV float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 struct Pix { int n, h, w; bool ok; };
 
+// Tile t of the walk -> (row tile, column tile).  grp (VU_TUNE_V5_GRP, round
+// 6): consecutive runs of 32 tiles -- the tiles one XCD's 32 CUs hold at a
+// time -- cover a 4 x 8 block of the tile grid instead of 2 x 16, when the
+// grid divides that way (per XCD: A of 4 row tiles + B of 8 column tiles
+// instead of 2 + 16, 4 instead of 5 MB at K = 1024).
+VU_DEV void v5_tile(int t, int ntiles, int grp, int& mt, int& nt) {
+  if (grp) {
+    const int g = t >> 5, i = t & 31, ngc = ntiles >> 3;
+    const int gr = g / ngc;
+    mt = gr * 4 + (i >> 3);
+    nt = (g - gr * ngc) * 8 + (i & 7);
+  } else {
+    mt = t / ntiles;
+    nt = t - mt * ntiles;
+  }
+}
+
 template <int BN, bool STATS, bool ACC, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
-__global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
+__global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp) {
   constexpr int WNC = BN / WN;          // columns per wave: 64 or 32
   constexpr int TM = BM / WM / 16;      // 4 pixel fragments per wave
   constexpr int TN = WNC / 16;          // 4 or 2 column fragments per wave
@@ -107,8 +124,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
     const int tap = k0 / g.C;
     const int cbase = k0 - tap * g.C;
     if (sg_kt == 0) {
-      const int mt = sg_t / ntiles;
-      const int n0 = (sg_t - mt * ntiles) * BN;
+      int mt, ntl;
+      v5_tile(sg_t, ntiles, grp, mt, ntl);
+      const int n0 = ntl * BN;
 #pragma unroll
       for (int i = 0; i < LA; ++i) {
         const int m = mt * BM + ((i * NT + tid) >> 3);
@@ -196,8 +214,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const bool last = ckt == nk - 1;
-    const int mt = ct / ntiles;
-    const int m0 = mt * BM, n0 = (ct - mt * ntiles) * BN;
+    int mt, ntl;
+    v5_tile(ct, ntiles, grp, mt, ntl);
+    const int m0 = mt * BM, n0 = ntl * BN;
     const int col0 = n0 + wn * WNC + 4 * GS * gq;
     if (last) {
 #pragma unroll
@@ -321,17 +340,20 @@ int cu_count5() {
 }
 
 int g_v5 = 1;  // VU_TUNE_V5: 0 off, 1 on, k >= 2 on with the grid capped at k (tests)
+int g_v5_grp = 0;  // VU_TUNE_V5_GRP
 
 template <int BN, bool STATS, bool ACC>
 int launch5(const VuGemmFwd& p, hipStream_t st) {
   const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
-  const int64_t T = (M / BM) * (p.ncol / BN);
+  const int64_t mtiles = M / BM, ntiles = p.ncol / BN;
+  const int64_t T = mtiles * ntiles;
   int64_t grid = T < cu_count5() ? T : cu_count5();
   if (g_v5 >= 2 && grid > g_v5) grid = g_v5;
+  const int grp = g_v5_grp && ntiles >= 8 && ntiles % 8 == 0 && mtiles % 4 == 0 && T % 32 == 0 ? 1 : 0;
   if (p.relu)
-    hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC, true>), dim3((unsigned)grid), dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC, true>), dim3((unsigned)grid), dim3(NT), 0, st, p, grp);
   else
-    hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC>), dim3((unsigned)grid), dim3(NT), 0, st, p);
+    hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC>), dim3((unsigned)grid), dim3(NT), 0, st, p, grp);
   return (int)hipGetLastError();
 }
 
@@ -371,6 +393,10 @@ int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st) {
 int gemm_fwd_v5_tune(int key, int value) {
   if (key == VU_TUNE_V5) {
     g_v5 = value < 0 ? 0 : value;
+    return 0;
+  }
+  if (key == VU_TUNE_V5_GRP) {
+    g_v5_grp = value ? 1 : 0;
     return 0;
   }
   return -1;
