@@ -275,6 +275,13 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     (the grouping measured 5-8 % slower on the up1 / up2 ConvT GEMMs:
  *     per XCD, sharing A across 16 column tiles beats the smaller set). */
 #define VU_TUNE_V5_GRP 36
+/*   VU_TUNE_V5_WIDE: 1 = the persistent short-K 1x1 / ConvT GEMM takes
+ *     256 x 256 output tiles on 32-wide K steps (half the operand bytes per
+ *     MFMA of the 256 x 128 tiles, the same 96 KB in flight) for problems with
+ *     a full round of such tiles and no accumulate; 0 (default) = 256 x 128
+ *     (the wide tiles measured 3-15 % slower per shape: each step fetches
+ *     half cache lines of every operand row). */
+#define VU_TUNE_V5_WIDE 37
 int vu_gemm_set_tuning(int key, int value);
 /* Bit mask of the experiment modes currently non-zero (bit 0 V6_XM, 1 V7_XM,
  * 2 FP8_XM): 0 in production.  bench.py refuses to report while it is not. */

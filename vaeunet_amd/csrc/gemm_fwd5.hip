@@ -39,6 +39,15 @@ VU_DEV int fb(int row) { return (row & 3) | (((row >> (GS == 4 ? 4 : 3)) & 1) <<
 template <int GS>
 VU_DEV int swz_b(int row, int chunk) { return row * KB + ((chunk ^ fb<GS>(row)) << 4); }
 
+// 256-column tiles (round 6, VU_TUNE_V5_WIDE): 32-wide K steps, 64-byte LDS
+// rows.  ds_read_b128 serves 16-lane groups {0-3,12-15,20-27}, ...; a lane
+// reads row r16 = lane & 15 (+ a fragment base) at chunk lane >> 4, so the
+// physical chunk is the logical one XOR 2 * bit 2 of the row for A and XOR
+// 2 * bit 5 for B (whose fragment rows step by 32 every 4 lanes): every
+// group then hits 16 distinct 16-byte slots of a 256-byte bank window.
+VU_DEV int swz_aw(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
+VU_DEV int swz_bw(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 5) & 1) << 1)) << 4); }
+
 template <int N>
 VU_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
@@ -72,21 +81,29 @@ VU_DEV void v5_tile(int t, int ntiles, int grp, int& mt, int& nt) {
 
 template <int BN, bool STATS, bool ACC, bool RELU = false>  // RELU: epilogue ReLU (VuGemmFwd.relu)
 __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp) {
-  constexpr int WNC = BN / WN;          // columns per wave: 64 or 32
+  constexpr bool WD = BN == 256;        // round 6: 256 x 256 tiles on 32-wide K steps
+  static_assert(!(WD && ACC), "the wide tiles have no accumulate variant (registers)");
+  constexpr int KBY = WD ? 64 : KB;     // bytes of K per LDS row per step
+  constexpr int KST = KBY / 2;          // K elements per step
+  constexpr int CH = KBY / 16;          // 16-byte chunks per row
+  constexpr int RS = WD ? 2 : 3;        // log2(CH)
+  constexpr int NSW = WD ? 4 : NS;      // ring slots: NSW - 1 steps in flight (96 KB either way)
+  constexpr int KK = KST / 32;          // MFMA k-slabs per step
+  constexpr int WNC = BN / WN;          // columns per wave: 128, 64 or 32
   constexpr int TM = BM / WM / 16;      // 4 pixel fragments per wave
-  constexpr int TN = WNC / 16;          // 4 or 2 column fragments per wave
+  constexpr int TN = WNC / 16;          // 8, 4 or 2 column fragments per wave
   constexpr int GS = TN;                // a lane owns 4*GS consecutive columns
   constexpr int CPL = GS / 2;           // 16-byte pieces per lane and pixel
-  constexpr int LA = BM * 8 / NT, LB = BN * 8 / NT, NL = LA + LB;
+  constexpr int LA = BM * CH / NT, LB = BN * CH / NT, NL = LA + LB;
   constexpr int NST = TM * CPL + (STATS ? 2 * TN : 0);  // vector stores per epilogue
-  constexpr int STAGE = (BM + BN) * KB;
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  constexpr int STAGE = (BM + BN) * KBY;
+  __shared__ __attribute__((aligned(16))) char smem[NSW * STAGE];
 
   const VuGather& g = p.a;
   const int M = g.N * g.H * g.W;  // < 2^31 (host check)
   const int HW = g.H * g.W;
   const int K = g.R * g.S * g.C;
-  const int nk = (K + 63) / 64;
+  const int nk = (K + KST - 1) / KST;
   const int ntiles = p.ncol / BN;
   const int T = (M / BM) * ntiles;
   const int G = gridDim.x;
@@ -98,7 +115,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid - (wid / WN) * WN;
   const int gq = lane >> 4, r16 = lane & 15;
-  const int pchunk = lane & 7;
+  const int pchunk = lane & (CH - 1);
   // pixel -> (n, h, w) and ConvT column -> (tap, channel) decodes: once per
   // tile per row, by multiply-shift (runtime integer divisions were ~1/3 of
   // the kernel's VALU instructions)
@@ -111,16 +128,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
   // k-steps its row pointers are resolved once and then advance by 64
   // channels per step (the per-step gather decode cost more VALU time than
   // the MFMAs of the step).
-  const int lch_a = pchunk ^ ((tid >> 3) & 7);     // row & 7 is the same for all LA rows
+  // row & 7 (row bit 2 for the wide tiles) is the same for all LA rows
+  const int lch_a = WD ? pchunk ^ (((tid >> 4) & 1) << 1) : pchunk ^ ((tid >> 3) & 7);
   int sg_t = lb, sg_kt = 0, seg_step = 0, seg_rem = 0;
   const bf16_t* ap[LA];
   const bf16_t* bp[LB];
   int lch_b[LB];
 #pragma unroll
-  for (int i = 0; i < LB; ++i) lch_b[i] = pchunk ^ fb<GS>((i * NT + tid) >> 3);
+  for (int i = 0; i < LB; ++i)
+    lch_b[i] = WD ? pchunk ^ ((((i * NT + tid) >> 7) & 1) << 1) : pchunk ^ fb<GS>((i * NT + tid) >> 3);
   Pix pa[LA];
   auto stage = [&](int slot) {
-    const int k0 = sg_kt * 64;
+    const int k0 = sg_kt * KST;
     const int tap = k0 / g.C;
     const int cbase = k0 - tap * g.C;
     if (sg_kt == 0) {
@@ -129,7 +148,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
       const int n0 = ntl * BN;
 #pragma unroll
       for (int i = 0; i < LA; ++i) {
-        const int m = mt * BM + ((i * NT + tid) >> 3);
+        const int m = mt * BM + ((i * NT + tid) >> RS);
         pa[i].n = (int)div_hw.div((uint32_t)m);
         const int rem = m - pa[i].n * HW;
         pa[i].h = (int)div_w.div((uint32_t)rem);
@@ -137,7 +156,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
       }
 #pragma unroll
       for (int i = 0; i < LB; ++i)
-        bp[i] = bmat + (int64_t)(n0 + ((i * NT + tid) >> 3)) * p.ldb + lch_b[i] * 8;
+        bp[i] = bmat + (int64_t)(n0 + ((i * NT + tid) >> RS)) * p.ldb + lch_b[i] * 8;
     }
     if (sg_kt == 0 || cbase == 0 || cbase == g.cend[0] || (g.nsrc > 2 && cbase == g.cend[1])) {
       const int r = tap / g.S, s = tap - (tap / g.S) * g.S;
@@ -157,8 +176,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
       seg_rem = g.cend[t] - cbase;
     }
     char* A = smem + slot * STAGE;
-    char* B = A + BM * KB;
-    const int off = seg_step * 64;
+    char* B = A + BM * KBY;
+    const int off = seg_step * KST;
     const bool cin = lch_a * 8 < seg_rem - off;  // channel tail of the source
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
@@ -203,10 +222,15 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
 
   int ct = lb, ckt = 0;  // tile / k-step being computed
   stage(0);
-  if (S > 1) stage(1);
+#pragma unroll
+  for (int q = 1; q < NSW - 1; ++q)
+    if (S > q) stage(q);
   for (int s = 0; s < S; ++s) {
     const bool after_epi = s > 0 && ckt == 0;
-    if (s + 1 < S) {
+    // steps issued after s that may stay in flight (and the last epilogue's stores)
+    if (NSW == 4 && s + 2 < S) {
+      if (after_epi) wait_vm<2 * NL + NST>(); else wait_vm<2 * NL>();
+    } else if (s + 1 < S) {
       if (after_epi) wait_vm<NL + NST>(); else wait_vm<NL>();
     } else {
       if (after_epi) wait_vm<NST>(); else wait_vm<0>();
@@ -228,22 +252,24 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
         }
       }
     }
-    if (s + 2 < S) stage((s + 2) % NS);
-    const char* A = smem + (s % NS) * STAGE;
-    const char* B = A + BM * KB;
-    u32x4 af[2][TM], bf[2][TN];
+    if (s + NSW - 1 < S) stage((s + NSW - 1) % NSW);
+    const char* A = smem + (s % NSW) * STAGE;
+    const char* B = A + BM * KBY;
+    u32x4 af[KK][TM], bf[KK][TN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       const int ch = kk * 4 + gq;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[kk][i] = *reinterpret_cast<const u32x4*>(A + swz_a(wm * 64 + 16 * i + r16, ch));
+        af[kk][i] = *reinterpret_cast<const u32x4*>(A + (WD ? swz_aw(wm * 64 + 16 * i + r16, ch)
+                                                             : swz_a(wm * 64 + 16 * i + r16, ch)));
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        bf[kk][j] = *reinterpret_cast<const u32x4*>(B + swz_b<GS>(wn * WNC + wrow(j, r16), ch));
+        bf[kk][j] = *reinterpret_cast<const u32x4*>(B + (WD ? swz_bw(wn * WNC + wrow(j, r16), ch)
+                                                             : swz_b<GS>(wn * WNC + wrow(j, r16), ch)));
     }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < KK; ++kk) {
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -274,9 +300,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
     if constexpr (RELU)
 #pragma unroll
       for (int i = 0; i < TM; ++i) epi_relu(acc[i]);
-    // the old values were loaded before stage(s + 2): only that stage may stay in flight
+    // the old values were loaded before stage(s + NSW - 1): only that stage may stay in flight
     if (ACC) {
-      if (s + 2 < S) wait_vm<NL>(); else wait_vm<0>();
+      if (s + NSW - 1 < S) wait_vm<NL>(); else wait_vm<0>();
     }
     if (STATS) {
       const int srow = (m0 >> 6) + wm;  // 64-row statistics tile
@@ -360,8 +386,26 @@ int launch5(const VuGemmFwd& p, hipStream_t st) {
 template <int BN>
 int launch_bn(const VuGemmFwd& p, hipStream_t st) {
   const bool stats = p.stat_sum != nullptr, acc = p.accumulate != 0;
-  if (stats) return acc ? launch5<BN, true, true>(p, st) : launch5<BN, true, false>(p, st);
-  return acc ? launch5<BN, false, true>(p, st) : launch5<BN, false, false>(p, st);
+  if constexpr (BN == 256) {
+    if (acc) return (int)hipErrorInvalidValue;
+    return stats ? launch5<BN, true, false>(p, st) : launch5<BN, false, false>(p, st);
+  } else {
+    if (stats) return acc ? launch5<BN, true, true>(p, st) : launch5<BN, true, false>(p, st);
+    return acc ? launch5<BN, false, true>(p, st) : launch5<BN, false, false>(p, st);
+  }
+}
+
+int g_v5_wide = 0;  // VU_TUNE_V5_WIDE
+
+// the 256 x 256 tiles: a whole round of tiles (one per CU), no accumulate,
+// ConvTranspose outputs in 32-channel runs, at least two 32-wide K steps
+bool wide_ok(const VuGemmFwd& p) {
+  if (!g_v5_wide || p.accumulate || p.ncol % 256 != 0) return false;
+  if (p.out_mode == 1 && p.cout % 32 != 0) return false;
+  const int64_t M = (int64_t)p.a.N * p.a.H * p.a.W;
+  const int K = p.a.R * p.a.S * p.a.C;
+  if (K < 64) return false;
+  return (M / BM) * (p.ncol / 256) >= cu_count5();
 }
 
 }  // namespace
@@ -387,12 +431,17 @@ int gemm_fwd_v5_bm(const VuGemmFwd& p, int dtype) {
 
 int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st) {
   if (p.ncol == 64) return launch_bn<64>(p, st);
+  if (wide_ok(p)) return launch_bn<256>(p, st);
   return launch_bn<128>(p, st);
 }
 
 int gemm_fwd_v5_tune(int key, int value) {
   if (key == VU_TUNE_V5) {
     g_v5 = value < 0 ? 0 : value;
+    return 0;
+  }
+  if (key == VU_TUNE_V5_WIDE) {
+    g_v5_wide = value ? 1 : 0;
     return 0;
   }
   if (key == VU_TUNE_V5_GRP) {
