@@ -282,10 +282,6 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     (the wide tiles measured 3-15 % slower per shape: each step fetches
  *     half cache lines of every operand row). */
 #define VU_TUNE_V5_WIDE 37
-/*   VU_TUNE_V5_NT: cache policy of the persistent short-K GEMM's LDS fills:
- *     bit 0 = A (activations) streaming / non-temporal, bit 1 = B (weights);
- *     0 (default) = both the default policy. */
-#define VU_TUNE_V5_NT 38
 int vu_gemm_set_tuning(int key, int value);
 /* Bit mask of the experiment modes currently non-zero (bit 0 V6_XM, 1 V7_XM,
  * 2 FP8_XM): 0 in production.  bench.py refuses to report while it is not. */

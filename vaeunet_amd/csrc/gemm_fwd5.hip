@@ -68,7 +68,7 @@ struct Pix { int n, h, w; bool ok; };
 // grid divides that way (per XCD: A of 4 row tiles + B of 8 column tiles
 // instead of 2 + 16, 4 instead of 5 MB at K = 1024).
 VU_DEV void v5_tile(int t, int ntiles, int grp, int& mt, int& nt) {
-  if (grp & 1) {
+  if (grp) {
     const int g = t >> 5, i = t & 31, ngc = ntiles >> 3;
     const int gr = g / ngc;
     mt = gr * 4 + (i >> 3);
@@ -182,18 +182,12 @@ __global__ __launch_bounds__(NT, 1) void gemm_fwd_v5_kernel(VuGemmFwd p, int grp
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const void* gp = (ap[i] != nullptr && cin) ? (const void*)(ap[i] + off) : zp;
-      if (grp & 2)   // VU_TUNE_V5_NT bit 0: A fills with the streaming (nt) policy
-        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 2);
-      else
-        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(A + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       const void* gp = k0 + lch_b[i] * 8 < K ? (const void*)(bp[i] + k0) : zp;
-      if (grp & 4)   // VU_TUNE_V5_NT bit 1: B fills with the streaming (nt) policy
-        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 2);
-      else
-        __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(gp, (lds_void*)(B + (i * NT + wid * 64) * 16), 16, 0, 0);
     }
     ++seg_step;
     if (++sg_kt == nk) {
@@ -373,7 +367,6 @@ int cu_count5() {
 
 int g_v5 = 1;  // VU_TUNE_V5: 0 off, 1 on, k >= 2 on with the grid capped at k (tests)
 int g_v5_grp = 0;  // VU_TUNE_V5_GRP
-int g_v5_nt = 0;   // VU_TUNE_V5_NT
 
 template <int BN, bool STATS, bool ACC>
 int launch5(const VuGemmFwd& p, hipStream_t st) {
@@ -382,9 +375,7 @@ int launch5(const VuGemmFwd& p, hipStream_t st) {
   const int64_t T = mtiles * ntiles;
   int64_t grid = T < cu_count5() ? T : cu_count5();
   if (g_v5 >= 2 && grid > g_v5) grid = g_v5;
-  // kernel flags: bit 0 the 4 x 8 tile groups, bits 1-2 the fill policies
-  const int grp = (g_v5_grp && ntiles >= 8 && ntiles % 8 == 0 && mtiles % 4 == 0 && T % 32 == 0 ? 1 : 0) |
-                  (g_v5_nt << 1);
+  const int grp = g_v5_grp && ntiles >= 8 && ntiles % 8 == 0 && mtiles % 4 == 0 && T % 32 == 0 ? 1 : 0;
   if (p.relu)
     hipLaunchKernelGGL((gemm_fwd_v5_kernel<BN, STATS, ACC, true>), dim3((unsigned)grid), dim3(NT), 0, st, p, grp);
   else
@@ -447,11 +438,6 @@ int gemm_fwd_v5_launch(const VuGemmFwd& p, hipStream_t st) {
 int gemm_fwd_v5_tune(int key, int value) {
   if (key == VU_TUNE_V5) {
     g_v5 = value < 0 ? 0 : value;
-    return 0;
-  }
-  if (key == VU_TUNE_V5_NT) {
-    if (value < 0 || value > 3) return (int)hipErrorInvalidValue;
-    g_v5_nt = value;
     return 0;
   }
   if (key == VU_TUNE_V5_WIDE) {

@@ -49,12 +49,16 @@ class _BceDice(torch.autograd.Function):
         ctx.save_for_backward(x, t, sums)
         ctx.cfg = (smooth, w_bce, w_dice)
         ctx.mark_non_differentiable(parts)
+        # no zero gradient materialised for `parts` (one fill launch less per step)
+        ctx.set_materialize_grads(False)
         return loss, parts
 
     @staticmethod
     def backward(ctx, gout, _gparts):
         x, t, sums = ctx.saved_tensors
         smooth, w_bce, w_dice = ctx.cfg
+        if gout is None:
+            return None, None, None, None, None
         g = gout.float().contiguous()
         grad = torch.empty_like(x)
         call("vu_bce_dice_bwd", ptr(x), ptr(t), x.numel(), ptr(sums), smooth, w_bce, w_dice,
