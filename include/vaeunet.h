@@ -211,7 +211,9 @@ int vu_slab_reduce(const float* slab, int splits, int ni, int nj, int C,
  *     VU_TUNE_FP8_GRID caps the grid) */
 #define VU_TUNE_FP8_PP 21
 /*   VU_TUNE_ATTN: 1 (default) batched attention-gate kernels (U pixel rows /
- *     vectors of loads in flight per lane), 0 = one row per iteration */
+ *     vectors of loads in flight per lane), 0 = one row per iteration,
+ *     2 = as 1 with the psi backward that emits the BatchNorm partials on
+ *     two rows per lane (fewer VGPRs, one more wave per SIMD) */
 #define VU_TUNE_ATTN 22
 /*   VU_TUNE_FP8_C64: 1 (default) 64 -> 64 fp8 convs on the resident-weight
  *     tile-stream kernel (statistics row tile 64), 0 = the step-loop kernel */

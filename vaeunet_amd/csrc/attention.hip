@@ -823,10 +823,16 @@ extern "C" int vu_attn_psi_bwd_bnb(const void* ug, const void* ux, int64_t P, in
   const int nblk = (int)vu_attn_psi_bwd_blocks(P);
   if (nblk == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  // VU_TUNE_ATTN 2: two pixel rows per lane in flight instead of four (209 -> 162 VGPRs, occupancy 2 -> 3)
   DISPATCH_T(dtype, {
-    hipLaunchKernelGGL((psi_bwd_u_kernel<T, 4, true>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux, P,
-                       F, sg, tg, sx, tx, wpsi, dq, (T*)ds, workspace, mean_g, invstd_g, mean_x, invstd_x, bnb_g,
-                       bnb_x);
+    if (g_attn == 2)
+      hipLaunchKernelGGL((psi_bwd_u_kernel<T, 2, true>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux,
+                         P, F, sg, tg, sx, tx, wpsi, dq, (T*)ds, workspace, mean_g, invstd_g, mean_x, invstd_x,
+                         bnb_g, bnb_x);
+    else
+      hipLaunchKernelGGL((psi_bwd_u_kernel<T, 4, true>), dim3(nblk), dim3(256), 0, st, (const T*)ug, (const T*)ux,
+                         P, F, sg, tg, sx, tx, wpsi, dq, (T*)ds, workspace, mean_g, invstd_g, mean_x, invstd_x,
+                         bnb_g, bnb_x);
   })
   hipLaunchKernelGGL(part_final, dim3((F + 1 + 31) / 32), dim3(COLSUM_THREADS), 0, st, workspace, nblk, F + 1, dwpsi,
                      F, dbpsi, accumulate);
